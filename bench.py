@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""Benchmark of the batched HoverAviary DYN path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E]
+
+One "step" = one env.step() of every env (HoverAviary, cf2x, Physics.DYN, ActionType.RPM,
+240 Hz physics / 30 Hz control -> 8 substeps) on synthetic uniform [-1, 1] actions that are
+resident in HBM before the timed region.  Unit of work: one drone advanced one 1/240 s
+substep (drone*dt).  value = drone*dt of all ranks / max-over-ranks wall time of K steps.
+
+Multi-GPU: one process per GPU (torchrun); each rank owns E envs (weak scaling), there is no
+collective inside the timed loop.  The RCCL all-gather of the observation batch to a learner
+on rank 0 (config 5) is timed separately and reported under "gather".
+
+Extra JSON fields: "roofline" (step kernel, HIP events on the launch stream), "cpu_baseline"
+(the oracle, rank 0 at N=1), "sweep" (large-N roofline), "kernel_us".
+"""
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def alg_bytes_per_drone_step(act="rpm", real_bytes=8):
+    """SURVEY.md §8(d) algorithmic bytes per drone per ctrl step (obs materialised), with the
+    state in the compute precision ("fp32; double for fp64"):
+      read  state 13*r + action 4A + action history 14*4A
+      write state 13*r + last rpm 4*r + obs (12+15A)*4 + reward/terminated/truncated 6
+    fp32 RPM: 52+16+224+52+16+288+6 = 654 B (81.75 B per drone*dt), as SURVEY quotes;
+    fp64 RPM: 104+16+224+104+32+288+6 = 774 B (96.75 B per drone*dt)."""
+    A = 4 if act == "rpm" else 1
+    return 13 * real_bytes + 4 * A + 14 * 4 * A + 13 * real_bytes + 4 * real_bytes + (12 + 15 * A) * 4 + 6
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_info():
+    model = platform.processor() or ""
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name"):
+                model = line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return model, os.cpu_count()
+
+
+def cpu_baseline(seconds=10.0, act="rpm"):
+    """Reference-shaped numpy oracle (one env object, per-drone Python loop, 8 substeps per
+    step) on one core: the stand-in for the reference's own env.step()."""
+    from oracle.ref_aviary import RefAviary
+    A = 4 if act == "rpm" else 1
+    rng = np.random.default_rng(0)
+    env = RefAviary(act=act, task="hover")
+    env.reset()
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        a = rng.uniform(-1, 1, (1, A)).astype(np.float32)
+        _, _, te, tr, _ = env.step(a)
+        if te or tr:
+            env.reset()
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    model, ncpu = cpu_info()
+    return {"value": steps * env.PYB_STEPS_PER_CTRL / el, "unit": "drone*dt/s", "cores": 1, "kind": "port",
+            "sample": f"{steps} HoverAviary env.step() calls (cf2x, DYN, RPM, U[-1,1] actions, auto-reset) "
+                      f"in {el:.1f} s on 1 core of '{model}' ({ncpu} host CPUs); numpy fp64 restatement of "
+                      "BaseAviary.step without pybullet call overhead (flatters the reference)"}
+
+
+def time_steps(sim, pool, steps, warmup):
+    """Run warmup + timed steps; returns (wall seconds, mean kernel us)."""
+    P = pool.shape[0]
+    for k in range(warmup):
+        sim.step(pool[k % P])
+    torch.cuda.synchronize(sim.device)
+    stream = torch.cuda.current_stream(sim.device)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if torch.distributed.is_initialized():
+        torch.distributed.barrier()
+    torch.cuda.synchronize(sim.device)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        ev[k][0].record(stream)
+        sim.step(pool[(warmup + k) % P])
+        ev[k][1].record(stream)
+    torch.cuda.synchronize(sim.device)
+    wall = time.perf_counter() - t0
+    if torch.distributed.is_initialized():
+        torch.distributed.barrier()
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    return wall, 1000.0 * float(np.mean(kern_ms))
+
+
+def make_pool(E, A, device, seed, pool=64):
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    return (torch.rand((pool, E, 1, A), generator=g, device=device) * 2 - 1).contiguous()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--act", default="rpm", choices=["rpm", "one_d_rpm"])
+    ap.add_argument("--precision", default="f64", choices=["f32", "f64"],
+                    help="f64 (default) is the parity-gated path (<=1e-10 vs the fp64 oracle)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        torch.distributed.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    device = torch.device(f"cuda:{local_rank}")
+    torch.cuda.set_device(device)
+
+    from gym_pybullet_drones_routing_amd.enums import ActionType
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+
+    E = args.envs
+    A = 4 if args.act == "rpm" else 1
+    sim = BatchedAviarySim(n_envs=E, task="hover", act=ActionType(args.act), precision=args.precision,
+                           autoreset=True, device=device)
+    nsub = sim.pyb_steps_per_ctrl
+    pool = make_pool(E, A, device, seed=1000 + rank)
+    wall, kern_us = time_steps(sim, pool, args.steps, args.warmup)
+    if world > 1:
+        t = torch.tensor([wall], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        wall = float(t.item())
+    drone_dt = world * E * nsub * args.steps
+    value = drone_dt / wall
+    ms_per_step = 1000.0 * wall / args.steps
+    rbytes = 8 if args.precision == "f64" else 4
+    alg = alg_bytes_per_drone_step(args.act, rbytes) * E
+    achieved = alg / (kern_us * 1e-6) / 1e9
+    result = {
+        "metric": "env-steps/sec (drone·dt) at 4096 envs, 1/2/4/8 GPU; state L2 vs PyBullet",
+        "value": value, "unit": "drone*dt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32" if args.precision == "f32" else "f64", "data": "synthetic",
+        "config": {"workload": f"{E} HoverAviary envs per GPU (cf2x, Physics.DYN, ActionType.{args.act.upper()}, "
+                               f"240/30 Hz = {nsub} substeps/step, U[-1,1] actions, SB3 auto-reset)",
+                   "n_envs_per_gpu": E, "global_envs": E * world, "drones_per_env": 1,
+                   "parallelism": f"env-sharded x{world} (no collective in the step loop)"},
+        "kernel_us": kern_us,
+        "ctrl_steps_per_s": world * E * args.steps / wall,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "kernel": "gpd::step_kernel<%s,%d,false>" % ("double" if rbytes == 8 else "float", A),
+                     "alg_bytes_per_launch": alg},
+    }
+
+    if world > 1:
+        # config 5: RCCL all-gather of the observation batch (+ reward / done) to the learner
+        obs_all = torch.empty((world,) + tuple(sim.obs.shape), dtype=sim.obs.dtype, device=device)
+        rew_all = torch.empty((world, E), dtype=torch.float32, device=device)
+        torch.distributed.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        G = max(10, args.steps // 3)
+        for k in range(G):
+            sim.step(pool[k % pool.shape[0]])
+            torch.distributed.all_gather_into_tensor(obs_all, sim.obs)
+            torch.distributed.all_gather_into_tensor(rew_all, sim.reward)
+        torch.cuda.synchronize(device)
+        gw = torch.tensor([time.perf_counter() - t0], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(gw, op=torch.distributed.ReduceOp.MAX)
+        gw = float(gw.item())
+        result["gather"] = {"ms_per_step": 1000 * gw / G, "value": world * E * nsub * G / gw,
+                            "bytes_per_step": int(obs_all.numel() * 4 + rew_all.numel() * 4)}
+
+    if rank == 0 and world == 1 and not args.no_sweep:
+        sweep = []
+        for e_large in (65536, 1 << 20, 1 << 22):
+            s2 = BatchedAviarySim(n_envs=e_large, task="hover", act=ActionType(args.act),
+                                  precision=args.precision, autoreset=True, device=device)
+            p2 = make_pool(e_large, A, device, seed=7, pool=4)
+            w2, k2 = time_steps(s2, p2, 20, 3)
+            ach = alg_bytes_per_drone_step(args.act, rbytes) * e_large / (k2 * 1e-6) / 1e9
+            sweep.append({"n_envs": e_large, "kernel_us": k2, "ms_per_step": 1000 * w2 / 20,
+                          "value": e_large * nsub * 20 / w2, "achieved_GBps": ach, "frac": ach / HBM_PEAK_GBPS})
+            s2.close()
+            del p2
+            torch.cuda.empty_cache()
+        result["sweep"] = sweep
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.act)
+        result["speedup_vs_cpu_baseline"] = value / result["cpu_baseline"]["value"]
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    sim.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

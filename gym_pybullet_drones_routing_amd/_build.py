@@ -1,0 +1,51 @@
+"""Build the in-tree HIP library ``libgpd.so`` (gfx950) with hipcc.
+
+The library must live in-tree so that it travels to the GPU box with the repository snapshot.
+"""
+import os
+import pathlib
+import shutil
+import subprocess
+
+PKG_DIR = pathlib.Path(__file__).resolve().parent
+CSRC = PKG_DIR / "csrc"
+INCLUDE = PKG_DIR.parent / "include"
+LIB_PATH = PKG_DIR / "libgpd.so"
+SOURCES = [CSRC / "gpd.hip", CSRC / "gpd_kernels.h", CSRC / "gpd_device.h", INCLUDE / "gpd.h"]
+ARCH = os.environ.get("GPD_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc():
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: cannot build the gfx950 HIP library")
+
+
+def needs_build():
+    if not LIB_PATH.exists():
+        return True
+    t = LIB_PATH.stat().st_mtime
+    return any(src.stat().st_mtime > t for src in SOURCES)
+
+
+def build(force=False, verbose=False):
+    """Compile csrc/gpd.hip into libgpd.so for gfx950 (code object v5, loadable by the
+    HIP runtime that ships inside the torch wheel)."""
+    if not force and not needs_build():
+        return LIB_PATH
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-mcode-object-version=5", "-O3", "-std=c++17",
+           "-fPIC", "-shared", "-Wall", "-Wno-unused-result", f"-I{INCLUDE}", "-o", str(tmp),
+           str(CSRC / "gpd.hip")]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + " ".join(cmd) + "\n" + res.stdout + res.stderr)
+    if verbose and (res.stdout or res.stderr):
+        print(res.stdout + res.stderr)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

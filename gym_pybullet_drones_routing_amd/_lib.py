@@ -1,0 +1,123 @@
+"""ctypes binding of the C ABI declared in ``include/gpd.h``.
+
+This is the same binding a maintainer of the reference would add.
+There is deliberately NO CPU fallback: if ``libgpd.so`` is missing or fails to load,
+every entry point raises ``GpdLibraryError``.
+"""
+import ctypes
+import pathlib
+
+# The HIP runtime must be the one torch already loaded (same SONAME libamdhip64.so.7):
+# import torch first so that libgpd.so binds to it instead of a second runtime copy.
+import torch  # noqa: F401  (imported for its side effect on the dynamic linker)
+
+LIB_PATH = pathlib.Path(__file__).resolve().parent / "libgpd.so"
+
+GPD_OK = 0
+GPD_EINVAL = -1
+GPD_EHIP = -2
+GPD_ENOMEM = -3
+GPD_EUNSUPPORTED = -4
+
+GPD_MODEL_CF2X, GPD_MODEL_CF2P, GPD_MODEL_RACE = 0, 1, 2
+GPD_ACT_RPM, GPD_ACT_ONE_D_RPM = 0, 1
+GPD_TASK_NONE, GPD_TASK_HOVER, GPD_TASK_MULTIHOVER = 0, 1, 2
+GPD_F_GND, GPD_F_DRAG, GPD_F_DW, GPD_F_GEOM_WRENCH = 1, 2, 4, 8
+GPD_F32, GPD_F64 = 0, 1
+
+# Every symbol include/gpd.h declares (checked by tests/test_lib_symbols.py).
+EXPORTED = ("gpd_abi_version", "gpd_last_error", "gpd_default_params", "gpd_create", "gpd_destroy",
+            "gpd_get_constants", "gpd_reset", "gpd_step", "gpd_integrate", "gpd_get_state20",
+            "gpd_get_raw_state", "gpd_set_raw_state", "gpd_get_step_counters",
+            "gpd_set_step_counters", "gpd_state_bytes", "gpd_save_state", "gpd_load_state")
+
+
+class GpdLibraryError(RuntimeError):
+    pass
+
+
+class GpdError(RuntimeError):
+    def __init__(self, fn, code, msg):
+        super().__init__(f"{fn} failed with code {code}: {msg}")
+        self.code = code
+
+
+class DroneParams(ctypes.Structure):
+    _fields_ = [("model", ctypes.c_int)] + [(n, ctypes.c_double) for n in (
+        "m", "arm", "thrust2weight", "ixx", "iyy", "izz", "kf", "km",
+        "collision_h", "collision_r", "collision_z_offset", "max_speed_kmh",
+        "gnd_eff_coeff", "prop_radius", "drag_coeff_xy", "drag_coeff_z",
+        "dw_coeff_1", "dw_coeff_2", "dw_coeff_3")] + [("prop_pos", (ctypes.c_double * 3) * 4)]
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("n_envs", ctypes.c_int), ("drones_per_env", ctypes.c_int), ("pyb_freq", ctypes.c_int),
+                ("ctrl_freq", ctypes.c_int), ("act_type", ctypes.c_int), ("task", ctypes.c_int),
+                ("physics_flags", ctypes.c_int), ("precision", ctypes.c_int), ("autoreset", ctypes.c_int),
+                ("episode_len_sec", ctypes.c_double),
+                ("init_xyzs_host", ctypes.POINTER(ctypes.c_double)),
+                ("init_rpys_host", ctypes.POINTER(ctypes.c_double))]
+
+
+class Constants(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in (
+        "gravity", "hover_rpm", "max_rpm", "max_thrust", "max_xy_torque", "max_z_torque",
+        "gnd_eff_h_clip", "pyb_timestep", "ctrl_timestep")] + [(n, ctypes.c_int) for n in (
+            "pyb_steps_per_ctrl", "action_buffer_size", "obs_width", "act_width", "n_drones",
+            "trunc_step_counter")]
+
+
+_lib = None
+
+
+def load():
+    """Load libgpd.so (once) and declare the C signatures."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise GpdLibraryError(f"{LIB_PATH} is missing: run `python -m gym_pybullet_drones_routing_amd._build` "
+                              "(or __graft_entry__.build()) to compile the gfx950 HIP library")
+    try:
+        lib = ctypes.CDLL(str(LIB_PATH))
+    except OSError as exc:
+        raise GpdLibraryError(f"cannot load {LIB_PATH}: {exc}") from exc
+    vp, i, ci = ctypes.c_void_p, ctypes.c_int, ctypes.c_int
+    sig = {
+        "gpd_abi_version": (ci, []),
+        "gpd_last_error": (ctypes.c_char_p, []),
+        "gpd_default_params": (ci, [i, ctypes.POINTER(DroneParams)]),
+        "gpd_create": (ci, [ctypes.POINTER(DroneParams), ctypes.POINTER(Config), ctypes.POINTER(vp)]),
+        "gpd_destroy": (ci, [vp]),
+        "gpd_get_constants": (ci, [vp, ctypes.POINTER(Constants)]),
+        "gpd_reset": (ci, [vp, vp, vp, vp]),
+        "gpd_step": (ci, [vp, vp, vp, vp, vp, vp, vp, vp]),
+        "gpd_integrate": (ci, [vp, vp, i, vp, vp]),
+        "gpd_get_state20": (ci, [vp, vp, vp]),
+        "gpd_get_raw_state": (ci, [vp, vp, vp]),
+        "gpd_set_raw_state": (ci, [vp, vp, vp]),
+        "gpd_get_step_counters": (ci, [vp, vp, vp]),
+        "gpd_set_step_counters": (ci, [vp, vp, vp]),
+        "gpd_state_bytes": (ctypes.c_size_t, [vp]),
+        "gpd_save_state": (ci, [vp, vp, vp]),
+        "gpd_load_state": (ci, [vp, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(fn_name, rc):
+    if rc != GPD_OK:
+        raise GpdError(fn_name, rc, _lib.gpd_last_error().decode(errors="replace"))
+    return rc
+
+
+def default_params(model):
+    lib = load()
+    p = DroneParams()
+    check("gpd_default_params", lib.gpd_default_params(model, ctypes.byref(p)))
+    return p

@@ -1,0 +1,532 @@
+// gpd.hip — C ABI (include/gpd.h) of the batched quadrotor DYN path on MI355X (gfx950).
+//
+// Host side: validates the configuration (BaseAviary.__init__ checks, BaseAviary.py:79-80),
+// derives the model constants in double exactly as BaseAviary.py:117-128 does, builds the
+// reset template (INIT_XYZS / INIT_RPYS through the Bullet orientation round trip,
+// BaseAviary.py:194-207, :486-491, :509-519), owns the SoA device state and launches the
+// kernels of gpd_kernels.h on the caller's stream.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gpd.h"
+#include "gpd_kernels.h"
+
+using namespace gpd;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) return fail(GPD_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// ---- host restatements of the Bullet helpers (double), for the reset template only
+void h_quat_to_mat(const double q[4], double m[9]) {
+  const double x = q[0], y = q[1], z = q[2], w = q[3];
+  const double d = x * x + y * y + z * z + w * w, s = 2.0 / d;
+  const double xs = x * s, ys = y * s, zs = z * s;
+  const double wx = w * xs, wy = w * ys, wz = w * zs, xx = x * xs, xy = x * ys, xz = x * zs;
+  const double yy = y * ys, yz = y * zs, zz = z * zs;
+  m[0] = 1.0 - (yy + zz); m[1] = xy - wz; m[2] = xz + wy;
+  m[3] = xy + wz; m[4] = 1.0 - (xx + zz); m[5] = yz - wx;
+  m[6] = xz - wy; m[7] = yz + wx; m[8] = 1.0 - (xx + yy);
+}
+void h_mat_to_quat(const double m[9], double q[4]) {
+  const double tr = m[0] + m[4] + m[8];
+  double t[4];
+  if (tr > 0.0) {
+    double s = std::sqrt(tr + 1.0);
+    t[3] = s * 0.5; s = 0.5 / s;
+    t[0] = (m[7] - m[5]) * s; t[1] = (m[2] - m[6]) * s; t[2] = (m[3] - m[1]) * s;
+  } else {
+    const int i = m[0] < m[4] ? (m[4] < m[8] ? 2 : 1) : (m[0] < m[8] ? 2 : 0);
+    const int j = (i + 1) % 3, k = (i + 2) % 3;
+    double s = std::sqrt(m[i * 4] - m[j * 4] - m[k * 4] + 1.0);
+    t[i] = s * 0.5; s = 0.5 / s;
+    t[3] = (m[k * 3 + j] - m[j * 3 + k]) * s;
+    t[j] = (m[j * 3 + i] + m[i * 3 + j]) * s;
+    t[k] = (m[k * 3 + i] + m[i * 3 + k]) * s;
+  }
+  for (int a = 0; a < 4; ++a) q[a] = t[a];
+}
+void h_roundtrip(const double q[4], double out[4]) {
+  double m[9];
+  h_quat_to_mat(q, m);
+  h_mat_to_quat(m, out);
+}
+void h_euler(const double q[4], double rpy[3]) {
+  const double x = q[0], y = q[1], z = q[2], w = q[3];
+  const double sarg = -2.0 * (x * z - w * y);
+  if (sarg <= -0.99999) {
+    rpy[0] = 0.0; rpy[1] = -0.5 * M_PI; rpy[2] = 2.0 * std::atan2(x, -y);
+  } else if (sarg >= 0.99999) {
+    rpy[0] = 0.0; rpy[1] = 0.5 * M_PI; rpy[2] = 2.0 * std::atan2(-x, y);
+  } else {
+    rpy[1] = std::asin(std::fmin(1.0, std::fmax(-1.0, sarg)));
+    rpy[0] = std::atan2(2.0 * (y * z + w * x), w * w - x * x - y * y + z * z);
+    rpy[2] = std::atan2(2.0 * (x * y + w * z), w * w + x * x - y * y - z * z);
+  }
+}
+void h_quat_from_euler(const double rpy[3], double q[4]) {  // btQuaternion::setEulerZYX
+  const double hy = rpy[2] * 0.5, hp = rpy[1] * 0.5, hr = rpy[0] * 0.5;
+  const double cy = std::cos(hy), sy = std::sin(hy), cp = std::cos(hp), sp = std::sin(hp);
+  const double cr = std::cos(hr), sr = std::sin(hr);
+  q[0] = sr * cp * cy - cr * sp * sy;
+  q[1] = cr * sp * cy + sr * cp * sy;
+  q[2] = cr * cp * sy - sr * sp * cy;
+  q[3] = cr * cp * cy + sr * sp * sy;
+}
+
+}  // namespace
+
+struct gpd_sim {
+  gpd_drone_params P;
+  gpd_config cfg;
+  gpd_constants K;
+  int E, D, N, A, W, nsub, ring_len, prec, tpb;
+  long long npad;
+  void* d_state = nullptr;
+  float* d_ring = nullptr;
+  int32_t* d_steps = nullptr;
+  void* d_init = nullptr;
+  void* d_target = nullptr;
+  int head = 0;  // ring slot receiving the next action (global: all envs step in lockstep)
+  double bound_xy;
+  std::vector<double> init_tmpl;  // [D][10]
+  std::vector<double> target;     // [D][3]
+};
+
+namespace {
+
+template <typename R>
+Consts<R> make_consts(const gpd_sim* s) {
+  const gpd_drone_params& P = s->P;
+  Consts<R> c;
+  c.dt = (R)s->K.pyb_timestep;
+  c.m = (R)P.m;
+  c.gravity = (R)s->K.gravity;
+  c.kf = (R)P.kf;
+  c.km = (R)P.km;
+  c.L = (R)P.arm;
+  c.Ls2 = (R)(P.arm / std::sqrt(2.0));
+  c.jx = (R)P.ixx; c.jy = (R)P.iyy; c.jz = (R)P.izz;
+  c.ijx = (R)(1.0 / P.ixx); c.ijy = (R)(1.0 / P.iyy); c.ijz = (R)(1.0 / P.izz);
+  c.ge_coeff = (R)P.gnd_eff_coeff;
+  c.prop_r = (R)P.prop_radius;
+  c.ge_clip = (R)s->K.gnd_eff_h_clip;
+  c.drag_xy = (R)P.drag_coeff_xy;
+  c.drag_z = (R)P.drag_coeff_z;
+  c.two_pi = (R)(2.0 * M_PI);
+  c.dw1 = (R)P.dw_coeff_1; c.dw2 = (R)P.dw_coeff_2; c.dw3 = (R)P.dw_coeff_3;
+  for (int k = 0; k < 4; ++k) {
+    c.rx[k] = (R)P.prop_pos[k][0];
+    c.ry[k] = (R)P.prop_pos[k][1];
+    c.rz[k] = (R)P.prop_pos[k][2];
+  }
+  c.hover_f32 = (float)s->K.hover_rpm;
+  c.model = P.model;
+  c.flags = s->cfg.physics_flags;
+  c.nsub = s->nsub;
+  return c;
+}
+
+template <typename R>
+SimView<R> make_view(const gpd_sim* s) {
+  SimView<R> v;
+  v.state = (R*)s->d_state;
+  v.ring = s->d_ring;
+  v.steps = s->d_steps;
+  v.init = (const R*)s->d_init;
+  v.target = (const R*)s->d_target;
+  v.npad = s->npad;
+  v.N = s->N; v.D = s->D; v.A = s->A; v.W = s->W; v.tpb = s->tpb; v.ring_len = s->ring_len;
+  v.task = s->cfg.task;
+  v.autoreset = s->cfg.autoreset;
+  v.trunc_sc = s->K.trunc_step_counter;
+  v.bound_xy = (R)s->bound_xy;
+  return v;
+}
+
+template <typename R>
+int upload_tables(gpd_sim* s) {
+  std::vector<R> ini(s->init_tmpl.begin(), s->init_tmpl.end());
+  std::vector<R> tgt(s->target.begin(), s->target.end());
+  HIP_TRY(hipMemcpy(s->d_init, ini.data(), ini.size() * sizeof(R), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s->d_target, tgt.data(), tgt.size() * sizeof(R), hipMemcpyHostToDevice));
+  return GPD_OK;
+}
+
+inline unsigned grid_for(long long n, int tpb) { return (unsigned)((n + tpb - 1) / tpb); }
+inline size_t real_size(const gpd_sim* s) { return s->prec == GPD_F64 ? sizeof(double) : sizeof(float); }
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+template <typename R>
+int launch_step(gpd_sim* s, const float* actions, float* obs, float* reward, uint8_t* term, uint8_t* trunc,
+                float* terminal_obs, hipStream_t st) {
+  StepIO<R> io;
+  io.actions = actions; io.obs = obs; io.reward = reward; io.term = term; io.trunc = trunc;
+  io.terminal_obs = terminal_obs; io.head = s->head;
+  const SimView<R> v = make_view<R>(s);
+  const Consts<R> c = make_consts<R>(s);
+  const unsigned grid = grid_for(s->N, s->tpb);
+  const bool multi = s->D > 1;
+  if (s->A == 4) {
+    if (multi) hipLaunchKernelGGL((step_kernel<R, 4, true>), dim3(grid), dim3(kWave), 0, st, v, io, c);
+    else hipLaunchKernelGGL((step_kernel<R, 4, false>), dim3(grid), dim3(kWave), 0, st, v, io, c);
+  } else {
+    if (multi) hipLaunchKernelGGL((step_kernel<R, 1, true>), dim3(grid), dim3(kWave), 0, st, v, io, c);
+    else hipLaunchKernelGGL((step_kernel<R, 1, false>), dim3(grid), dim3(kWave), 0, st, v, io, c);
+  }
+  HIP_TRY(hipGetLastError());
+  s->head = (s->head + 1) % s->ring_len;
+  return GPD_OK;
+}
+
+template <typename R>
+int launch_integrate(gpd_sim* s, const void* rpm, int n_sub, void* traj, hipStream_t st) {
+  const SimView<R> v = make_view<R>(s);
+  const Consts<R> c = make_consts<R>(s);
+  const unsigned grid = grid_for(s->N, s->tpb);
+  if (s->D > 1)
+    hipLaunchKernelGGL((integrate_kernel<R, true>), dim3(grid), dim3(kWave), 0, st, v, c, (const R*)rpm, n_sub, (R*)traj);
+  else
+    hipLaunchKernelGGL((integrate_kernel<R, false>), dim3(grid), dim3(kWave), 0, st, v, c, (const R*)rpm, n_sub, (R*)traj);
+  HIP_TRY(hipGetLastError());
+  return GPD_OK;
+}
+
+template <typename R>
+int launch_reset(gpd_sim* s, const uint8_t* mask, float* obs, hipStream_t st) {
+  const SimView<R> v = make_view<R>(s);
+  hipLaunchKernelGGL((reset_kernel<R>), dim3(grid_for(s->N, 256)), dim3(256), 0, st, v, mask, obs, s->head);
+  HIP_TRY(hipGetLastError());
+  return GPD_OK;
+}
+
+template <typename R>
+int launch_state20(gpd_sim* s, void* out, int raw, hipStream_t st) {
+  const SimView<R> v = make_view<R>(s);
+  hipLaunchKernelGGL((state20_kernel<R>), dim3(grid_for(s->N, 256)), dim3(256), 0, st, v, (R*)out, raw);
+  HIP_TRY(hipGetLastError());
+  return GPD_OK;
+}
+
+template <typename R>
+int launch_set_raw(gpd_sim* s, const void* in, hipStream_t st) {
+  const SimView<R> v = make_view<R>(s);
+  hipLaunchKernelGGL((set_raw_kernel<R>), dim3(grid_for(s->N, 256)), dim3(256), 0, st, v, (const R*)in);
+  HIP_TRY(hipGetLastError());
+  return GPD_OK;
+}
+
+void free_sim(gpd_sim* s) {
+  if (!s) return;
+  if (s->d_state) (void)hipFree(s->d_state);
+  if (s->d_ring) (void)hipFree(s->d_ring);
+  if (s->d_steps) (void)hipFree(s->d_steps);
+  if (s->d_init) (void)hipFree(s->d_init);
+  if (s->d_target) (void)hipFree(s->d_target);
+  delete s;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gpd_abi_version(void) { return GPD_ABI_VERSION; }
+
+const char* gpd_last_error(void) { return g_err.c_str(); }
+
+int gpd_default_params(int model, gpd_drone_params* out) {
+  if (!out) return fail(GPD_EINVAL, "gpd_default_params: out is NULL");
+  gpd_drone_params p;
+  std::memset(&p, 0, sizeof(p));
+  p.model = model;
+  // <properties> common to the three URDFs (cf2x.urdf:5)
+  p.gnd_eff_coeff = 11.36859; p.drag_coeff_xy = 9.1785e-7; p.drag_coeff_z = 10.311e-7;
+  p.dw_coeff_1 = 2267.18; p.dw_coeff_2 = .16; p.dw_coeff_3 = -.11;
+  p.collision_h = .025; p.collision_r = .06; p.collision_z_offset = 0.0;  // collision cylinder
+  double pp[4][3];
+  if (model == GPD_MODEL_CF2X || model == GPD_MODEL_CF2P) {             // cf2x.urdf / cf2p.urdf
+    p.arm = 0.0397; p.kf = 3.16e-10; p.km = 7.94e-12; p.thrust2weight = 2.25; p.max_speed_kmh = 30;
+    p.prop_radius = 2.31348e-2; p.m = 0.027;
+    if (model == GPD_MODEL_CF2X) {
+      p.ixx = 1.4e-5; p.iyy = 1.4e-5; p.izz = 2.17e-5;
+      const double c[4][3] = {{0.028, -0.028, 0}, {-0.028, -0.028, 0}, {-0.028, 0.028, 0}, {0.028, 0.028, 0}};
+      std::memcpy(pp, c, sizeof(pp));
+    } else {
+      p.ixx = 2.3951e-5; p.iyy = 2.3951e-5; p.izz = 3.2347e-5;
+      const double c[4][3] = {{0.0397, 0, 0}, {0, 0.0397, 0}, {-0.0397, 0, 0}, {0, -0.0397, 0}};
+      std::memcpy(pp, c, sizeof(pp));
+    }
+  } else if (model == GPD_MODEL_RACE) {                                   // racer.urdf
+    p.arm = 0.109; p.kf = 8.47e-9; p.km = 2.13e-11; p.thrust2weight = 4.17; p.max_speed_kmh = 200;
+    p.prop_radius = 12.7e-2; p.m = 0.830; p.ixx = .003113; p.iyy = .003113; p.izz = .003113;
+    const double c[4][3] = {{0.0850, 0.0675, 0}, {-0.0850, 0.0675, 0}, {-0.085, -0.0675, 0}, {0.085, -0.0675, 0}};
+    std::memcpy(pp, c, sizeof(pp));
+  } else {
+    return fail(GPD_EINVAL, "gpd_default_params: unknown drone model");
+  }
+  std::memcpy(p.prop_pos, pp, sizeof(pp));
+  *out = p;
+  return GPD_OK;
+}
+
+int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** out) {
+  if (!params || !cfg || !out) return fail(GPD_EINVAL, "gpd_create: NULL argument");
+  *out = nullptr;
+  const gpd_config& C = *cfg;
+  if (C.n_envs < 1) return fail(GPD_EINVAL, "gpd_create: n_envs must be >= 1");
+  if (C.drones_per_env < 1 || C.drones_per_env > kWave)
+    return fail(GPD_EINVAL, "gpd_create: drones_per_env must be in [1, 64]");
+  if (C.pyb_freq < 1 || C.ctrl_freq < 1) return fail(GPD_EINVAL, "gpd_create: frequencies must be >= 1");
+  if (C.pyb_freq % C.ctrl_freq != 0)
+    return fail(GPD_EINVAL, "[ERROR] in BaseAviary.__init__(), pyb_freq is not divisible by env_freq.");
+  if (C.ctrl_freq / 2 < 1)
+    return fail(GPD_EUNSUPPORTED, "gpd_create: ctrl_freq//2 == 0 gives an empty action buffer (unsupported)");
+  if (C.act_type != GPD_ACT_RPM && C.act_type != GPD_ACT_ONE_D_RPM)
+    return fail(GPD_EUNSUPPORTED, "gpd_create: only ActionType.RPM / ONE_D_RPM run on this path");
+  if (C.task < GPD_TASK_NONE || C.task > GPD_TASK_MULTIHOVER) return fail(GPD_EINVAL, "gpd_create: bad task");
+  if (C.task == GPD_TASK_HOVER && C.drones_per_env != 1)
+    return fail(GPD_EINVAL, "gpd_create: HoverAviary is single-drone (drones_per_env must be 1)");
+  if (C.precision != GPD_F32 && C.precision != GPD_F64) return fail(GPD_EINVAL, "gpd_create: bad precision");
+  if (C.physics_flags & ~(GPD_F_GND | GPD_F_DRAG | GPD_F_DW | GPD_F_GEOM_WRENCH))
+    return fail(GPD_EINVAL, "gpd_create: unknown physics flag");
+  if (params->model < GPD_MODEL_CF2X || params->model > GPD_MODEL_RACE)
+    return fail(GPD_EINVAL, "gpd_create: unknown drone model");
+  const long long Nll = (long long)C.n_envs * C.drones_per_env;
+  if (Nll > (1LL << 31) - 64) return fail(GPD_EINVAL, "gpd_create: too many drones");
+
+  gpd_sim* s = new gpd_sim();
+  s->P = *params;
+  s->cfg = C;
+  s->cfg.init_xyzs_host = nullptr;
+  s->cfg.init_rpys_host = nullptr;
+  s->E = C.n_envs;
+  s->D = C.drones_per_env;
+  s->N = (int)Nll;
+  s->A = C.act_type == GPD_ACT_RPM ? 4 : 1;
+  s->ring_len = C.ctrl_freq / 2;  // ACTION_BUFFER_SIZE = int(ctrl_freq//2)  BaseRLAviary.py:66
+  s->W = 12 + s->ring_len * s->A;
+  s->nsub = C.pyb_freq / C.ctrl_freq;
+  s->prec = C.precision;
+  s->tpb = (kWave / s->D) * s->D;
+  s->npad = ((long long)s->N + 63) / 64 * 64;
+  s->bound_xy = C.task == GPD_TASK_MULTIHOVER ? 2.0 : 1.5;
+
+  // derived constants (BaseAviary.py:117-128)
+  const gpd_drone_params& P = *params;
+  gpd_constants& K = s->K;
+  std::memset(&K, 0, sizeof(K));
+  K.gravity = 9.8 * P.m;
+  K.hover_rpm = std::sqrt(K.gravity / (4 * P.kf));
+  K.max_rpm = std::sqrt((P.thrust2weight * K.gravity) / (4 * P.kf));
+  K.max_thrust = 4 * P.kf * (K.max_rpm * K.max_rpm);
+  K.max_xy_torque = P.model == GPD_MODEL_CF2P ? P.arm * P.kf * (K.max_rpm * K.max_rpm)
+                                              : (2 * P.arm * P.kf * (K.max_rpm * K.max_rpm)) / std::sqrt(2.0);
+  K.max_z_torque = 2 * P.km * (K.max_rpm * K.max_rpm);
+  K.gnd_eff_h_clip = 0.25 * P.prop_radius *
+                     std::sqrt((15 * (K.max_rpm * K.max_rpm) * P.kf * P.gnd_eff_coeff) / K.max_thrust);
+  K.pyb_timestep = 1.0 / C.pyb_freq;
+  K.ctrl_timestep = 1.0 / C.ctrl_freq;
+  K.pyb_steps_per_ctrl = s->nsub;
+  K.action_buffer_size = s->ring_len;
+  K.obs_width = s->W;
+  K.act_width = s->A;
+  K.n_drones = s->N;
+  {  // truncated iff step_counter / PYB_FREQ > EPISODE_LEN_SEC  (HoverAviary.py:114)
+    long long sc = (long long)std::floor(C.episode_len_sec * C.pyb_freq);
+    if (sc < 0) sc = 0;
+    while (sc > 0 && (double)(sc - 1) / C.pyb_freq > C.episode_len_sec) --sc;
+    while (!((double)sc / C.pyb_freq > C.episode_len_sec)) ++sc;
+    K.trunc_step_counter = (int)std::min<long long>(sc, 0x7fffffff);
+  }
+
+  // reset template: INIT_XYZS (BaseAviary.py:194-197) and the orientation the client stores
+  s->init_tmpl.assign((size_t)s->D * 10, 0.0);
+  s->target.assign((size_t)s->D * 3, 0.0);
+  for (int d = 0; d < s->D; ++d) {
+    double xyz[3], rpy[3] = {0, 0, 0};
+    if (C.init_xyzs_host) {
+      for (int k = 0; k < 3; ++k) xyz[k] = C.init_xyzs_host[d * 3 + k];
+    } else {
+      xyz[0] = d * 4 * P.arm;
+      xyz[1] = d * 4 * P.arm;
+      xyz[2] = P.collision_h / 2 - P.collision_z_offset + .1;
+    }
+    if (C.init_rpys_host)
+      for (int k = 0; k < 3; ++k) rpy[k] = C.init_rpys_host[d * 3 + k];
+    double q0[4], qraw[4], qn[4], e[3];
+    h_quat_from_euler(rpy, q0);
+    h_roundtrip(q0, qraw);  // loadURDF stores the orientation through a btTransform
+    h_roundtrip(qraw, qn);  // readback (:517)
+    h_euler(qn, e);         // :518
+    double* t = &s->init_tmpl[(size_t)d * 10];
+    t[0] = xyz[0]; t[1] = xyz[1]; t[2] = xyz[2];
+    t[3] = qraw[0]; t[4] = qraw[1]; t[5] = qraw[2]; t[6] = qraw[3];
+    t[7] = e[0]; t[8] = e[1]; t[9] = e[2];
+    if (C.task == GPD_TASK_HOVER) {           // HoverAviary.py:51
+      s->target[d * 3 + 2] = 1.0;
+    } else if (C.task == GPD_TASK_MULTIHOVER) {  // MultiHoverAviary.py:71
+      s->target[d * 3 + 0] = xyz[0];
+      s->target[d * 3 + 1] = xyz[1];
+      s->target[d * 3 + 2] = xyz[2] + 1.0 / (d + 1);
+    }
+  }
+
+  const size_t rs = real_size(s);
+  hipError_t e1 = hipMalloc(&s->d_state, (size_t)kStateComps * s->npad * rs);
+  hipError_t e2 = hipMalloc((void**)&s->d_ring, (size_t)s->ring_len * s->npad * s->A * sizeof(float));
+  hipError_t e3 = hipMalloc((void**)&s->d_steps, (size_t)s->E * sizeof(int32_t));
+  hipError_t e4 = hipMalloc(&s->d_init, (size_t)s->D * 10 * rs);
+  hipError_t e5 = hipMalloc(&s->d_target, (size_t)s->D * 3 * rs);
+  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess) {
+    free_sim(s);
+    (void)hipGetLastError();
+    return fail(GPD_ENOMEM, "gpd_create: hipMalloc failed");
+  }
+  int rc = s->prec == GPD_F64 ? upload_tables<double>(s) : upload_tables<float>(s);
+  if (rc != GPD_OK) { free_sim(s); return rc; }
+  if (hipMemset(s->d_state, 0, (size_t)kStateComps * s->npad * rs) != hipSuccess ||
+      hipMemset(s->d_ring, 0, (size_t)s->ring_len * s->npad * s->A * sizeof(float)) != hipSuccess ||
+      hipMemset(s->d_steps, 0, (size_t)s->E * sizeof(int32_t)) != hipSuccess) {
+    free_sim(s);
+    return fail(GPD_EHIP, "gpd_create: hipMemset failed");
+  }
+  rc = s->prec == GPD_F64 ? launch_reset<double>(s, nullptr, nullptr, 0) : launch_reset<float>(s, nullptr, nullptr, 0);
+  if (rc == GPD_OK && hipDeviceSynchronize() != hipSuccess) rc = fail(GPD_EHIP, "gpd_create: initial reset failed");
+  if (rc != GPD_OK) { free_sim(s); return rc; }
+  *out = s;
+  return GPD_OK;
+}
+
+int gpd_destroy(gpd_sim* sim) {
+  if (!sim) return fail(GPD_EINVAL, "gpd_destroy: NULL sim");
+  (void)hipDeviceSynchronize();
+  free_sim(sim);
+  return GPD_OK;
+}
+
+int gpd_get_constants(const gpd_sim* sim, gpd_constants* out) {
+  if (!sim || !out) return fail(GPD_EINVAL, "gpd_get_constants: NULL argument");
+  *out = sim->K;
+  return GPD_OK;
+}
+
+int gpd_reset(gpd_sim* sim, const uint8_t* env_mask, float* obs, void* stream) {
+  if (!sim) return fail(GPD_EINVAL, "gpd_reset: NULL sim");
+  hipStream_t st = (hipStream_t)stream;
+  return sim->prec == GPD_F64 ? launch_reset<double>(sim, env_mask, obs, st) : launch_reset<float>(sim, env_mask, obs, st);
+}
+
+int gpd_step(gpd_sim* sim, const float* actions, float* obs, float* reward, uint8_t* terminated,
+             uint8_t* truncated, float* terminal_obs, void* stream) {
+  if (!sim || !actions || !obs || !reward || !terminated || !truncated)
+    return fail(GPD_EINVAL, "gpd_step: NULL argument");
+  if (sim->A == 4 && !aligned16(actions)) return fail(GPD_EINVAL, "gpd_step: actions must be 16-byte aligned");
+  if (sim->A == 4 && (!aligned16(obs) || (terminal_obs && !aligned16(terminal_obs))))
+    return fail(GPD_EINVAL, "gpd_step: obs buffers must be 16-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  return sim->prec == GPD_F64
+             ? launch_step<double>(sim, actions, obs, reward, terminated, truncated, terminal_obs, st)
+             : launch_step<float>(sim, actions, obs, reward, terminated, truncated, terminal_obs, st);
+}
+
+int gpd_integrate(gpd_sim* sim, const void* rpm, int n_sub, void* traj, void* stream) {
+  if (!sim || !rpm) return fail(GPD_EINVAL, "gpd_integrate: NULL argument");
+  if (n_sub < 0) return fail(GPD_EINVAL, "gpd_integrate: n_sub < 0");
+  if (n_sub == 0) return GPD_OK;
+  hipStream_t st = (hipStream_t)stream;
+  return sim->prec == GPD_F64 ? launch_integrate<double>(sim, rpm, n_sub, traj, st)
+                              : launch_integrate<float>(sim, rpm, n_sub, traj, st);
+}
+
+int gpd_get_state20(gpd_sim* sim, void* out, void* stream) {
+  if (!sim || !out) return fail(GPD_EINVAL, "gpd_get_state20: NULL argument");
+  hipStream_t st = (hipStream_t)stream;
+  return sim->prec == GPD_F64 ? launch_state20<double>(sim, out, 0, st) : launch_state20<float>(sim, out, 0, st);
+}
+
+int gpd_get_raw_state(gpd_sim* sim, void* out, void* stream) {
+  if (!sim || !out) return fail(GPD_EINVAL, "gpd_get_raw_state: NULL argument");
+  hipStream_t st = (hipStream_t)stream;
+  return sim->prec == GPD_F64 ? launch_state20<double>(sim, out, 1, st) : launch_state20<float>(sim, out, 1, st);
+}
+
+int gpd_set_raw_state(gpd_sim* sim, const void* in, void* stream) {
+  if (!sim || !in) return fail(GPD_EINVAL, "gpd_set_raw_state: NULL argument");
+  hipStream_t st = (hipStream_t)stream;
+  return sim->prec == GPD_F64 ? launch_set_raw<double>(sim, in, st) : launch_set_raw<float>(sim, in, st);
+}
+
+int gpd_get_step_counters(gpd_sim* sim, int32_t* out, void* stream) {
+  if (!sim || !out) return fail(GPD_EINVAL, "gpd_get_step_counters: NULL argument");
+  HIP_TRY(hipMemcpyAsync(out, sim->d_steps, (size_t)sim->E * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream));
+  return GPD_OK;
+}
+
+int gpd_set_step_counters(gpd_sim* sim, const int32_t* in, void* stream) {
+  if (!sim || !in) return fail(GPD_EINVAL, "gpd_set_step_counters: NULL argument");
+  HIP_TRY(hipMemcpyAsync(sim->d_steps, in, (size_t)sim->E * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream));
+  return GPD_OK;
+}
+
+size_t gpd_state_bytes(const gpd_sim* sim) {
+  if (!sim) return 0;
+  return 16 + (size_t)kStateComps * sim->npad * real_size(sim) +
+         (size_t)sim->ring_len * sim->npad * sim->A * sizeof(float) + (size_t)sim->E * sizeof(int32_t);
+}
+
+int gpd_save_state(gpd_sim* sim, void* blob_host, void* stream) {
+  if (!sim || !blob_host) return fail(GPD_EINVAL, "gpd_save_state: NULL argument");
+  hipStream_t st = (hipStream_t)stream;
+  char* b = (char*)blob_host;
+  int64_t hdr[2] = {(int64_t)sim->head, (int64_t)sim->N};
+  std::memcpy(b, hdr, 16);
+  size_t off = 16;
+  const size_t s1 = (size_t)kStateComps * sim->npad * real_size(sim);
+  const size_t s2 = (size_t)sim->ring_len * sim->npad * sim->A * sizeof(float);
+  const size_t s3 = (size_t)sim->E * sizeof(int32_t);
+  HIP_TRY(hipMemcpyAsync(b + off, sim->d_state, s1, hipMemcpyDeviceToHost, st)); off += s1;
+  HIP_TRY(hipMemcpyAsync(b + off, sim->d_ring, s2, hipMemcpyDeviceToHost, st)); off += s2;
+  HIP_TRY(hipMemcpyAsync(b + off, sim->d_steps, s3, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return GPD_OK;
+}
+
+int gpd_load_state(gpd_sim* sim, const void* blob_host, void* stream) {
+  if (!sim || !blob_host) return fail(GPD_EINVAL, "gpd_load_state: NULL argument");
+  hipStream_t st = (hipStream_t)stream;
+  const char* b = (const char*)blob_host;
+  int64_t hdr[2];
+  std::memcpy(hdr, b, 16);
+  if (hdr[1] != sim->N || hdr[0] < 0 || hdr[0] >= sim->ring_len)
+    return fail(GPD_EINVAL, "gpd_load_state: blob does not match this sim");
+  size_t off = 16;
+  const size_t s1 = (size_t)kStateComps * sim->npad * real_size(sim);
+  const size_t s2 = (size_t)sim->ring_len * sim->npad * sim->A * sizeof(float);
+  const size_t s3 = (size_t)sim->E * sizeof(int32_t);
+  HIP_TRY(hipMemcpyAsync(sim->d_state, b + off, s1, hipMemcpyHostToDevice, st)); off += s1;
+  HIP_TRY(hipMemcpyAsync(sim->d_ring, b + off, s2, hipMemcpyHostToDevice, st)); off += s2;
+  HIP_TRY(hipMemcpyAsync(sim->d_steps, b + off, s3, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  sim->head = (int)hdr[0];
+  return GPD_OK;
+}
+
+}  // extern "C"

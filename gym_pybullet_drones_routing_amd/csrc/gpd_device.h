@@ -1,0 +1,288 @@
+// gpd_device.h — per-drone DYN physics for gfx950, templated on the real type.
+//
+// One lane owns one drone for the whole launch: the raw state lives in VGPRs across all
+// PYB_STEPS_PER_CTRL substeps, the model constants arrive as kernel arguments (SGPRs), and
+// only the per-env neighbour positions (downwash) go through LDS.
+//
+// Every function cites the reference code it restates (paths relative to
+// gym_pybullet_drones/ in the reference) or the Bullet3 routine pybullet runs for it.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gpd {
+
+// ---------------------------------------------------------------- precision-overloaded math
+__device__ __forceinline__ float g_sqrt(float x) { return sqrtf(x); }
+__device__ __forceinline__ double g_sqrt(double x) { return sqrt(x); }
+__device__ __forceinline__ float g_sin(float x) { return sinf(x); }
+__device__ __forceinline__ double g_sin(double x) { return sin(x); }
+__device__ __forceinline__ float g_cos(float x) { return cosf(x); }
+__device__ __forceinline__ double g_cos(double x) { return cos(x); }
+__device__ __forceinline__ float g_atan2(float y, float x) { return atan2f(y, x); }
+__device__ __forceinline__ double g_atan2(double y, double x) { return atan2(y, x); }
+__device__ __forceinline__ float g_asin(float x) { return asinf(x); }
+__device__ __forceinline__ double g_asin(double x) { return asin(x); }
+__device__ __forceinline__ float g_exp(float x) { return expf(x); }
+__device__ __forceinline__ double g_exp(double x) { return exp(x); }
+__device__ __forceinline__ float g_abs(float x) { return fabsf(x); }
+__device__ __forceinline__ double g_abs(double x) { return fabs(x); }
+
+template <typename R> struct PiC;
+template <> struct PiC<float> { static constexpr float pi = 3.14159265358979323846f; };
+template <> struct PiC<double> { static constexpr double pi = 3.14159265358979323846; };
+
+// ---------------------------------------------------------------- model constants (kernel arg)
+enum : int { MODEL_CF2X = 0, MODEL_CF2P = 1, MODEL_RACE = 2 };
+enum : int { F_GND = 1, F_DRAG = 2, F_DW = 4, F_GEOM = 8 };
+
+template <typename R>
+struct Consts {
+  R dt;                    // PYB_TIMESTEP = 1./PYB_FREQ              BaseAviary.py:83
+  R m, gravity;            // M, GRAVITY = G*M                        :97, :117
+  R kf, km, L, Ls2;        // KF, KM, L, L/np.sqrt(2)                 :847
+  R jx, jy, jz;            // J diagonal                              :996
+  R ijx, ijy, ijz;         // J_INV diagonal                          :997
+  R ge_coeff, prop_r, ge_clip;             // :108-109, :128
+  R drag_xy, drag_z, two_pi;               // :1009, 2*np.pi (:773)
+  R dw1, dw2, dw3;                         // :1010-1012
+  R rx[4], ry[4], rz[4];                   // prop link origins (cf2x.urdf:42,54,66,78)
+  float hover_f32;         // float32(HOVER_RPM) (numpy 1.x casting, BaseRLAviary.py:192)
+  int model, flags, nsub;
+};
+
+template <typename R>
+struct Drone {
+  R px, py, pz;            // base position (physics-client copy == self.pos)
+  R qx, qy, qz, qw;        // base orientation AS STORED by resetBasePositionAndOrientation
+  R vx, vy, vz;            // base linear velocity
+  R wx, wy, wz;            // self.rpy_rates (body rates, DYN only)      :477, :874
+  R ax, ay, az;            // base angular velocity as written, R(q)·ω   :870
+};
+
+// ---------------------------------------------------------------- Bullet3 rotation helpers
+// btMatrix3x3::setRotation (pybullet getMatrixFromQuaternion, BaseAviary.py:836): row-major.
+template <typename R>
+__device__ __forceinline__ void quat_to_mat(R x, R y, R z, R w, R m[9]) {
+  const R d = x * x + y * y + z * z + w * w;
+  const R s = R(2) / d;
+  const R xs = x * s, ys = y * s, zs = z * s;
+  const R wx = w * xs, wy = w * ys, wz = w * zs;
+  const R xx = x * xs, xy = x * ys, xz = x * zs;
+  const R yy = y * ys, yz = y * zs, zz = z * zs;
+  m[0] = R(1) - (yy + zz); m[1] = xy - wz;           m[2] = xz + wy;
+  m[3] = xy + wz;          m[4] = R(1) - (xx + zz);  m[5] = yz - wx;
+  m[6] = xz - wy;          m[7] = yz + wx;           m[8] = R(1) - (xx + yy);
+}
+
+// btMatrix3x3::getRotation: basis -> quaternion [x,y,z,w] (w > 0 when trace > 0).
+template <typename R>
+__device__ __forceinline__ void mat_to_quat(const R m[9], R q[4]) {
+  const R trace = m[0] + m[4] + m[8];
+  if (trace > R(0)) {
+    R s = g_sqrt(trace + R(1));
+    q[3] = s * R(0.5);
+    s = R(0.5) / s;
+    q[0] = (m[7] - m[5]) * s;
+    q[1] = (m[2] - m[6]) * s;
+    q[2] = (m[3] - m[1]) * s;
+  } else {
+    // i = index of the largest diagonal entry, j = i+1, k = i+2 (mod 3); the three cases are
+    // spelled out so that every matrix access is a compile-time register index.
+    const int i = m[0] < m[4] ? (m[4] < m[8] ? 2 : 1) : (m[0] < m[8] ? 2 : 0);
+    if (i == 0) {         // j = 1, k = 2
+      R s = g_sqrt(((m[0] - m[4]) - m[8]) + R(1));
+      q[0] = s * R(0.5);
+      s = R(0.5) / s;
+      q[3] = (m[7] - m[5]) * s;
+      q[1] = (m[3] + m[1]) * s;
+      q[2] = (m[6] + m[2]) * s;
+    } else if (i == 1) {  // j = 2, k = 0
+      R s = g_sqrt(((m[4] - m[8]) - m[0]) + R(1));
+      q[1] = s * R(0.5);
+      s = R(0.5) / s;
+      q[3] = (m[2] - m[6]) * s;
+      q[2] = (m[7] + m[5]) * s;
+      q[0] = (m[1] + m[3]) * s;
+    } else {              // j = 0, k = 1
+      R s = g_sqrt(((m[8] - m[0]) - m[4]) + R(1));
+      q[2] = s * R(0.5);
+      s = R(0.5) / s;
+      q[3] = (m[3] - m[1]) * s;
+      q[0] = (m[2] + m[6]) * s;
+      q[1] = (m[5] + m[7]) * s;
+    }
+  }
+}
+
+// Readback of the orientation (BaseAviary.py:517): the stored quaternion comes back through
+// a btTransform basis, which re-normalises it.
+template <typename R>
+__device__ __forceinline__ void quat_readback(R x, R y, R z, R w, R qn[4]) {
+  R m[9];
+  quat_to_mat(x, y, z, w, m);
+  mat_to_quat(m, qn);
+}
+
+// btQuaternion::getEulerZYX (pybullet getEulerFromQuaternion, BaseAviary.py:518).
+template <typename R>
+__device__ __forceinline__ void quat_to_euler(const R q[4], R& roll, R& pitch, R& yaw) {
+  const R x = q[0], y = q[1], z = q[2], w = q[3];
+  const R sqx = x * x, sqy = y * y, sqz = z * z, squ = w * w;
+  const R sarg = R(-2) * (x * z - w * y);
+  if (sarg <= R(-0.99999)) {
+    pitch = R(-0.5) * PiC<R>::pi;
+    roll = R(0);
+    yaw = R(2) * g_atan2(x, -y);
+  } else if (sarg >= R(0.99999)) {
+    pitch = R(0.5) * PiC<R>::pi;
+    roll = R(0);
+    yaw = R(2) * g_atan2(-x, y);
+  } else {
+    R sa = sarg < R(-1) ? R(-1) : (sarg > R(1) ? R(1) : sarg);  // btAsin clamp
+    pitch = g_asin(sa);
+    roll = g_atan2(R(2) * (y * z + w * x), squ - sqx - sqy + sqz);
+    yaw = g_atan2(R(2) * (x * y + w * z), squ + sqx - sqy - sqz);
+  }
+}
+
+// float32 RPM from a float32 action exactly as numpy 1.x evaluates
+// HOVER_RPM * (1 + 0.05*target) on a float32 array (BaseRLAviary.py:192, :225).
+// hipcc would otherwise contract 1 + 0.05*a into one FMA (even through __fmul_rn/__fadd_rn),
+// which differs from numpy's two separately rounded float32 ops by up to 2 ulps of the RPM.
+__device__ __forceinline__ float action_to_rpm(float hover_f32, float a) {
+#pragma clang fp contract(off)
+  const float t = 0.05f * a;
+  const float u = 1.0f + t;
+  return hover_f32 * u;
+}
+
+// ---------------------------------------------------------------- one DYN substep
+// BaseAviary._dynamics (:815-874) + _integrateQ (:876-889), evaluated on the readback
+// snapshot (pos/vel from the client copy, qn = re-normalised orientation, rpy = its Euler
+// angles), optionally with the aero force terms of _groundEffect/_drag/_downwash added as a
+// body wrench (see DESIGN.md §2 "new combination").
+//   rpm  : this ctrl step's clipped action (current substep)
+//   last : self.last_clipped_action (previous ctrl step's rpm on the first substep)
+//   dwsum: summed downwash force along body z (already reduced over the env's drones)
+template <typename R>
+__device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R Rm[9], R roll, R pitch,
+                                            const R rpm[4], const R last[4], R dwsum,
+                                            const Consts<R>& c) {
+  R f[4], zt[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const R r2 = rpm[k] * rpm[k];
+    f[k] = r2 * c.kf;                                  // :838
+    zt[k] = r2 * c.km;                                 // :842
+  }
+  if (c.model == MODEL_RACE) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) zt[k] = -zt[k];        // :843-844
+  }
+  R fz = ((f[0] + f[1]) + f[2]) + f[3];                // np.sum(forces) :839
+  const R tz = ((-zt[0] + zt[1]) - zt[2]) + zt[3];     // :845
+  R tx, ty;
+  if (c.flags & F_GEOM) {                              // _physics: forces at prop links :698-705
+    tx = R(0); ty = R(0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { tx = tx + c.ry[k] * f[k]; ty = ty - c.rx[k] * f[k]; }
+  } else if (c.model == MODEL_CF2P) {                  // :849-851
+    tx = (f[1] - f[3]) * c.L;
+    ty = (-f[0] + f[2]) * c.L;
+  } else {                                             // CF2X / RACE :846-848 (roll-sign quirk kept)
+    tx = (((f[0] + f[1]) - f[2]) - f[3]) * c.Ls2;
+    ty = (((-f[0] + f[1]) + f[2]) - f[3]) * c.Ls2;
+  }
+  if ((c.flags & F_GND) && g_abs(roll) < PiC<R>::pi / R(2) && g_abs(pitch) < PiC<R>::pi / R(2)) {
+    // _groundEffect :732-750 — prop COM heights via forward kinematics, clipped, +z link force
+    R g[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      R h = s.pz + ((Rm[6] * c.rx[k] + Rm[7] * c.ry[k]) + Rm[8] * c.rz[k]);
+      h = h < c.ge_clip ? c.ge_clip : h;
+      const R qq = c.prop_r / (R(4) * h);
+      g[k] = ((rpm[k] * rpm[k]) * c.kf * c.ge_coeff) * (qq * qq);
+    }
+    fz = fz + (((g[0] + g[1]) + g[2]) + g[3]);
+    R gx = R(0), gy = R(0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { gx = gx + c.ry[k] * g[k]; gy = gy - c.rx[k] * g[k]; }
+    tx = tx + gx;
+    ty = ty + gy;
+  }
+  if (c.flags & F_DW) fz = fz + dwsum;                 // _downwash :801-811 (body z)
+  // R·(0,0,fz) - (0,0,GRAVITY) [+ drag]                 :839-841
+  R Fx = Rm[2] * fz, Fy = Rm[5] * fz, Fz = Rm[8] * fz;
+  if (c.flags & F_DRAG) {                              // _drag :773-774 with last_clipped_action
+    const R S = (((c.two_pi * last[0] / R(60) + c.two_pi * last[1] / R(60)) + c.two_pi * last[2] / R(60)) +
+                 c.two_pi * last[3] / R(60));
+    Fx = Fx + (-c.drag_xy * S) * s.vx;
+    Fy = Fy + (-c.drag_xy * S) * s.vy;
+    Fz = Fz + (-c.drag_z * S) * s.vz;
+  }
+  Fz = Fz - c.gravity;
+  // torques - ω × (Jω); ω̇ = J⁻¹ τ                     :852-854
+  const R jwx = c.jx * s.wx, jwy = c.jy * s.wy, jwz = c.jz * s.wz;
+  const R cx = s.wy * jwz - s.wz * jwy;
+  const R cy = s.wz * jwx - s.wx * jwz;
+  const R cz = s.wx * jwy - s.wy * jwx;
+  const R dwx = c.ijx * (tx - cx), dwy = c.ijy * (ty - cy), dwz = c.ijz * (tz - cz);
+  // semi-implicit Euler                                :855-859
+  s.vx = s.vx + c.dt * (Fx / c.m);
+  s.vy = s.vy + c.dt * (Fy / c.m);
+  s.vz = s.vz + c.dt * (Fz / c.m);
+  s.wx = s.wx + c.dt * dwx;
+  s.wy = s.wy + c.dt * dwy;
+  s.wz = s.wz + c.dt * dwz;
+  s.px = s.px + c.dt * s.vx;
+  s.py = s.py + c.dt * s.vy;
+  s.pz = s.pz + c.dt * s.vz;
+  // _integrateQ(quat, rpy_rates, dt)                  :876-889
+  const R p = s.wx, q = s.wy, r = s.wz;
+  const R nrm = g_sqrt(p * p + q * q + r * r);
+  if (nrm > R(1e-8)) {                                 // np.isclose(norm, 0): |norm| <= 1e-8
+    const R th = nrm * c.dt / R(2);
+    const R co = g_cos(th), si = g_sin(th);
+    const R k2 = R(2) / nrm;
+    const R P = (k2 * (R(0.5) * p)) * si, Q = (k2 * (R(0.5) * q)) * si, Rr = (k2 * (R(0.5) * r)) * si;
+    const R x = qn[0], y = qn[1], z = qn[2], w = qn[3];
+    s.qx = ((co * x + Rr * y) - Q * z) + P * w;
+    s.qy = ((-Rr * x + co * y) + P * z) + Q * w;
+    s.qz = ((Q * x - P * y) + co * z) + Rr * w;
+    s.qw = ((-P * x - Q * y) - Rr * z) + co * w;
+  } else {
+    s.qx = qn[0]; s.qy = qn[1]; s.qz = qn[2]; s.qw = qn[3];
+  }
+  // resetBaseVelocity(..., np.dot(rotation, rpy_rates))  :868-872
+  s.ax = (Rm[0] * s.wx + Rm[1] * s.wy) + Rm[2] * s.wz;
+  s.ay = (Rm[3] * s.wx + Rm[4] * s.wy) + Rm[5] * s.wz;
+  s.az = (Rm[6] * s.wx + Rm[7] * s.wy) + Rm[8] * s.wz;
+}
+
+// Summed downwash on drone (px,py,pz) from the env's D drones whose positions sit in LDS
+// (BaseAviary._downwash :798-811).  A wave-wide ballot skips the α/β/exp block whenever no
+// lane of the wave has an active pair (Δz > 0 ∧ Δxy < 10) for neighbour j.
+template <typename R>
+__device__ __forceinline__ R downwash_sum(R px, R py, R pz, const R* sx, const R* sy, const R* sz,
+                                          int base, int D, const Consts<R>& c) {
+  R total = R(0);
+  for (int j = 0; j < D; ++j) {
+    const R dz = sz[base + j] - pz;
+    const R ddx = sx[base + j] - px, ddy = sy[base + j] - py;
+    const R dxy = g_sqrt(ddx * ddx + ddy * ddy);
+    const bool hit = (dz > R(0)) && (dxy < R(10));
+    if (__ballot(hit) != 0ull) {
+      if (hit) {
+        const R qq = c.prop_r / (R(4) * dz);
+        const R alpha = c.dw1 * (qq * qq);
+        const R beta = c.dw2 * dz + c.dw3;
+        const R t = dxy / beta;
+        total = total + (-alpha * g_exp(R(-0.5) * (t * t)));
+      }
+    }
+  }
+  return total;
+}
+
+}  // namespace gpd

@@ -1,0 +1,224 @@
+"""Batched aviary on one GPU: the Python owner of a ``gpd_sim`` (include/gpd.h).
+
+``BatchedAviarySim`` holds the device state of ``n_envs`` identical aviaries (each with
+``drones_per_env`` drones) and the caller-visible I/O buffers (torch tensors in HBM).  Every
+call enqueues HIP work on the current torch stream of the sim's device; nothing here
+computes physics on the CPU.
+"""
+import ctypes
+import warnings
+
+import numpy as np
+import torch
+
+from . import _lib
+from .assets import default_params, model_id, parse_urdf
+from .enums import ActionType, DroneModel, Physics
+
+_TASKS = {"none": _lib.GPD_TASK_NONE, "hover": _lib.GPD_TASK_HOVER, "multihover": _lib.GPD_TASK_MULTIHOVER}
+_AERO = {"gnd": _lib.GPD_F_GND, "drag": _lib.GPD_F_DRAG, "dw": _lib.GPD_F_DW, "geom": _lib.GPD_F_GEOM_WRENCH}
+_PHYSICS = {
+    Physics.DYN: (),
+    Physics.PYB: ("geom",),
+    Physics.PYB_GND: ("geom", "gnd"),
+    Physics.PYB_DRAG: ("geom", "drag"),
+    Physics.PYB_DW: ("geom", "dw"),
+    Physics.PYB_GND_DRAG_DW: ("geom", "gnd", "drag", "dw"),
+}
+_warned_pyb = False
+
+
+def physics_flags(physics=Physics.DYN, aero=()):
+    """Map a reference ``Physics`` value (+ extra force terms) to GPD_F_* flags.
+
+    DYN is the reference's explicit integrator (BaseAviary.py:352-353).  The PYB* values are
+    served by the same explicit integrator with the PYB force placement (``_physics``
+    :679-711) and the requested aero terms; Bullet's own integrator/contact is
+    not reproduced, which is reported once with a warning.
+    """
+    global _warned_pyb
+    physics = Physics(physics)
+    terms = set(_PHYSICS[physics]) | set(aero)
+    unknown = terms - set(_AERO)
+    if unknown:
+        raise ValueError(f"unknown aero terms {sorted(unknown)}; expected a subset of {sorted(_AERO)}")
+    if physics != Physics.DYN and not _warned_pyb:
+        warnings.warn(f"{physics}: forces follow BaseAviary._physics/_groundEffect/_drag/_downwash but are "
+                      "integrated by the explicit DYN integrator (no Bullet damping/contact)", stacklevel=3)
+        _warned_pyb = True
+    flags = 0
+    for t in terms:
+        flags |= _AERO[t]
+    return flags
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class BatchedAviarySim:
+    """``n_envs`` x ``drones_per_env`` Crazyflie-class drones stepped in lockstep on one GPU."""
+
+    def __init__(self, n_envs, drones_per_env=1, drone_model=DroneModel.CF2X, urdf_path=None,
+                 pyb_freq=240, ctrl_freq=30, act=ActionType.RPM, task="hover",
+                 physics=Physics.DYN, aero=(), precision="f32", autoreset=True, episode_len_sec=8,
+                 initial_xyzs=None, initial_rpys=None, device=None):
+        self._lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise _lib.GpdLibraryError("BatchedAviarySim needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
+        act = ActionType(act)
+        if act not in (ActionType.RPM, ActionType.ONE_D_RPM):
+            raise NotImplementedError(f"{act} needs the PID controller (SURVEY §8 f2), not on this path")
+        if precision not in ("f32", "f64"):
+            raise ValueError("precision must be 'f32' or 'f64'")
+        self.drone_model = DroneModel(drone_model)
+        self.params = parse_urdf(urdf_path, self.drone_model) if urdf_path else default_params(self.drone_model)
+        self.params.model = model_id(self.drone_model)
+        self.n_envs, self.drones_per_env = int(n_envs), int(drones_per_env)
+        self.act_type = act
+        self.task = task
+        self.precision = precision
+        self.real_dtype = torch.float32 if precision == "f32" else torch.float64
+        cfg = _lib.Config()
+        cfg.n_envs = self.n_envs
+        cfg.drones_per_env = self.drones_per_env
+        cfg.pyb_freq = int(pyb_freq)
+        cfg.ctrl_freq = int(ctrl_freq)
+        cfg.act_type = _lib.GPD_ACT_RPM if act == ActionType.RPM else _lib.GPD_ACT_ONE_D_RPM
+        cfg.task = _TASKS[task]
+        cfg.physics_flags = physics_flags(physics, aero)
+        cfg.precision = _lib.GPD_F32 if precision == "f32" else _lib.GPD_F64
+        cfg.autoreset = 1 if autoreset else 0
+        cfg.episode_len_sec = float(episode_len_sec)
+        keep = []
+        for name, arr in (("init_xyzs_host", initial_xyzs), ("init_rpys_host", initial_rpys)):
+            if arr is not None:
+                a = np.ascontiguousarray(np.asarray(arr, dtype=np.float64).reshape(self.drones_per_env, 3))
+                keep.append(a)
+                setattr(cfg, name, a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        self.physics_flags = cfg.physics_flags
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check("gpd_create", self._lib.gpd_create(ctypes.byref(self.params), ctypes.byref(cfg),
+                                                          ctypes.byref(handle)))
+        self._h = handle
+        k = _lib.Constants()
+        _lib.check("gpd_get_constants", self._lib.gpd_get_constants(self._h, ctypes.byref(k)))
+        self.constants = k
+        self.n_drones = k.n_drones
+        self.obs_width = k.obs_width
+        self.act_width = k.act_width
+        self.pyb_steps_per_ctrl = k.pyb_steps_per_ctrl
+        E, D, W = self.n_envs, self.drones_per_env, self.obs_width
+        dev = self.device
+        self.obs = torch.zeros((E, D, W), dtype=torch.float32, device=dev)
+        self.terminal_obs = torch.zeros((E, D, W), dtype=torch.float32, device=dev)
+        self.reward = torch.zeros((E,), dtype=torch.float32, device=dev)
+        self.terminated = torch.zeros((E,), dtype=torch.uint8, device=dev)
+        self.truncated = torch.zeros((E,), dtype=torch.uint8, device=dev)
+        self.reset()
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.gpd_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _call(self, name, *args):
+        _lib.check(name, getattr(self._lib, name)(self._h, *args))
+
+    # ------------------------------------------------------------------ RL surface
+    def reset(self, env_mask=None):
+        """BaseAviary.reset (:220-255) for all envs or the envs where ``env_mask`` is true."""
+        m = None
+        if env_mask is not None:
+            m = torch.as_tensor(env_mask, device=self.device).to(torch.uint8).contiguous()
+            assert m.numel() == self.n_envs
+        with torch.cuda.device(self.device):
+            self._call("gpd_reset", _ptr(m), _ptr(self.obs), _stream(self.device))
+        return self.obs
+
+    def step(self, actions, terminal_obs=True):
+        """BaseAviary.step (:259-383) for every env; ``actions`` [E, D, A] float32 on the device.
+
+        Returns the sim-owned (obs, reward, terminated, truncated) tensors; they are
+        overwritten by the next call.  With autoreset, ``self.terminal_obs`` holds the final
+        rows of the envs that finished in this step."""
+        a = actions
+        if not (isinstance(a, torch.Tensor) and a.device == self.device and a.dtype == torch.float32
+                and a.is_contiguous()):
+            a = torch.as_tensor(a, dtype=torch.float32, device=self.device).contiguous()
+        if a.numel() != self.n_drones * self.act_width:
+            raise ValueError(f"actions must have {self.n_envs}x{self.drones_per_env}x{self.act_width} elements")
+        with torch.cuda.device(self.device):
+            self._call("gpd_step", _ptr(a), _ptr(self.obs), _ptr(self.reward), _ptr(self.terminated),
+                       _ptr(self.truncated), _ptr(self.terminal_obs) if terminal_obs else None,
+                       _stream(self.device))
+        return self.obs, self.reward, self.terminated, self.truncated
+
+    # ------------------------------------------------------------------ raw physics
+    def integrate(self, rpm, record=False):
+        """Raw DYN substeps: ``rpm`` [T, N, 4] (real dtype) -> optional trajectory [T, N, 20]."""
+        r = torch.as_tensor(rpm, dtype=self.real_dtype, device=self.device).contiguous()
+        T = r.shape[0]
+        assert r.numel() == T * self.n_drones * 4
+        traj = torch.empty((T, self.n_drones, 20), dtype=self.real_dtype, device=self.device) if record else None
+        with torch.cuda.device(self.device):
+            self._call("gpd_integrate", _ptr(r), int(T), _ptr(traj), _stream(self.device))
+        return traj
+
+    def state20(self):
+        """BaseAviary._getDroneStateVector (:541-561) for every drone, [N, 20]."""
+        out = torch.empty((self.n_drones, 20), dtype=self.real_dtype, device=self.device)
+        with torch.cuda.device(self.device):
+            self._call("gpd_get_state20", _ptr(out), _stream(self.device))
+        return out
+
+    def raw_state(self):
+        out = torch.empty((self.n_drones, 20), dtype=self.real_dtype, device=self.device)
+        with torch.cuda.device(self.device):
+            self._call("gpd_get_raw_state", _ptr(out), _stream(self.device))
+        return out
+
+    def set_raw_state(self, raw):
+        r = torch.as_tensor(raw, dtype=self.real_dtype, device=self.device).contiguous()
+        assert r.numel() == self.n_drones * 20
+        with torch.cuda.device(self.device):
+            self._call("gpd_set_raw_state", _ptr(r), _stream(self.device))
+
+    def step_counters(self):
+        out = torch.empty((self.n_envs,), dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            self._call("gpd_get_step_counters", _ptr(out), _stream(self.device))
+        return out
+
+    def set_step_counters(self, sc):
+        t = torch.as_tensor(sc, dtype=torch.int32, device=self.device).contiguous()
+        with torch.cuda.device(self.device):
+            self._call("gpd_set_step_counters", _ptr(t), _stream(self.device))
+
+    def save_state(self):
+        n = self._lib.gpd_state_bytes(self._h)
+        buf = ctypes.create_string_buffer(n)
+        with torch.cuda.device(self.device):
+            self._call("gpd_save_state", ctypes.cast(buf, ctypes.c_void_p), _stream(self.device))
+        return buf.raw
+
+    def load_state(self, blob):
+        n = self._lib.gpd_state_bytes(self._h)
+        if len(blob) != n:
+            raise ValueError(f"state blob has {len(blob)} bytes, expected {n}")
+        buf = ctypes.create_string_buffer(blob, n)
+        with torch.cuda.device(self.device):
+            self._call("gpd_load_state", ctypes.cast(buf, ctypes.c_void_p), _stream(self.device))

@@ -1,0 +1,170 @@
+/*
+ * gpd.h — C ABI of the MI355X-native batched quadrotor DYN path.
+ *
+ * This is the drop-in boundary for the reference's hot path (paths relative to the
+ * reference root, gym_pybullet_drones/):
+ *
+ *   gpd_create        <- BaseAviary.__init__            envs/BaseAviary.py:25-216
+ *                        (+ _parseURDFParameters :982-1014, derived constants :117-128,
+ *                           BaseRLAviary.__init__ action buffer envs/BaseRLAviary.py:66-67,
+ *                           HoverAviary TARGET_POS/EPISODE_LEN_SEC envs/HoverAviary.py:51-52,
+ *                           MultiHoverAviary TARGET_POS envs/MultiHoverAviary.py:71)
+ *   gpd_reset         <- BaseAviary.reset()             envs/BaseAviary.py:220-255
+ *                        (+ _housekeeping :451-505, readback :509-519, _computeObs
+ *                           envs/BaseRLAviary.py:284-319)
+ *   gpd_step          <- BaseAviary.step()              envs/BaseAviary.py:259-383, i.e.
+ *                        _preprocessAction (BaseRLAviary.py:160-239, RPM / ONE_D_RPM),
+ *                        PYB_STEPS_PER_CTRL x (_updateAndStoreKinematicInformation :509-519
+ *                        + _dynamics :815-874 + _integrateQ :876-889
+ *                        [+ _groundEffect :715-750, _drag :754-781, _downwash :785-811]),
+ *                        _computeObs / _computeReward / _computeTerminated /
+ *                        _computeTruncated (HoverAviary.py:68-117, MultiHoverAviary.py:75-130),
+ *                        plus SB3 VecEnv auto-reset (optional).
+ *   gpd_integrate     <- the raw _dynamics + readback substep (:815-889, :509-519) driven by
+ *                        explicit per-substep RPMs (parity / raw-integrator mode).
+ *   gpd_get_state20   <- BaseAviary._getDroneStateVector()  envs/BaseAviary.py:541-561
+ *
+ * Conventions
+ *   - All array arguments are DEVICE pointers (hipMalloc'd memory, e.g. a torch tensor's
+ *     data_ptr()) unless named *_host.  The caller owns every I/O buffer; the sim owns its
+ *     state.  No call allocates or synchronises except gpd_create / gpd_destroy /
+ *     gpd_save_state / gpd_load_state.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).  All work is
+ *     enqueued asynchronously on it.  Calls on one handle must be serialised by the caller.
+ *   - Drones are numbered env-major: drone n = env * drones_per_env + d.
+ *   - "real" below is float (GPD_F32) or double (GPD_F64), chosen at create time.
+ *   - Return value: GPD_OK (0) or a negative GPD_E* code; gpd_last_error() describes the
+ *     last failure of the calling thread.
+ */
+#ifndef GPD_H_
+#define GPD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPD_ABI_VERSION 1
+
+/* return codes */
+#define GPD_OK 0
+#define GPD_EINVAL (-1)       /* invalid argument / configuration (BaseAviary.py:79-80 ValueError) */
+#define GPD_EHIP (-2)         /* HIP runtime error */
+#define GPD_ENOMEM (-3)       /* device allocation failed */
+#define GPD_EUNSUPPORTED (-4) /* valid in the reference, not on this path (e.g. PID actions) */
+
+/* DroneModel (utils/enums.py:3-8) */
+#define GPD_MODEL_CF2X 0
+#define GPD_MODEL_CF2P 1
+#define GPD_MODEL_RACE 2
+
+/* ActionType subset on this path (utils/enums.py:35-41; BaseRLAviary.py:191-192, 224-225) */
+#define GPD_ACT_RPM 0
+#define GPD_ACT_ONE_D_RPM 1
+
+/* Task hooks (reward / terminated / truncated) */
+#define GPD_TASK_NONE 0       /* raw aviary: reward -1, never done (CtrlAviary-like) */
+#define GPD_TASK_HOVER 1      /* HoverAviary.py:68-117 */
+#define GPD_TASK_MULTIHOVER 2 /* MultiHoverAviary.py:75-130 */
+
+/* physics flags: force terms added to the explicit integrator (Physics enum utils/enums.py:13-21) */
+#define GPD_F_GND 1           /* _groundEffect  BaseAviary.py:715-750 */
+#define GPD_F_DRAG 2          /* _drag          BaseAviary.py:754-781 */
+#define GPD_F_DW 4            /* _downwash      BaseAviary.py:785-811 */
+#define GPD_F_GEOM_WRENCH 8   /* prop thrust torque from URDF prop positions (_physics :679-711)
+                                 instead of the DYN formula (:846-851) */
+
+/* precision */
+#define GPD_F32 0
+#define GPD_F64 1
+
+/* Drone model parameters (the URDF <properties>, inertial and prop-link values parsed by
+ * BaseAviary._parseURDFParameters, BaseAviary.py:982-1014). */
+typedef struct gpd_drone_params {
+  int model;                 /* GPD_MODEL_* (selects the DYN torque formula, :843-851) */
+  double m, arm, thrust2weight, ixx, iyy, izz, kf, km;
+  double collision_h, collision_r, collision_z_offset, max_speed_kmh;
+  double gnd_eff_coeff, prop_radius, drag_coeff_xy, drag_coeff_z;
+  double dw_coeff_1, dw_coeff_2, dw_coeff_3;
+  double prop_pos[4][3];     /* prop link inertial origins (cf2x.urdf:42,54,66,78) */
+} gpd_drone_params;
+
+typedef struct gpd_config {
+  int n_envs;                /* E >= 1 */
+  int drones_per_env;        /* D in [1, 64] (HoverAviary: 1) */
+  int pyb_freq;              /* PYB_FREQ, default 240 */
+  int ctrl_freq;             /* CTRL_FREQ, must divide pyb_freq (HoverAviary default 30) */
+  int act_type;              /* GPD_ACT_* */
+  int task;                  /* GPD_TASK_* */
+  int physics_flags;         /* OR of GPD_F_* */
+  int precision;             /* GPD_F32 or GPD_F64 */
+  int autoreset;             /* 1: done envs are reset inside gpd_step (SB3 VecEnv semantics) */
+  double episode_len_sec;    /* EPISODE_LEN_SEC (8 for both tasks) */
+  const double* init_xyzs_host; /* [D][3] INIT_XYZS shared by all envs, NULL = default (:194-197) */
+  const double* init_rpys_host; /* [D][3] INIT_RPYS, NULL = zeros */
+} gpd_config;
+
+/* Derived constants, BaseAviary.py:117-128 (read-only view for tests/facades). */
+typedef struct gpd_constants {
+  double gravity, hover_rpm, max_rpm, max_thrust, max_xy_torque, max_z_torque, gnd_eff_h_clip;
+  double pyb_timestep, ctrl_timestep;
+  int pyb_steps_per_ctrl, action_buffer_size, obs_width, act_width, n_drones;
+  int trunc_step_counter;    /* smallest step_counter with step_counter/PYB_FREQ > EPISODE_LEN_SEC */
+} gpd_constants;
+
+typedef struct gpd_sim gpd_sim;
+
+int gpd_abi_version(void);
+const char* gpd_last_error(void);
+
+/* Fill `out` with the built-in parameters of a drone model (cf2x/cf2p/racer URDF values). */
+int gpd_default_params(int model, gpd_drone_params* out);
+
+/* Create a batched aviary on the CURRENT HIP device; state is initialised as after reset()
+ * and the action ring (15 = ctrl_freq//2 slots) is zero, as BaseRLAviary._actionSpace leaves it. */
+int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** out);
+int gpd_destroy(gpd_sim* sim);
+int gpd_get_constants(const gpd_sim* sim, gpd_constants* out);
+
+/* reset(): envs with env_mask[e] != 0 (env_mask == NULL: all envs) go back to INIT_XYZS /
+ * INIT_RPYS with zero velocities, step_counter 0, last_clipped_action 0.  The action ring is
+ * NOT cleared (the reference never clears action_buffer).  If obs != NULL the reset
+ * observation rows [E][D][obs_width] float of the reset envs are written. */
+int gpd_reset(gpd_sim* sim, const uint8_t* env_mask, float* obs, void* stream);
+
+/* step(action): actions [E][D][act_width] float in, obs [E][D][obs_width] float,
+ * reward [E] float, terminated/truncated [E] uint8 out.  With autoreset, done envs are reset
+ * after their terminal row is copied to terminal_obs [E][D][obs_width] (if non-NULL; rows of
+ * envs that are not done are left untouched) and obs holds the reset observation. */
+int gpd_step(gpd_sim* sim, const float* actions, float* obs, float* reward,
+             uint8_t* terminated, uint8_t* truncated, float* terminal_obs, void* stream);
+
+/* Raw DYN integrator: n_sub substeps, row t of rpm [n_sub][N][4] (real) drives substep t of
+ * every drone; each substep is followed by the readback (PYB_STEPS_PER_CTRL = 1 cadence).
+ * traj (nullable) receives the 20-float state after every substep, [n_sub][N][20] real. */
+int gpd_integrate(gpd_sim* sim, const void* rpm, int n_sub, void* traj, void* stream);
+
+/* 20-float state vectors [N][20] real (BaseAviary.py:541-561). */
+int gpd_get_state20(gpd_sim* sim, void* out, void* stream);
+
+/* Raw per-drone state [N][20] real = pos(3) quat_xyzw as stored by the physics client (4)
+ * vel(3) rpy_rates(3) ang_v_world(3) last_clipped_action(4).  Used for checkpoints and to
+ * seed arbitrary initial conditions. */
+int gpd_get_raw_state(gpd_sim* sim, void* out, void* stream);
+int gpd_set_raw_state(gpd_sim* sim, const void* in, void* stream);
+/* step counters [E] int32 */
+int gpd_get_step_counters(gpd_sim* sim, int32_t* out, void* stream);
+int gpd_set_step_counters(gpd_sim* sim, const int32_t* in, void* stream);
+
+/* Whole-sim checkpoint (state, action ring, ring head, step counters) to/from host memory.
+ * gpd_state_bytes gives the blob size.  These synchronise `stream`. */
+size_t gpd_state_bytes(const gpd_sim* sim);
+int gpd_save_state(gpd_sim* sim, void* blob_host, void* stream);
+int gpd_load_state(gpd_sim* sim, const void* blob_host, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPD_H_ */

@@ -1,0 +1,53 @@
+"""Helpers that drive the CPU oracle (oracle/) the way the GPU path is driven.
+
+Test infrastructure only.  ``run_vec`` reproduces SB3 DummyVecEnv auto-reset semantics on a
+list of reference-shaped envs: when an env finishes, its last obs becomes the terminal
+observation and the returned obs is the reset observation.
+"""
+import numpy as np
+
+from oracle.ref_aviary import RefAviary
+
+
+def state_rel_err(a, b):
+    """Per-drone relative L2 error of the state (SURVEY §8(d) gate): pos, quat (sign
+    canonicalised to w >= 0), rpy, vel, ang_v - columns 0..15 of the 20-float state vector.
+    The last_clipped_action columns (16..19) are inputs, not integrated state, and are left out
+    so that their ~1.4e4 magnitude cannot hide errors."""
+    a = np.array(a, dtype=np.float64)[..., :16]
+    b = np.array(b, dtype=np.float64)[..., :16]
+    for x in (a, b):
+        s = np.where(x[..., 6:7] < 0, -1.0, 1.0)
+        x[..., 3:7] *= s
+    num = np.linalg.norm(a - b, axis=-1)
+    den = np.maximum(np.linalg.norm(b, axis=-1), 1e-6)
+    return num / den
+
+
+def run_integrate(rpms, raw0=None, **kw):
+    """Oracle trajectory for rpm [T, N, 4]; one RefAviary holding all N drones (no downwash
+    unless requested, so drones are independent)."""
+    T, N, _ = rpms.shape
+    env = RefAviary(num_drones=N, task="none", **kw)
+    if raw0 is not None:
+        env.set_raw_state(raw0)
+    return env.integrate(rpms)
+
+
+def run_vec(actions, n_envs, drones_per_env=1, act="rpm", task="hover", **kw):
+    """actions [T, E, D, A] float32 -> obs [T, E, D, W], reward [T, E], term/trunc [T, E],
+    terminal obs dict {(t, e): [D, W]}."""
+    envs = [RefAviary(num_drones=drones_per_env, act=act, task=task, **kw) for _ in range(n_envs)]
+    T = actions.shape[0]
+    obs_l, rew, te, tr, term_obs = [], np.zeros((T, n_envs)), np.zeros((T, n_envs), bool), np.zeros((T, n_envs), bool), {}
+    for t in range(T):
+        row = []
+        for e, env in enumerate(envs):
+            o, r, a_t, b_t, _ = env.step(actions[t, e])
+            rew[t, e], te[t, e], tr[t, e] = r, a_t, b_t
+            if a_t or b_t:
+                term_obs[(t, e)] = o
+                o, _ = env.reset()
+            row.append(o)
+        obs_l.append(np.stack(row))
+    return np.stack(obs_l), rew, te, tr, term_obs
