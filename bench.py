@@ -86,8 +86,31 @@ def cpu_baseline(seconds=10.0, act="rpm"):
                       "BaseAviary.step without pybullet call overhead (flatters the reference)"}
 
 
+def time_graph(sim, pool, steps, warmup, per_graph=16):
+    """Timed region in hipGraph mode: one graph = `per_graph` consecutive env.step() launches
+    reading distinct pre-filled action slots; returns (wall seconds, steps actually run)."""
+    P = pool.shape[0]
+    graph = sim.capture_graph([pool[k % P] for k in range(per_graph)])
+    reps = max(1, steps // per_graph)
+    for _ in range(max(1, warmup // per_graph)):
+        graph.replay()
+    torch.cuda.synchronize(sim.device)
+    if torch.distributed.is_initialized():
+        torch.distributed.barrier()
+    torch.cuda.synchronize(sim.device)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        graph.replay()
+    torch.cuda.synchronize(sim.device)
+    wall = time.perf_counter() - t0
+    if torch.distributed.is_initialized():
+        torch.distributed.barrier()
+    return wall, reps * per_graph
+
+
 def time_steps(sim, pool, steps, warmup):
-    """Run warmup + timed steps; returns (wall seconds, mean kernel us)."""
+    """Eager launches with a HIP event pair around every gpd_step on the launch stream;
+    returns (wall seconds, mean kernel us)."""
     P = pool.shape[0]
     for k in range(warmup):
         sim.step(pool[k % P])
@@ -128,6 +151,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="time eager launches instead of hipGraph replays")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -149,14 +173,20 @@ def main():
                            autoreset=True, device=device)
     nsub = sim.pyb_steps_per_ctrl
     pool = make_pool(E, A, device, seed=1000 + rank)
-    wall, kern_us = time_steps(sim, pool, args.steps, args.warmup)
+    # (1) eager pass: per-launch HIP events give the step kernel's duration (roofline)
+    eager_wall, kern_us = time_steps(sim, pool, args.steps, args.warmup)
+    # (2) timed pass: the same steps replayed from a hipGraph (no host launch overhead)
+    if args.eager:
+        wall, steps_run = eager_wall, args.steps
+    else:
+        wall, steps_run = time_graph(sim, pool, args.steps, args.warmup)
     if world > 1:
-        t = torch.tensor([wall], device=device, dtype=torch.float64)
+        t = torch.tensor([wall, eager_wall], device=device, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        wall = float(t.item())
-    drone_dt = world * E * nsub * args.steps
+        wall, eager_wall = float(t[0].item()), float(t[1].item())
+    drone_dt = world * E * nsub * steps_run
     value = drone_dt / wall
-    ms_per_step = 1000.0 * wall / args.steps
+    ms_per_step = 1000.0 * wall / steps_run
     rbytes = 8 if args.precision == "f64" else 4
     alg = alg_bytes_per_drone_step(args.act, rbytes) * E
     achieved = alg / (kern_us * 1e-6) / 1e9
@@ -165,11 +195,14 @@ def main():
         "value": value, "unit": "drone*dt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f32" if args.precision == "f32" else "f64", "data": "synthetic",
+        "mode": "eager launches" if args.eager else "hipGraph replay, 16 env.step launches per graph",
         "config": {"workload": f"{E} HoverAviary envs per GPU (cf2x, Physics.DYN, ActionType.{args.act.upper()}, "
                                f"240/30 Hz = {nsub} substeps/step, U[-1,1] actions, SB3 auto-reset)",
                    "n_envs_per_gpu": E, "global_envs": E * world, "drones_per_env": 1,
                    "parallelism": f"env-sharded x{world} (no collective in the step loop)"},
         "kernel_us": kern_us,
+        "eager": {"ms_per_step": 1000.0 * eager_wall / args.steps,
+                  "value": world * E * nsub * args.steps / eager_wall},
         "ctrl_steps_per_s": world * E * args.steps / wall,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
@@ -193,7 +226,8 @@ def main():
         gw = torch.tensor([time.perf_counter() - t0], device=device, dtype=torch.float64)
         torch.distributed.all_reduce(gw, op=torch.distributed.ReduceOp.MAX)
         gw = float(gw.item())
-        result["gather"] = {"ms_per_step": 1000 * gw / G, "value": world * E * nsub * G / gw,
+        result["gather"] = {"mode": "eager step + RCCL all_gather of obs and reward per step",
+                            "ms_per_step": 1000 * gw / G, "value": world * E * nsub * G / gw,
                             "bytes_per_step": int(obs_all.numel() * 4 + rew_all.numel() * 4)}
 
     if rank == 0 and world == 1 and not args.no_sweep:

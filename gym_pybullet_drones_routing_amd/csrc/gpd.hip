@@ -100,10 +100,11 @@ struct gpd_sim {
   long long npad;
   void* d_state = nullptr;
   float* d_ring = nullptr;
-  int32_t* d_steps = nullptr;
+  int2* d_ctr = nullptr;          // [E] {step_counter, ring head}
   void* d_init = nullptr;
   void* d_target = nullptr;
-  int head = 0;  // ring slot receiving the next action (global: all envs step in lockstep)
+  void* d_consts = nullptr;       // Consts<real> in device memory
+  int tile_bytes = 0;             // dynamic LDS of the step kernel
   double bound_xy;
   std::vector<double> init_tmpl;  // [D][10]
   std::vector<double> target;     // [D][3]
@@ -131,6 +132,8 @@ Consts<R> make_consts(const gpd_sim* s) {
   c.drag_z = (R)P.drag_coeff_z;
   c.two_pi = (R)(2.0 * M_PI);
   c.dw1 = (R)P.dw_coeff_1; c.dw2 = (R)P.dw_coeff_2; c.dw3 = (R)P.dw_coeff_3;
+  c.inv_m = (R)(1.0 / P.m);
+  c.rpm2rad = (R)(2.0 * M_PI / 60.0);
   for (int k = 0; k < 4; ++k) {
     c.rx[k] = (R)P.prop_pos[k][0];
     c.ry[k] = (R)P.prop_pos[k][1];
@@ -148,7 +151,7 @@ SimView<R> make_view(const gpd_sim* s) {
   SimView<R> v;
   v.state = (R*)s->d_state;
   v.ring = s->d_ring;
-  v.steps = s->d_steps;
+  v.ctr = s->d_ctr;
   v.init = (const R*)s->d_init;
   v.target = (const R*)s->d_target;
   v.npad = s->npad;
@@ -164,8 +167,17 @@ template <typename R>
 int upload_tables(gpd_sim* s) {
   std::vector<R> ini(s->init_tmpl.begin(), s->init_tmpl.end());
   std::vector<R> tgt(s->target.begin(), s->target.end());
+  const Consts<R> c = make_consts<R>(s);
   HIP_TRY(hipMemcpy(s->d_init, ini.data(), ini.size() * sizeof(R), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(s->d_target, tgt.data(), tgt.size() * sizeof(R), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s->d_consts, &c, sizeof(c), hipMemcpyHostToDevice));
+  // the observation tile can exceed the 64 KiB default dynamic-LDS limit for long histories
+  if (s->tile_bytes > 65536) {
+    const void* fns[4] = {(const void*)step_kernel<R, 4, true>, (const void*)step_kernel<R, 4, false>,
+                          (const void*)step_kernel<R, 1, true>, (const void*)step_kernel<R, 1, false>};
+    for (const void* f : fns)
+      HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, s->tile_bytes));
+  }
   return GPD_OK;
 }
 
@@ -178,27 +190,27 @@ int launch_step(gpd_sim* s, const float* actions, float* obs, float* reward, uin
                 float* terminal_obs, hipStream_t st) {
   StepIO<R> io;
   io.actions = actions; io.obs = obs; io.reward = reward; io.term = term; io.trunc = trunc;
-  io.terminal_obs = terminal_obs; io.head = s->head;
+  io.terminal_obs = terminal_obs;
   const SimView<R> v = make_view<R>(s);
-  const Consts<R> c = make_consts<R>(s);
+  const Consts<R>* c = (const Consts<R>*)s->d_consts;
   const unsigned grid = grid_for(s->N, s->tpb);
   const bool multi = s->D > 1;
+  const size_t lds = (size_t)s->tile_bytes;
   if (s->A == 4) {
-    if (multi) hipLaunchKernelGGL((step_kernel<R, 4, true>), dim3(grid), dim3(kWave), 0, st, v, io, c);
-    else hipLaunchKernelGGL((step_kernel<R, 4, false>), dim3(grid), dim3(kWave), 0, st, v, io, c);
+    if (multi) hipLaunchKernelGGL((step_kernel<R, 4, true>), dim3(grid), dim3(kWave), lds, st, v, io, c);
+    else hipLaunchKernelGGL((step_kernel<R, 4, false>), dim3(grid), dim3(kWave), lds, st, v, io, c);
   } else {
-    if (multi) hipLaunchKernelGGL((step_kernel<R, 1, true>), dim3(grid), dim3(kWave), 0, st, v, io, c);
-    else hipLaunchKernelGGL((step_kernel<R, 1, false>), dim3(grid), dim3(kWave), 0, st, v, io, c);
+    if (multi) hipLaunchKernelGGL((step_kernel<R, 1, true>), dim3(grid), dim3(kWave), lds, st, v, io, c);
+    else hipLaunchKernelGGL((step_kernel<R, 1, false>), dim3(grid), dim3(kWave), lds, st, v, io, c);
   }
   HIP_TRY(hipGetLastError());
-  s->head = (s->head + 1) % s->ring_len;
   return GPD_OK;
 }
 
 template <typename R>
 int launch_integrate(gpd_sim* s, const void* rpm, int n_sub, void* traj, hipStream_t st) {
   const SimView<R> v = make_view<R>(s);
-  const Consts<R> c = make_consts<R>(s);
+  const Consts<R>* c = (const Consts<R>*)s->d_consts;
   const unsigned grid = grid_for(s->N, s->tpb);
   if (s->D > 1)
     hipLaunchKernelGGL((integrate_kernel<R, true>), dim3(grid), dim3(kWave), 0, st, v, c, (const R*)rpm, n_sub, (R*)traj);
@@ -211,7 +223,7 @@ int launch_integrate(gpd_sim* s, const void* rpm, int n_sub, void* traj, hipStre
 template <typename R>
 int launch_reset(gpd_sim* s, const uint8_t* mask, float* obs, hipStream_t st) {
   const SimView<R> v = make_view<R>(s);
-  hipLaunchKernelGGL((reset_kernel<R>), dim3(grid_for(s->N, 256)), dim3(256), 0, st, v, mask, obs, s->head);
+  hipLaunchKernelGGL((reset_kernel<R>), dim3(grid_for(s->N, 256)), dim3(256), 0, st, v, mask, obs);
   HIP_TRY(hipGetLastError());
   return GPD_OK;
 }
@@ -236,9 +248,10 @@ void free_sim(gpd_sim* s) {
   if (!s) return;
   if (s->d_state) (void)hipFree(s->d_state);
   if (s->d_ring) (void)hipFree(s->d_ring);
-  if (s->d_steps) (void)hipFree(s->d_steps);
+  if (s->d_ctr) (void)hipFree(s->d_ctr);
   if (s->d_init) (void)hipFree(s->d_init);
   if (s->d_target) (void)hipFree(s->d_target);
+  if (s->d_consts) (void)hipFree(s->d_consts);
   delete s;
 }
 
@@ -326,6 +339,11 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   s->tpb = (kWave / s->D) * s->D;
   s->npad = ((long long)s->N + 63) / 64 * 64;
   s->bound_xy = C.task == GPD_TASK_MULTIHOVER ? 2.0 : 1.5;
+  s->tile_bytes = step_tile_bytes(s->A, s->ring_len);
+  if (s->tile_bytes > 160 * 1024) {
+    delete s;
+    return fail(GPD_EUNSUPPORTED, "gpd_create: ctrl_freq too high (observation tile exceeds 160 KiB of LDS)");
+  }
 
   // derived constants (BaseAviary.py:117-128)
   const gpd_drone_params& P = *params;
@@ -390,10 +408,12 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   const size_t rs = real_size(s);
   hipError_t e1 = hipMalloc(&s->d_state, (size_t)kStateComps * s->npad * rs);
   hipError_t e2 = hipMalloc((void**)&s->d_ring, (size_t)s->ring_len * s->npad * s->A * sizeof(float));
-  hipError_t e3 = hipMalloc((void**)&s->d_steps, (size_t)s->E * sizeof(int32_t));
+  hipError_t e3 = hipMalloc((void**)&s->d_ctr, (size_t)s->E * sizeof(int2));
   hipError_t e4 = hipMalloc(&s->d_init, (size_t)s->D * 10 * rs);
   hipError_t e5 = hipMalloc(&s->d_target, (size_t)s->D * 3 * rs);
-  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess) {
+  hipError_t e6 = hipMalloc(&s->d_consts, s->prec == GPD_F64 ? sizeof(Consts<double>) : sizeof(Consts<float>));
+  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess ||
+      e6 != hipSuccess) {
     free_sim(s);
     (void)hipGetLastError();
     return fail(GPD_ENOMEM, "gpd_create: hipMalloc failed");
@@ -402,7 +422,7 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   if (rc != GPD_OK) { free_sim(s); return rc; }
   if (hipMemset(s->d_state, 0, (size_t)kStateComps * s->npad * rs) != hipSuccess ||
       hipMemset(s->d_ring, 0, (size_t)s->ring_len * s->npad * s->A * sizeof(float)) != hipSuccess ||
-      hipMemset(s->d_steps, 0, (size_t)s->E * sizeof(int32_t)) != hipSuccess) {
+      hipMemset(s->d_ctr, 0, (size_t)s->E * sizeof(int2)) != hipSuccess) {
     free_sim(s);
     return fail(GPD_EHIP, "gpd_create: hipMemset failed");
   }
@@ -474,37 +494,37 @@ int gpd_set_raw_state(gpd_sim* sim, const void* in, void* stream) {
 
 int gpd_get_step_counters(gpd_sim* sim, int32_t* out, void* stream) {
   if (!sim || !out) return fail(GPD_EINVAL, "gpd_get_step_counters: NULL argument");
-  HIP_TRY(hipMemcpyAsync(out, sim->d_steps, (size_t)sim->E * sizeof(int32_t), hipMemcpyDeviceToDevice,
-                         (hipStream_t)stream));
+  HIP_TRY(hipMemcpy2DAsync(out, sizeof(int32_t), sim->d_ctr, sizeof(int2), sizeof(int32_t), (size_t)sim->E,
+                           hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return GPD_OK;
 }
 
 int gpd_set_step_counters(gpd_sim* sim, const int32_t* in, void* stream) {
   if (!sim || !in) return fail(GPD_EINVAL, "gpd_set_step_counters: NULL argument");
-  HIP_TRY(hipMemcpyAsync(sim->d_steps, in, (size_t)sim->E * sizeof(int32_t), hipMemcpyDeviceToDevice,
-                         (hipStream_t)stream));
+  HIP_TRY(hipMemcpy2DAsync(sim->d_ctr, sizeof(int2), in, sizeof(int32_t), sizeof(int32_t), (size_t)sim->E,
+                           hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return GPD_OK;
 }
 
 size_t gpd_state_bytes(const gpd_sim* sim) {
   if (!sim) return 0;
   return 16 + (size_t)kStateComps * sim->npad * real_size(sim) +
-         (size_t)sim->ring_len * sim->npad * sim->A * sizeof(float) + (size_t)sim->E * sizeof(int32_t);
+         (size_t)sim->ring_len * sim->npad * sim->A * sizeof(float) + (size_t)sim->E * sizeof(int2);
 }
 
 int gpd_save_state(gpd_sim* sim, void* blob_host, void* stream) {
   if (!sim || !blob_host) return fail(GPD_EINVAL, "gpd_save_state: NULL argument");
   hipStream_t st = (hipStream_t)stream;
   char* b = (char*)blob_host;
-  int64_t hdr[2] = {(int64_t)sim->head, (int64_t)sim->N};
+  int64_t hdr[2] = {(int64_t)GPD_ABI_VERSION, (int64_t)sim->N};
   std::memcpy(b, hdr, 16);
   size_t off = 16;
   const size_t s1 = (size_t)kStateComps * sim->npad * real_size(sim);
   const size_t s2 = (size_t)sim->ring_len * sim->npad * sim->A * sizeof(float);
-  const size_t s3 = (size_t)sim->E * sizeof(int32_t);
+  const size_t s3 = (size_t)sim->E * sizeof(int2);
   HIP_TRY(hipMemcpyAsync(b + off, sim->d_state, s1, hipMemcpyDeviceToHost, st)); off += s1;
   HIP_TRY(hipMemcpyAsync(b + off, sim->d_ring, s2, hipMemcpyDeviceToHost, st)); off += s2;
-  HIP_TRY(hipMemcpyAsync(b + off, sim->d_steps, s3, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(b + off, sim->d_ctr, s3, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   return GPD_OK;
 }
@@ -515,17 +535,16 @@ int gpd_load_state(gpd_sim* sim, const void* blob_host, void* stream) {
   const char* b = (const char*)blob_host;
   int64_t hdr[2];
   std::memcpy(hdr, b, 16);
-  if (hdr[1] != sim->N || hdr[0] < 0 || hdr[0] >= sim->ring_len)
+  if (hdr[1] != sim->N || hdr[0] != GPD_ABI_VERSION)
     return fail(GPD_EINVAL, "gpd_load_state: blob does not match this sim");
   size_t off = 16;
   const size_t s1 = (size_t)kStateComps * sim->npad * real_size(sim);
   const size_t s2 = (size_t)sim->ring_len * sim->npad * sim->A * sizeof(float);
-  const size_t s3 = (size_t)sim->E * sizeof(int32_t);
+  const size_t s3 = (size_t)sim->E * sizeof(int2);
   HIP_TRY(hipMemcpyAsync(sim->d_state, b + off, s1, hipMemcpyHostToDevice, st)); off += s1;
   HIP_TRY(hipMemcpyAsync(sim->d_ring, b + off, s2, hipMemcpyHostToDevice, st)); off += s2;
-  HIP_TRY(hipMemcpyAsync(sim->d_steps, b + off, s3, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(sim->d_ctr, b + off, s3, hipMemcpyHostToDevice, st));
   HIP_TRY(hipStreamSynchronize(st));
-  sim->head = (int)hdr[0];
   return GPD_OK;
 }
 

@@ -1,8 +1,9 @@
 // gpd_device.h — per-drone DYN physics for gfx950, templated on the real type.
 //
 // One lane owns one drone for the whole launch: the raw state lives in VGPRs across all
-// PYB_STEPS_PER_CTRL substeps, the model constants arrive as kernel arguments (SGPRs), and
-// only the per-env neighbour positions (downwash) go through LDS.
+// PYB_STEPS_PER_CTRL substeps, the model constants are read through a uniform device pointer
+// (scalar loads into SGPRs, re-loaded rather than spilled), and only the per-env neighbour
+// positions (downwash), the reward reduction and the observation tile go through LDS.
 //
 // Every function cites the reference code it restates (paths relative to
 // gym_pybullet_drones/ in the reference) or the Bullet3 routine pybullet runs for it.
@@ -32,7 +33,7 @@ template <typename R> struct PiC;
 template <> struct PiC<float> { static constexpr float pi = 3.14159265358979323846f; };
 template <> struct PiC<double> { static constexpr double pi = 3.14159265358979323846; };
 
-// ---------------------------------------------------------------- model constants (kernel arg)
+// ---------------------------------------------------------------- model constants (device memory)
 enum : int { MODEL_CF2X = 0, MODEL_CF2P = 1, MODEL_RACE = 2 };
 enum : int { F_GND = 1, F_DRAG = 2, F_DW = 4, F_GEOM = 8 };
 
@@ -47,6 +48,8 @@ struct Consts {
   R drag_xy, drag_z, two_pi;               // :1009, 2*np.pi (:773)
   R dw1, dw2, dw3;                         // :1010-1012
   R rx[4], ry[4], rz[4];                   // prop link origins (cf2x.urdf:42,54,66,78)
+  R inv_m;                 // 1/M      (F/M as a multiply; differs from the division by <= 1 ulp)
+  R rpm2rad;               // 2*pi/60  (drag: sum(2*pi*rpm/60))
   float hover_f32;         // float32(HOVER_RPM) (numpy 1.x casting, BaseRLAviary.py:192)
   int model, flags, nsub;
 };
@@ -122,6 +125,62 @@ __device__ __forceinline__ void quat_readback(R x, R y, R z, R w, R qn[4]) {
   R m[9];
   quat_to_mat(x, y, z, w, m);
   mat_to_quat(m, qn);
+}
+
+// Fused readback + rotation matrix, the form the hot loop uses.  Mathematically identical to
+// quat_readback() followed by quat_to_mat(qn): Bullet's basis->quaternion conversion returns
+// q/|q| with the sign chosen so that w > 0 when trace(R) > 0, else so that the component of the
+// largest diagonal entry is positive, and mat(q/|q|) == mat(q) because setRotation divides by
+// |q|^2.  Computing it this way saves a second matrix build and a square-root branch per
+// substep; the results differ from the literal Bullet sequence only by rounding (~1 ulp).
+template <typename R>
+__device__ __forceinline__ void readback_fused(R x, R y, R z, R w, R qn[4], R m[9]) {
+  const R d = x * x + y * y + z * z + w * w;
+  const R s = R(2) / d;
+  const R xs = x * s, ys = y * s, zs = z * s;
+  const R wx = w * xs, wy = w * ys, wz = w * zs;
+  const R xx = x * xs, xy = x * ys, xz = x * zs;
+  const R yy = y * ys, yz = y * zs, zz = z * zs;
+  m[0] = R(1) - (yy + zz); m[1] = xy - wz;           m[2] = xz + wy;
+  m[3] = xy + wz;          m[4] = R(1) - (xx + zz);  m[5] = yz - wx;
+  m[6] = xz - wy;          m[7] = yz + wx;           m[8] = R(1) - (xx + yy);
+  const R trace = m[0] + m[4] + m[8];
+  R key;
+  if (trace > R(0)) {
+    key = w;
+  } else {
+    const int i = m[0] < m[4] ? (m[4] < m[8] ? 2 : 1) : (m[0] < m[8] ? 2 : 0);
+    key = i == 0 ? x : (i == 1 ? y : z);
+  }
+  R inv = R(1) / g_sqrt(d);
+  inv = key < R(0) ? -inv : inv;
+  qn[0] = x * inv; qn[1] = y * inv; qn[2] = z * inv; qn[3] = w * inv;
+}
+
+// sin/cos of the half rotation angle of _integrateQ (:887-888).  |theta| = |omega|*dt/2 is
+// small for all but violently tumbling drones, so a Taylor series (error < 1e-16 relative for
+// |theta| < 0.5 in double, < 1e-9 in float) replaces the library call there.
+__device__ __forceinline__ void small_sincos(double th, double& s, double& c) {
+  if (fabs(th) < 0.5) {
+    const double t2 = th * th;
+    s = th * (1.0 + t2 * (-1.0 / 6 + t2 * (1.0 / 120 + t2 * (-1.0 / 5040 + t2 * (1.0 / 362880 +
+             t2 * (-1.0 / 39916800 + t2 * (1.0 / 6227020800.0)))))));
+    c = 1.0 + t2 * (-0.5 + t2 * (1.0 / 24 + t2 * (-1.0 / 720 + t2 * (1.0 / 40320 + t2 * (-1.0 / 3628800 +
+             t2 * (1.0 / 479001600.0 + t2 * (-1.0 / 87178291200.0)))))));
+  } else {
+    s = sin(th);
+    c = cos(th);
+  }
+}
+__device__ __forceinline__ void small_sincos(float th, float& s, float& c) {
+  if (fabsf(th) < 0.5f) {
+    const float t2 = th * th;
+    s = th * (1.0f + t2 * (-1.0f / 6 + t2 * (1.0f / 120 + t2 * (-1.0f / 5040 + t2 * (1.0f / 362880)))));
+    c = 1.0f + t2 * (-0.5f + t2 * (1.0f / 24 + t2 * (-1.0f / 720 + t2 * (1.0f / 40320 + t2 * (-1.0f / 3628800)))));
+  } else {
+    s = sinf(th);
+    c = cosf(th);
+  }
 }
 
 // btQuaternion::getEulerZYX (pybullet getEulerFromQuaternion, BaseAviary.py:518).
@@ -215,8 +274,7 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R 
   // R·(0,0,fz) - (0,0,GRAVITY) [+ drag]                 :839-841
   R Fx = Rm[2] * fz, Fy = Rm[5] * fz, Fz = Rm[8] * fz;
   if (c.flags & F_DRAG) {                              // _drag :773-774 with last_clipped_action
-    const R S = (((c.two_pi * last[0] / R(60) + c.two_pi * last[1] / R(60)) + c.two_pi * last[2] / R(60)) +
-                 c.two_pi * last[3] / R(60));
+    const R S = ((last[0] * c.rpm2rad + last[1] * c.rpm2rad) + last[2] * c.rpm2rad) + last[3] * c.rpm2rad;
     Fx = Fx + (-c.drag_xy * S) * s.vx;
     Fy = Fy + (-c.drag_xy * S) * s.vy;
     Fz = Fz + (-c.drag_z * S) * s.vz;
@@ -229,9 +287,9 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R 
   const R cz = s.wx * jwy - s.wy * jwx;
   const R dwx = c.ijx * (tx - cx), dwy = c.ijy * (ty - cy), dwz = c.ijz * (tz - cz);
   // semi-implicit Euler                                :855-859
-  s.vx = s.vx + c.dt * (Fx / c.m);
-  s.vy = s.vy + c.dt * (Fy / c.m);
-  s.vz = s.vz + c.dt * (Fz / c.m);
+  s.vx = s.vx + c.dt * (Fx * c.inv_m);
+  s.vy = s.vy + c.dt * (Fy * c.inv_m);
+  s.vz = s.vz + c.dt * (Fz * c.inv_m);
   s.wx = s.wx + c.dt * dwx;
   s.wy = s.wy + c.dt * dwy;
   s.wz = s.wz + c.dt * dwz;
@@ -242,8 +300,9 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R 
   const R p = s.wx, q = s.wy, r = s.wz;
   const R nrm = g_sqrt(p * p + q * q + r * r);
   if (nrm > R(1e-8)) {                                 // np.isclose(norm, 0): |norm| <= 1e-8
-    const R th = nrm * c.dt / R(2);
-    const R co = g_cos(th), si = g_sin(th);
+    const R th = nrm * c.dt * R(0.5);
+    R co, si;
+    small_sincos(th, si, co);
     const R k2 = R(2) / nrm;
     const R P = (k2 * (R(0.5) * p)) * si, Q = (k2 * (R(0.5) * q)) * si, Rr = (k2 * (R(0.5) * r)) * si;
     const R x = qn[0], y = qn[1], z = qn[2], w = qn[3];

@@ -2,28 +2,46 @@
 //
 // HBM layout (owned by the sim):
 //   state  real [20][npad]   SoA: pos(3) quat_raw(4) vel(3) rpy_rates(3) ang_v(3) last_rpm(4)
-//   ring   float[15][npad*A] action history ring (BaseRLAviary.action_buffer), global head
-//   steps  int32[E]          per-env step_counter
+//   ring   float[L][npad*A]  action history ring (BaseRLAviary.action_buffer),
+//                            L = ACTION_BUFFER_SIZE = ctrl_freq//2
+//   ctr    int2[E]           per-env {step_counter, ring head}: the head is the ring slot that
+//                            receives the env's next action.  All envs advance it in lockstep,
+//                            but keeping it per env (instead of a host-side launch argument)
+//                            makes gpd_step a fixed-argument launch that a hipGraph can replay.
 //   init   real [D][10]      per-drone reset template: pos(3) quat_raw(4) rpy(3)
 //   target real [D][3]       task target positions
-// One lane = one drone; one 64-lane block holds floor(64/D) whole envs so that the
+//   consts Consts<real>      model constants, read through a uniform pointer
+// One lane = one drone; one 64-lane block (one wave) holds floor(64/D) whole envs so that the
 // per-env exchange (downwash positions, reward/done reduction) stays inside a block.
+//
+// Observation rows are [E][D][W] row-major (W = 12 + L*A, the Gym layout).  A lane's row is W
+// floats, so writing rows straight from registers would scatter 16-byte pieces over 64
+// different cache lines per store instruction.  Instead the wave assembles its 64 rows in an
+// LDS tile stored column-major (tile[col][lane], one pad element per column so that the
+// transposed reads are bank-conflict free):
+//   * the L-1 history columns are DMA'd from the ring straight into the tile with
+//     global_load_lds at kernel start, so their HBM latency hides under the physics;
+//   * the 12 state columns and the current action are written from registers at the end;
+//   * the tile is then streamed out with fully coalesced 16-byte (A=4) / 4-byte (A=1) stores.
 #pragma once
 #include "gpd_device.h"
 
 namespace gpd {
 
 constexpr int kStateComps = 20;
-constexpr int kRing = 15;  // ACTION_BUFFER_SIZE = ctrl_freq//2 for the default 30 Hz; runtime value below
 constexpr int kWave = 64;
+constexpr int kPad = kWave + 1;  // tile column stride (elements)
 
 enum : int { TASK_NONE = 0, TASK_HOVER = 1, TASK_MULTIHOVER = 2 };
+
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+typedef __attribute__((address_space(1))) void* gbl_void_ptr;
 
 template <typename R>
 struct SimView {
   R* state;               // [20][npad]
   float* ring;            // [ring_len][npad*A]
-  int32_t* steps;         // [E]
+  int2* ctr;              // [E] {step_counter, ring head}
   const R* init;          // [D][10]
   const R* target;        // [D][3]
   long long npad;         // component stride of `state` (elements)
@@ -40,19 +58,30 @@ struct StepIO {
   uint8_t* term;          // [E]
   uint8_t* trunc;         // [E]
   float* terminal_obs;    // [N][W] or null
-  int head;               // ring slot receiving this step's action
 };
 
+// Only what the dynamics reads: ang_v is write-only, last_clipped_action is read only by drag.
 template <typename R>
-__device__ __forceinline__ void load_drone(const SimView<R>& v, long long n, Drone<R>& s, R last[4]) {
+__device__ __forceinline__ void load_drone(const SimView<R>& v, long long n, Drone<R>& s, R last[4], bool need_last) {
   const R* st = v.state;
   const long long p = v.npad;
   s.px = st[0 * p + n]; s.py = st[1 * p + n]; s.pz = st[2 * p + n];
   s.qx = st[3 * p + n]; s.qy = st[4 * p + n]; s.qz = st[5 * p + n]; s.qw = st[6 * p + n];
   s.vx = st[7 * p + n]; s.vy = st[8 * p + n]; s.vz = st[9 * p + n];
   s.wx = st[10 * p + n]; s.wy = st[11 * p + n]; s.wz = st[12 * p + n];
-  s.ax = st[13 * p + n]; s.ay = st[14 * p + n]; s.az = st[15 * p + n];
-  last[0] = st[16 * p + n]; last[1] = st[17 * p + n]; last[2] = st[18 * p + n]; last[3] = st[19 * p + n];
+  s.ax = s.ay = s.az = R(0);
+  if (need_last) {
+    last[0] = st[16 * p + n]; last[1] = st[17 * p + n]; last[2] = st[18 * p + n]; last[3] = st[19 * p + n];
+  } else {
+    last[0] = last[1] = last[2] = last[3] = R(0);
+  }
+}
+
+template <typename R>
+__device__ __forceinline__ void load_drone_full(const SimView<R>& v, long long n, Drone<R>& s, R last[4]) {
+  load_drone(v, n, s, last, true);
+  const long long p = v.npad;
+  s.ax = v.state[13 * p + n]; s.ay = v.state[14 * p + n]; s.az = v.state[15 * p + n];
 }
 
 template <typename R>
@@ -73,8 +102,7 @@ template <typename R, bool MULTI>
 __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const R last[4], const Consts<R>& c,
                                               R* sx, R* sy, R* sz, int tid, int base, int D) {
   R qn[4], Rm[9];
-  quat_readback(s.qx, s.qy, s.qz, s.qw, qn);   // :346-347 -> :517
-  quat_to_mat(qn[0], qn[1], qn[2], qn[3], Rm); // :836
+  readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);  // :346-347 -> :517, :836
   R roll = R(0), pitch = R(0), yaw;
   if (c.flags & F_GND) quat_to_euler(qn, roll, pitch, yaw);  // self.rpy used by :742
   R dw = R(0);
@@ -87,28 +115,39 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
   dyn_substep(s, qn, Rm, roll, pitch, rpm, last, dw, c);
 }
 
+// Bytes of dynamic LDS the step kernel needs for its observation tile.
+__host__ __device__ inline int step_tile_bytes(int A, int ring_len) {
+  return A == 4 ? (3 + ring_len) * kPad * 16 : (12 + ring_len) * kPad * 4;
+}
+
 // ---------------------------------------------------------------------------------------
 // gpd_step: one env.step() for every env (BaseAviary.py:259-383) in ONE launch.
 template <typename R, int A, bool MULTI>
-__global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io, Consts<R> c) {
-  __shared__ R sx[2 * kWave], sy[2 * kWave], sz[2 * kWave];  // x2: inactive tail lanes may index past tpb
-  __shared__ float srew[2 * kWave], sdist[2 * kWave];
-  __shared__ int sflag[2 * kWave];
+__global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io, const Consts<R>* __restrict__ cp) {
+  extern __shared__ float4 tile4[];          // A == 4: [3+L][kPad] float4
+  float* tilef = reinterpret_cast<float*>(tile4);  // A == 1: [12+L][kPad] float
+  __shared__ R sx[MULTI ? 2 * kWave : 1], sy[MULTI ? 2 * kWave : 1], sz[MULTI ? 2 * kWave : 1];
+  __shared__ float srew[MULTI ? 2 * kWave : 1], sdist[MULTI ? 2 * kWave : 1];
+  __shared__ int sflag[MULTI ? 2 * kWave : 1];
+  const Consts<R>& c = *cp;
   const int tid = threadIdx.x;
   const int D = MULTI ? v.D : 1;
   const int d = MULTI ? tid % D : 0;
   const int base = tid - d;
-  const long long n = (long long)blockIdx.x * v.tpb + tid;
-  const bool active = tid < v.tpb && n < v.N;
+  const long long n0 = (long long)blockIdx.x * v.tpb;
+  const long long n = n0 + tid;
+  const int nact = (int)((v.N - n0) < v.tpb ? (v.N - n0) : v.tpb);  // drones owned by this block
+  const bool active = tid < nact;
   const long long nn = active ? n : 0;  // inactive lanes compute on drone 0 and store nothing
   const long long e = MULTI ? nn / D : nn;
+  const bool drag = (c.flags & F_DRAG) != 0;
 
   Drone<R> s;
   R last[4];
-  load_drone(v, nn, s, last);
-  const int sc = v.steps[e];
-
-  // _preprocessAction: action_buffer.append(action); rpm = HOVER_RPM*(1+0.05*a)
+  load_drone(v, nn, s, last, drag);
+  const int2 cv = v.ctr[e];
+  const int sc = cv.x;        // step_counter
+  const int head = cv.y;      // ring slot receiving this step's action
   float a[A];
   if (A == 4) {
     const float4 a4 = *reinterpret_cast<const float4*>(io.actions + nn * 4);
@@ -116,6 +155,22 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
   } else {
     a[0] = io.actions[nn];
   }
+
+  // ---- prefetch the L-1 oldest actions of the history ring into the tile (LDS-DMA); they are
+  //      only needed for the observation, so their latency hides under the substeps below.
+  const int nh = v.ring_len - 1;
+  const long long slot_stride = v.npad * A;
+  for (int k = 0; k < nh; ++k) {
+    int slot = head + 1 + k;
+    slot -= slot >= v.ring_len ? v.ring_len : 0;
+    const float* src = v.ring + (long long)slot * slot_stride + nn * A;
+    if (A == 4)
+      __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tile4 + (3 + k) * kPad), 16, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tilef + (12 + k) * kPad), 4, 0, 0);
+  }
+
+  // _preprocessAction: rpm = HOVER_RPM*(1+0.05*a)  (BaseRLAviary.py:191-192, :224-225)
   R rpm[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) rpm[k] = (R)action_to_rpm(c.hover_f32, a[A == 4 ? k : 0]);
@@ -126,8 +181,8 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
   }
   // final readback (:374) -> obs / reward / done
-  R qn[4], roll, pitch, yaw;
-  quat_readback(s.qx, s.qy, s.qz, s.qw, qn);
+  R qn[4], Rm[9], roll, pitch, yaw;
+  readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
   quat_to_euler(qn, roll, pitch, yaw);
 
   // ---- task hooks, evaluated before step_counter += PYB_STEPS_PER_CTRL (:376-382)
@@ -147,7 +202,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
       sflag[tid] = oob ? 1 : 0;
       __syncthreads();
       if (d == 0) {
-        // MultiHoverAviary: summed reward, Σ dist < 1e-4, any drone out of bounds
+        // MultiHoverAviary: summed reward, sum of distances < 1e-4, any drone out of bounds
         float rs = 0.0f, ds = 0.0f;
         int anyo = 0;
         for (int j = 0; j < D; ++j) { rs += srew[base + j]; ds += sdist[base + j]; anyo |= sflag[base + j]; }
@@ -171,48 +226,35 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
   const bool done = term || trunc;
   const bool do_reset = done && v.autoreset;
 
-  if (!active) return;
+  // current action into the ring (deque.append); the DMA above never reads slot `head`
+  if (active) {
+    float* ring_cur = v.ring + (long long)head * slot_stride + n * A;
+    if (A == 4) *reinterpret_cast<float4*>(ring_cur) = make_float4(a[0], a[1], a[2], a[3]);
+    else ring_cur[0] = a[0];
+  }
 
-  // ---- observation row: [pos, rpy, vel, ang_v] then the 15-slot action history
   float row12[12] = {(float)s.px, (float)s.py, (float)s.pz, (float)roll, (float)pitch, (float)yaw,
                      (float)s.vx, (float)s.vy, (float)s.vz, (float)s.ax, (float)s.ay, (float)s.az};
-  const long long slot_stride = v.npad * A;
-  // current action into the ring (deque.append)
-  float* ring_cur = v.ring + (long long)io.head * slot_stride + n * A;
-  if (A == 4) *reinterpret_cast<float4*>(ring_cur) = make_float4(a[0], a[1], a[2], a[3]);
-  else ring_cur[0] = a[0];
-
-  float* orow = io.obs + n * v.W;
-  float* trow = (do_reset && io.terminal_obs) ? io.terminal_obs + n * v.W : nullptr;
-  // history: oldest first = slots head+1 .. head+ring_len-1, then the current action
-  for (int k = 0; k < v.ring_len - 1; ++k) {
-    int slot = io.head + 1 + k;
-    slot -= slot >= v.ring_len ? v.ring_len : 0;
-    const float* src = v.ring + (long long)slot * slot_stride + n * A;
-    if (A == 4) {
-      const float4 h = *reinterpret_cast<const float4*>(src);
-      *reinterpret_cast<float4*>(orow + 12 + k * 4) = h;
-      if (trow) *reinterpret_cast<float4*>(trow + 12 + k * 4) = h;
-    } else {
-      orow[12 + k] = src[0];
-      if (trow) trow[12 + k] = src[0];
-    }
-  }
-  const int kc = v.ring_len - 1;
-  if (A == 4) {
-    const float4 h = make_float4(a[0], a[1], a[2], a[3]);
-    *reinterpret_cast<float4*>(orow + 12 + kc * 4) = h;
-    if (trow) *reinterpret_cast<float4*>(trow + 12 + kc * 4) = h;
-  } else {
-    orow[12 + kc] = a[0];
-    if (trow) trow[12 + kc] = a[0];
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // history DMA has landed in the tile
 
   if (do_reset) {
-    // terminal row -> terminal_obs; env back to INIT_XYZS / INIT_RPYS (_housekeeping :458-477)
-    if (trow) {
+    // terminal row (rare) straight to terminal_obs, then back to INIT_XYZS / INIT_RPYS
+    // (_housekeeping :458-477; SB3 DummyVecEnv keeps the last obs as terminal_observation)
+    if (io.terminal_obs && active) {
+      float* trow = io.terminal_obs + n * v.W;
 #pragma unroll
       for (int k = 0; k < 12; ++k) trow[k] = row12[k];
+      for (int k = 0; k < nh; ++k) {
+        if (A == 4) {
+          const float4 h = tile4[(3 + k) * kPad + tid];
+          trow[12 + 4 * k + 0] = h.x; trow[12 + 4 * k + 1] = h.y;
+          trow[12 + 4 * k + 2] = h.z; trow[12 + 4 * k + 3] = h.w;
+        } else {
+          trow[12 + k] = tilef[(12 + k) * kPad + tid];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < A; ++j) trow[12 + nh * A + j] = a[j];
     }
     const R* ini = v.init + d * 10;
     s.px = ini[0]; s.py = ini[1]; s.pz = ini[2];
@@ -227,29 +269,57 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
 #pragma unroll
     for (int k = 6; k < 12; ++k) row12[k] = 0.0f;
   }
+
+  // ---- state columns + current action into the tile, then coalesced copy-out of the rows
   if (A == 4) {
-    *reinterpret_cast<float4*>(orow + 0) = make_float4(row12[0], row12[1], row12[2], row12[3]);
-    *reinterpret_cast<float4*>(orow + 4) = make_float4(row12[4], row12[5], row12[6], row12[7]);
-    *reinterpret_cast<float4*>(orow + 8) = make_float4(row12[8], row12[9], row12[10], row12[11]);
+    tile4[0 * kPad + tid] = make_float4(row12[0], row12[1], row12[2], row12[3]);
+    tile4[1 * kPad + tid] = make_float4(row12[4], row12[5], row12[6], row12[7]);
+    tile4[2 * kPad + tid] = make_float4(row12[8], row12[9], row12[10], row12[11]);
+    tile4[(3 + nh) * kPad + tid] = make_float4(a[0], a[1], a[2], a[3]);
   } else {
 #pragma unroll
-    for (int k = 0; k < 12; ++k) orow[k] = row12[k];
+    for (int k = 0; k < 12; ++k) tilef[k * kPad + tid] = row12[k];
+    tilef[(12 + nh) * kPad + tid] = a[0];
   }
+  __syncthreads();
+  {
+    const int NC = A == 4 ? 3 + v.ring_len : 12 + v.ring_len;  // tile columns (float4 / float)
+    const int total = nact * NC;
+    const int drow = kWave / NC, dcol = kWave - drow * NC;
+    int row = tid / NC, col = tid - (tid / NC) * NC;
+    if (A == 4) {
+      float4* dst = reinterpret_cast<float4*>(io.obs) + n0 * NC;
+      for (int g = tid; g < total; g += kWave) {
+        dst[g] = tile4[col * kPad + row];
+        col += dcol; row += drow;
+        if (col >= NC) { col -= NC; ++row; }
+      }
+    } else {
+      float* dst = io.obs + n0 * NC;
+      for (int g = tid; g < total; g += kWave) {
+        dst[g] = tilef[col * kPad + row];
+        col += dcol; row += drow;
+        if (col >= NC) { col -= NC; ++row; }
+      }
+    }
+  }
+  if (!active) return;
   store_drone(v, n, s, last);
   if (d == 0) {
     io.reward[e] = reward;
     io.term[e] = term ? 1 : 0;
     io.trunc[e] = trunc ? 1 : 0;
-    v.steps[e] = do_reset ? 0 : sc + c.nsub;
+    v.ctr[e] = make_int2(do_reset ? 0 : sc + c.nsub, head + 1 == v.ring_len ? 0 : head + 1);
   }
 }
 
 // ---------------------------------------------------------------------------------------
 // gpd_integrate: n_sub raw substeps with explicit per-substep RPMs, each followed by a readback.
 template <typename R, bool MULTI>
-__global__ __launch_bounds__(kWave) void integrate_kernel(SimView<R> v, Consts<R> c, const R* __restrict__ rpm_in,
-                                                          int n_sub, R* __restrict__ traj) {
-  __shared__ R sx[2 * kWave], sy[2 * kWave], sz[2 * kWave];  // x2: inactive tail lanes may index past tpb
+__global__ __launch_bounds__(kWave) void integrate_kernel(SimView<R> v, const Consts<R>* __restrict__ cp,
+                                                          const R* __restrict__ rpm_in, int n_sub, R* __restrict__ traj) {
+  __shared__ R sx[MULTI ? 2 * kWave : 1], sy[MULTI ? 2 * kWave : 1], sz[MULTI ? 2 * kWave : 1];
+  const Consts<R>& c = *cp;
   const int tid = threadIdx.x;
   const int D = MULTI ? v.D : 1;
   const int d = MULTI ? tid % D : 0;
@@ -257,9 +327,10 @@ __global__ __launch_bounds__(kWave) void integrate_kernel(SimView<R> v, Consts<R
   const long long n = (long long)blockIdx.x * v.tpb + tid;
   const bool active = tid < v.tpb && n < v.N;
   const long long nn = active ? n : 0;
+  (void)d;
   Drone<R> s;
   R last[4];
-  load_drone(v, nn, s, last);
+  load_drone(v, nn, s, last, true);
   const long long N = v.N;
   for (int t = 0; t < n_sub; ++t) {
     R rpm[4];
@@ -269,8 +340,8 @@ __global__ __launch_bounds__(kWave) void integrate_kernel(SimView<R> v, Consts<R
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];
     if (traj && active) {
-      R qn[4], roll, pitch, yaw;
-      quat_readback(s.qx, s.qy, s.qz, s.qw, qn);
+      R qn[4], Rm[9], roll, pitch, yaw;
+      readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
       quat_to_euler(qn, roll, pitch, yaw);
       R* o = traj + ((long long)t * N + n) * 20;
       o[0] = s.px; o[1] = s.py; o[2] = s.pz;
@@ -281,13 +352,15 @@ __global__ __launch_bounds__(kWave) void integrate_kernel(SimView<R> v, Consts<R
       o[16] = last[0]; o[17] = last[1]; o[18] = last[2]; o[19] = last[3];
     }
   }
-  if (active) store_drone(v, n, s, last);
+  if (!active) return;
+  if (n_sub == 0) return;
+  store_drone(v, n, s, last);
 }
 
 // ---------------------------------------------------------------------------------------
 // gpd_reset: masked re-initialisation (+ reset observation rows).
 template <typename R>
-__global__ __launch_bounds__(256) void reset_kernel(SimView<R> v, const uint8_t* __restrict__ mask, float* obs, int head) {
+__global__ __launch_bounds__(256) void reset_kernel(SimView<R> v, const uint8_t* __restrict__ mask, float* obs) {
   const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= v.N) return;
   const long long e = n / v.D;
@@ -302,7 +375,8 @@ __global__ __launch_bounds__(256) void reset_kernel(SimView<R> v, const uint8_t*
   s.ax = s.ay = s.az = R(0);
   R last[4] = {R(0), R(0), R(0), R(0)};
   store_drone(v, n, s, last);
-  if (d == 0) v.steps[e] = 0;
+  const int head = v.ctr[e].y;
+  if (d == 0) v.ctr[e].x = 0;
   if (obs) {
     float* orow = obs + n * v.W;
     orow[0] = (float)ini[0]; orow[1] = (float)ini[1]; orow[2] = (float)ini[2];
@@ -319,20 +393,20 @@ __global__ __launch_bounds__(256) void reset_kernel(SimView<R> v, const uint8_t*
   }
 }
 
-// state20 (BaseAviary._getDroneStateVector :541-561) / raw state transposes
+// state20 (BaseAviary._getDroneStateVector :541-561, literal Bullet readback) / raw transposes
 template <typename R>
 __global__ __launch_bounds__(256) void state20_kernel(SimView<R> v, R* __restrict__ out, int raw) {
   const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= v.N) return;
-  Drone<R> s;
-  R last[4];
-  load_drone(v, n, s, last);
   R* o = out + n * 20;
   if (raw) {
     const long long p = v.npad;
     for (int k = 0; k < 20; ++k) o[k] = v.state[k * p + n];
     return;
   }
+  Drone<R> s;
+  R last[4];
+  load_drone_full(v, n, s, last);
   R qn[4], roll, pitch, yaw;
   quat_readback(s.qx, s.qy, s.qz, s.qw, qn);
   quat_to_euler(qn, roll, pitch, yaw);

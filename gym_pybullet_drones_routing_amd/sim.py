@@ -65,7 +65,7 @@ class BatchedAviarySim:
 
     def __init__(self, n_envs, drones_per_env=1, drone_model=DroneModel.CF2X, urdf_path=None,
                  pyb_freq=240, ctrl_freq=30, act=ActionType.RPM, task="hover",
-                 physics=Physics.DYN, aero=(), precision="f32", autoreset=True, episode_len_sec=8,
+                 physics=Physics.DYN, aero=(), precision="f64", autoreset=True, episode_len_sec=8,
                  initial_xyzs=None, initial_rpys=None, device=None):
         self._lib = _lib.load()
         if not torch.cuda.is_available():
@@ -166,6 +166,25 @@ class BatchedAviarySim:
                        _ptr(self.truncated), _ptr(self.terminal_obs) if terminal_obs else None,
                        _stream(self.device))
         return self.obs, self.reward, self.terminated, self.truncated
+
+    def capture_graph(self, actions_seq, terminal_obs=True):
+        """Record ``len(actions_seq)`` consecutive :meth:`step` launches into one HIP graph
+        (``torch.cuda.CUDAGraph``).  Each ``replay()`` advances every env by that many steps,
+        reading the given action tensors (refill them in place between replays).  gpd_step is
+        a fixed-argument launch - the ring head and step counters live in device memory - so
+        one recorded sequence stays valid for any number of replays.  Capture records only;
+        the sim does not advance until the first replay."""
+        seq = []
+        for a in actions_seq:
+            if not (isinstance(a, torch.Tensor) and a.device == self.device and a.dtype == torch.float32
+                    and a.is_contiguous() and a.numel() == self.n_drones * self.act_width):
+                raise ValueError("capture_graph needs contiguous float32 action tensors on the sim's device")
+            seq.append(a)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.device(self.device), torch.cuda.graph(g):
+            for a in seq:
+                self.step(a, terminal_obs=terminal_obs)
+        return g
 
     # ------------------------------------------------------------------ raw physics
     def integrate(self, rpm, record=False):
