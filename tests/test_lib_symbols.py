@@ -1,0 +1,58 @@
+"""The C-ABI library builds, loads and exports every symbol include/gpd.h declares.
+
+No compute call is made here (no GPU in the CPU suite); only host-side entry points that
+never touch the device (ABI version, last error, built-in parameters) are called."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gpd.h")
+
+
+def _declared():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(gpd_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from gym_pybullet_drones_routing_amd import _build, _lib
+    _build.build()
+    return _lib.load()
+
+
+def test_header_and_binding_agree():
+    from gym_pybullet_drones_routing_amd import _lib
+    assert set(_declared()) == set(_lib.EXPORTED)
+
+
+def test_every_declared_symbol_is_exported(lib):
+    for name in _declared():
+        assert hasattr(lib, name), name
+    out = os.popen(f"nm -D --defined-only {lib._name}").read()
+    for name in _declared():
+        assert re.search(rf"\bT {name}\b", out), f"{name} not exported as a text symbol"
+
+
+def test_host_only_entry_points(lib):
+    from gym_pybullet_drones_routing_amd import _lib
+    assert lib.gpd_abi_version() == 1
+    p = _lib.DroneParams()
+    assert lib.gpd_default_params(7, ctypes.byref(p)) == _lib.GPD_EINVAL
+    assert b"unknown drone model" in lib.gpd_last_error()
+    assert lib.gpd_default_params(_lib.GPD_MODEL_CF2X, ctypes.byref(p)) == _lib.GPD_OK
+    assert p.kf == 3.16e-10 and p.m == 0.027
+    assert lib.gpd_destroy(None) == _lib.GPD_EINVAL
+    assert lib.gpd_state_bytes(None) == 0
+
+
+def test_struct_sizes_match_header():
+    """ctypes mirrors of gpd_drone_params / gpd_config / gpd_constants have the C layout."""
+    from gym_pybullet_drones_routing_amd import _lib
+    # int + 19 doubles (8-aligned after the int) + 12 doubles
+    assert ctypes.sizeof(_lib.DroneParams) == 8 + 19 * 8 + 12 * 8
+    assert ctypes.sizeof(_lib.Config) == 9 * 4 + 4 + 8 + 8 + 8
+    assert ctypes.sizeof(_lib.Constants) == 9 * 8 + 6 * 4 + 0
