@@ -86,6 +86,28 @@ def cpu_baseline(seconds=10.0, act="rpm"):
                       "BaseAviary.step without pybullet call overhead (flatters the reference)"}
 
 
+def cpu_baseline_openmp(E, seconds=5.0, act="rpm", threads=16):
+    """The C oracle (oracle/gpd_oracle.c, fp64, OpenMP over envs) stepping E HoverAviary envs on
+    `threads` host cores: the optimised-CPU reference point for the same batched workload."""
+    from oracle.c_oracle import COracle
+    A = 4 if act == "rpm" else 1
+    c = COracle(n_envs=E, task="hover", act=act, threads=threads)
+    rng = np.random.default_rng(0)
+    pool = rng.uniform(-1, 1, (8, E, 1, A)).astype(np.float32)
+    c.step(pool[0])
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        c.step(pool[steps % 8])
+        steps += 1
+    el = time.perf_counter() - t0
+    c.close()
+    model, ncpu = cpu_info()
+    return {"value": E * 8 * steps / el, "unit": "drone*dt/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} steps of {E} HoverAviary envs (C fp64 restatement, OpenMP, {threads} threads of "
+                      f"'{model}') in {el:.1f} s"}
+
+
 def time_graph(sim, pool, steps, warmup, per_graph=16):
     """Timed region in hipGraph mode: one graph = `per_graph` consecutive env.step() launches
     reading distinct pre-filled action slots; returns (wall seconds, steps actually run)."""
@@ -165,6 +187,7 @@ def main():
     torch.cuda.set_device(device)
 
     from gym_pybullet_drones_routing_amd.enums import ActionType
+    from gym_pybullet_drones_routing_amd.shard import gather_batch, max_over_ranks, rank_seed
     from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
 
     E = args.envs
@@ -172,7 +195,7 @@ def main():
     sim = BatchedAviarySim(n_envs=E, task="hover", act=ActionType(args.act), precision=args.precision,
                            autoreset=True, device=device)
     nsub = sim.pyb_steps_per_ctrl
-    pool = make_pool(E, A, device, seed=1000 + rank)
+    pool = make_pool(E, A, device, seed=rank_seed(1000, rank))
     # (1) eager pass: per-launch HIP events give the step kernel's duration (roofline)
     eager_wall, kern_us = time_steps(sim, pool, args.steps, args.warmup)
     # (2) timed pass: the same steps replayed from a hipGraph (no host launch overhead)
@@ -180,10 +203,8 @@ def main():
         wall, steps_run = eager_wall, args.steps
     else:
         wall, steps_run = time_graph(sim, pool, args.steps, args.warmup)
-    if world > 1:
-        t = torch.tensor([wall, eager_wall], device=device, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        wall, eager_wall = float(t[0].item()), float(t[1].item())
+    wall = max_over_ranks(wall, device)
+    eager_wall = max_over_ranks(eager_wall, device)
     drone_dt = world * E * nsub * steps_run
     value = drone_dt / wall
     ms_per_step = 1000.0 * wall / steps_run
@@ -212,20 +233,18 @@ def main():
 
     if world > 1:
         # config 5: RCCL all-gather of the observation batch (+ reward / done) to the learner
-        obs_all = torch.empty((world,) + tuple(sim.obs.shape), dtype=sim.obs.dtype, device=device)
-        rew_all = torch.empty((world, E), dtype=torch.float32, device=device)
+        obs_all = torch.empty((world * E,) + tuple(sim.obs.shape[1:]), dtype=sim.obs.dtype, device=device)
+        rew_all = torch.empty((world * E,), dtype=torch.float32, device=device)
         torch.distributed.barrier()
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
         G = max(10, args.steps // 3)
         for k in range(G):
             sim.step(pool[k % pool.shape[0]])
-            torch.distributed.all_gather_into_tensor(obs_all, sim.obs)
-            torch.distributed.all_gather_into_tensor(rew_all, sim.reward)
+            gather_batch(sim.obs, obs_all)
+            gather_batch(sim.reward, rew_all)
         torch.cuda.synchronize(device)
-        gw = torch.tensor([time.perf_counter() - t0], device=device, dtype=torch.float64)
-        torch.distributed.all_reduce(gw, op=torch.distributed.ReduceOp.MAX)
-        gw = float(gw.item())
+        gw = max_over_ranks(time.perf_counter() - t0, device)
         result["gather"] = {"mode": "eager step + RCCL all_gather of obs and reward per step",
                             "ms_per_step": 1000 * gw / G, "value": world * E * nsub * G / gw,
                             "bytes_per_step": int(obs_all.numel() * 4 + rew_all.numel() * 4)}
@@ -248,6 +267,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.act)
         result["speedup_vs_cpu_baseline"] = value / result["cpu_baseline"]["value"]
+        try:
+            result["cpu_baseline_openmp"] = cpu_baseline_openmp(E, args.cpu_seconds, args.act,
+                                                                threads=min(16, os.cpu_count() or 1))
+        except Exception as exc:  # the C oracle is optional for the bench
+            result["cpu_baseline_openmp"] = {"error": str(exc)}
 
     if rank == 0:
         print(json.dumps(result), flush=True)

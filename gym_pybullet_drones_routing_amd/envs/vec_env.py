@@ -1,0 +1,125 @@
+"""Batched VecEnv view: ``num_envs`` HoverAviary / MultiHoverAviary envs in one HIP launch per step.
+
+The reference reaches its env through stable-baselines3 ``make_vec_env(HoverAviary, n_envs=1)``
+(DummyVecEnv, ``examples/learn.py:53-64``).  ``AviaryVecEnv`` is the MI355X replacement for that
+whole vector: it implements the SB3 ``VecEnv`` protocol (``reset``, ``step_async``,
+``step_wait``, ``num_envs``, spaces, ``get_attr`` ...) with DummyVecEnv's auto-reset semantics
+(``infos[i]["terminal_observation"]``, ``infos[i]["TimeLimit.truncated"]``), so SB3 PPO can use it
+where stable_baselines3 is installed.  ``output="torch"`` keeps everything in HBM for a
+GPU-resident learner (infos become a dict of tensors).
+"""
+import numpy as np
+import torch
+
+from ..enums import ActionType, DroneModel, ObservationType, Physics
+from ..sim import BatchedAviarySim
+from .spaces import action_space, observation_space
+
+
+class AviaryVecEnv:
+    def __init__(self, num_envs, task="hover", num_drones=1, drone_model=DroneModel.CF2X, initial_xyzs=None,
+                 initial_rpys=None, physics=Physics.DYN, aero=(), pyb_freq=240, ctrl_freq=30,
+                 obs=ObservationType.KIN, act=ActionType.RPM, precision="f64", device=None, output="numpy",
+                 episode_len_sec=8, urdf_path=None):
+        if ObservationType(obs) != ObservationType.KIN:
+            raise NotImplementedError("ObservationType.RGB is out of scope")
+        if output not in ("numpy", "torch"):
+            raise ValueError("output must be 'numpy' or 'torch'")
+        if task == "hover" and num_drones != 1:
+            raise ValueError("HoverAviary is single-drone")
+        self.sim = BatchedAviarySim(n_envs=num_envs, drones_per_env=num_drones, drone_model=drone_model,
+                                    urdf_path=urdf_path, pyb_freq=pyb_freq, ctrl_freq=ctrl_freq, act=act,
+                                    task=task, physics=physics, aero=aero, precision=precision, autoreset=True,
+                                    episode_len_sec=episode_len_sec, initial_xyzs=initial_xyzs,
+                                    initial_rpys=initial_rpys, device=device)
+        self.num_envs = int(num_envs)
+        self.num_drones = int(num_drones)
+        self.output = output
+        self.action_space = action_space(num_drones, self.sim.act_width)
+        self.observation_space = observation_space(num_drones, self.sim.act_width, int(ctrl_freq // 2))
+        self._actions = torch.zeros((num_envs, num_drones, self.sim.act_width), dtype=torch.float32,
+                                    device=self.sim.device)
+        self.render_mode = None
+
+    # ------------------------------------------------------------------ VecEnv protocol
+    def reset(self):
+        obs = self.sim.reset()
+        return obs.clone() if self.output == "torch" else obs.cpu().numpy()
+
+    def step_async(self, actions):
+        if isinstance(actions, torch.Tensor):
+            self._actions.copy_(actions.reshape(self._actions.shape))
+        else:
+            a = np.asarray(actions, dtype=np.float32).reshape(self._actions.shape)
+            self._actions.copy_(torch.from_numpy(a))
+
+    def step_wait(self):
+        obs, rew, te, tr = self.sim.step(self._actions, terminal_obs=True)
+        done = (te | tr).bool()
+        if self.output == "torch":
+            infos = {"terminal_observation": self.sim.terminal_obs.clone(),
+                     "TimeLimit.truncated": (tr.bool() & ~te.bool()), "done_mask": done}
+            return obs.clone(), rew.clone(), done, infos
+        o, r, d = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy()
+        te_n, tr_n = te.cpu().numpy().astype(bool), tr.cpu().numpy().astype(bool)
+        infos = [{"answer": 42} for _ in range(self.num_envs)]
+        if d.any():
+            tobs = self.sim.terminal_obs.cpu().numpy()
+            for e in np.nonzero(d)[0]:
+                infos[e]["TimeLimit.truncated"] = bool(tr_n[e] and not te_n[e])
+                infos[e]["terminal_observation"] = tobs[e].copy()
+        return o, r, d, infos
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def close(self):
+        self.sim.close()
+
+    def seed(self, seed=None):
+        return [None] * self.num_envs   # resets are deterministic, as in the reference (:243)
+
+    def get_attr(self, attr_name, indices=None):
+        n = len(self._indices(indices))
+        return [getattr(self, attr_name)] * n
+
+    def set_attr(self, attr_name, value, indices=None):
+        setattr(self, attr_name, value)
+
+    def env_method(self, method_name, *args, indices=None, **kwargs):
+        return [getattr(self, method_name)(*args, **kwargs) for _ in self._indices(indices)]
+
+    def env_is_wrapped(self, wrapper_class, indices=None):
+        return [False] * len(self._indices(indices))
+
+    def get_images(self):
+        return [None] * self.num_envs
+
+    def render(self, mode=None):
+        return None
+
+    def _indices(self, indices):
+        if indices is None:
+            return list(range(self.num_envs))
+        if isinstance(indices, int):
+            return [indices]
+        return list(indices)
+
+
+def make_vec_env(env_cls, n_envs=1, seed=None, env_kwargs=None, **vec_kwargs):
+    """``stable_baselines3.common.env_util.make_vec_env`` stand-in for the two RL aviaries:
+    builds ONE batched ``AviaryVecEnv`` instead of ``n_envs`` Python env objects."""
+    from .HoverAviary import HoverAviary
+    from .MultiHoverAviary import MultiHoverAviary
+    kw = dict(env_kwargs or {})
+    if env_cls is HoverAviary or env_cls == "hover-aviary-v0":
+        task, nd = "hover", 1
+    elif env_cls is MultiHoverAviary or env_cls == "multihover-aviary-v0":
+        task, nd = "multihover", kw.pop("num_drones", 2)
+    else:
+        raise ValueError(f"no batched implementation for {env_cls}")
+    for k in ("gui", "record", "neighbourhood_radius"):
+        kw.pop(k, None)
+    kw.setdefault("physics", Physics.DYN)
+    return AviaryVecEnv(n_envs, task=task, num_drones=nd, **kw, **vec_kwargs)

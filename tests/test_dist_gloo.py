@@ -1,0 +1,85 @@
+"""World-size-2 gloo test of the multi-GPU path (gym_pybullet_drones_routing_amd.shard) on CPU.
+
+Each rank steps its env shard (the C oracle stands in for the per-GPU HIP sim, since this
+suite has no GPU) and all-gathers the observations; the gathered batch must equal one process
+stepping all envs, and the max-over-ranks timing helper must return the global max."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+class _OracleShard:
+    """Adapter: C oracle with the sim's step() signature, returning torch tensors."""
+
+    def __init__(self, n_envs):
+        from oracle.c_oracle import COracle
+        self.o = COracle(n_envs=n_envs, task="hover", threads=1)
+
+    def step(self, actions):
+        obs, rew, te, tr = self.o.step(actions.numpy())
+        return (torch.from_numpy(obs.copy()), torch.from_numpy(rew.copy()),
+                torch.from_numpy(te.astype(np.uint8)), torch.from_numpy(tr.astype(np.uint8)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, E, T, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gym_pybullet_drones_routing_amd.shard import ShardedStepper, env_shard, max_over_ranks
+        start, count = env_shard(E, rank, world)
+        stepper = ShardedStepper(_OracleShard(count), E)
+        rng = np.random.default_rng(0)
+        acts = torch.from_numpy(rng.uniform(-1, 1, (T, E, 1, 4)).astype(np.float32))
+        outs = []
+        for t in range(T):
+            obs, rew, te, tr = stepper.step(acts[t])
+            outs.append((obs.numpy().copy(), rew.numpy().copy(), te.numpy().copy(), tr.numpy().copy()))
+        mx = max_over_ranks(float(rank + 1))
+        if rank == 0:
+            q.put((outs, mx, start, count))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_step_and_gather_gloo():
+    from oracle.c_oracle import COracle
+    E, T, world = 8, 30, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, E, T, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs, mx, start, count = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert (start, count) == (0, 4) and mx == 2.0
+    ref = COracle(n_envs=E, task="hover", threads=1)
+    rng = np.random.default_rng(0)
+    acts = rng.uniform(-1, 1, (T, E, 1, 4)).astype(np.float32)
+    for t in range(T):
+        o, r, te, tr = ref.step(acts[t])
+        np.testing.assert_array_equal(outs[t][0], o)
+        np.testing.assert_array_equal(outs[t][1], r)
+        np.testing.assert_array_equal(outs[t][2].astype(bool), te)
+        np.testing.assert_array_equal(outs[t][3].astype(bool), tr)
+
+
+def test_env_shard_split():
+    from gym_pybullet_drones_routing_amd.shard import env_shard
+    assert [env_shard(32768, r, 8) for r in (0, 7)] == [(0, 4096), (28672, 4096)]
+    with pytest.raises(ValueError):
+        env_shard(10, 0, 3)
