@@ -110,24 +110,31 @@ def cpu_baseline_openmp(E, seconds=5.0, act="rpm", threads=16):
 
 def time_graph(sim, pool, steps, warmup, per_graph=16):
     """Timed region in hipGraph mode: one graph = `per_graph` consecutive env.step() launches
-    reading distinct pre-filled action slots; returns (wall seconds, steps actually run)."""
+    reading distinct pre-filled action slots.  A HIP event pair on the launch stream brackets
+    the replays, so (event time / launches) is the step kernel's average duration including the
+    in-graph kernel boundary (an upper bound; rocprofv3 reports the kernel alone).
+    Returns (wall seconds, steps run, kernel us)."""
     P = pool.shape[0]
     graph = sim.capture_graph([pool[k % P] for k in range(per_graph)])
     reps = max(1, steps // per_graph)
     for _ in range(max(1, warmup // per_graph)):
         graph.replay()
+    stream = torch.cuda.current_stream(sim.device)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(sim.device)
     if torch.distributed.is_initialized():
         torch.distributed.barrier()
     torch.cuda.synchronize(sim.device)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for _ in range(reps):
         graph.replay()
+    ev1.record(stream)
     torch.cuda.synchronize(sim.device)
     wall = time.perf_counter() - t0
     if torch.distributed.is_initialized():
         torch.distributed.barrier()
-    return wall, reps * per_graph
+    return wall, reps * per_graph, 1000.0 * ev0.elapsed_time(ev1) / (reps * per_graph)
 
 
 def time_steps(sim, pool, steps, warmup):
@@ -196,13 +203,14 @@ def main():
                            autoreset=True, device=device)
     nsub = sim.pyb_steps_per_ctrl
     pool = make_pool(E, A, device, seed=rank_seed(1000, rank))
-    # (1) eager pass: per-launch HIP events give the step kernel's duration (roofline)
-    eager_wall, kern_us = time_steps(sim, pool, args.steps, args.warmup)
-    # (2) timed pass: the same steps replayed from a hipGraph (no host launch overhead)
+    # (1) eager pass (also the SB3-style per-call number); per-launch event pairs
+    eager_wall, eager_kern_us = time_steps(sim, pool, args.steps, args.warmup)
+    # (2) timed pass: the same steps replayed from a hipGraph (no host launch overhead); the
+    #     roofline's kernel duration comes from the events around these replays
     if args.eager:
-        wall, steps_run = eager_wall, args.steps
+        wall, steps_run, kern_us = eager_wall, args.steps, eager_kern_us
     else:
-        wall, steps_run = time_graph(sim, pool, args.steps, args.warmup)
+        wall, steps_run, kern_us = time_graph(sim, pool, args.steps, args.warmup)
     wall = max_over_ranks(wall, device)
     eager_wall = max_over_ranks(eager_wall, device)
     drone_dt = world * E * nsub * steps_run
@@ -223,7 +231,8 @@ def main():
                    "parallelism": f"env-sharded x{world} (no collective in the step loop)"},
         "kernel_us": kern_us,
         "eager": {"ms_per_step": 1000.0 * eager_wall / args.steps,
-                  "value": world * E * nsub * args.steps / eager_wall},
+                  "value": world * E * nsub * args.steps / eager_wall,
+                  "kernel_us_per_launch_events": eager_kern_us},
         "ctrl_steps_per_s": world * E * args.steps / wall,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
@@ -254,11 +263,11 @@ def main():
         for e_large in (65536, 1 << 20, 1 << 22):
             s2 = BatchedAviarySim(n_envs=e_large, task="hover", act=ActionType(args.act),
                                   precision=args.precision, autoreset=True, device=device)
-            p2 = make_pool(e_large, A, device, seed=7, pool=4)
-            w2, k2 = time_steps(s2, p2, 20, 3)
+            p2 = make_pool(e_large, A, device, seed=7, pool=16)
+            w2, n2, k2 = time_graph(s2, p2, 32, 16)
             ach = alg_bytes_per_drone_step(args.act, rbytes) * e_large / (k2 * 1e-6) / 1e9
-            sweep.append({"n_envs": e_large, "kernel_us": k2, "ms_per_step": 1000 * w2 / 20,
-                          "value": e_large * nsub * 20 / w2, "achieved_GBps": ach, "frac": ach / HBM_PEAK_GBPS})
+            sweep.append({"n_envs": e_large, "kernel_us": k2, "ms_per_step": 1000 * w2 / n2,
+                          "value": e_large * nsub * n2 / w2, "achieved_GBps": ach, "frac": ach / HBM_PEAK_GBPS})
             s2.close()
             del p2
             torch.cuda.empty_cache()

@@ -29,6 +29,24 @@ __device__ __forceinline__ double g_exp(double x) { return exp(x); }
 __device__ __forceinline__ float g_abs(float x) { return fabsf(x); }
 __device__ __forceinline__ double g_abs(double x) { return fabs(x); }
 
+// 1/sqrt(x) for x > 0: the hardware estimate (v_rsq_*) refined by Newton steps
+// y <- y + y*(1/2 - x*y*y/2); two steps for double (error <= ~2 ulp), one for float.  Replaces
+// a divide + square-root pair (~20 dependent f64 instructions) on the substep's critical chain.
+__device__ __forceinline__ double g_rsqrt(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  double e = fma(-h * y, y, 0.5);
+  y = fma(y, e, y);
+  e = fma(-h * y, y, 0.5);
+  return fma(y, e, y);
+}
+__device__ __forceinline__ float g_rsqrt(float x) {
+  float y = __builtin_amdgcn_rsqf(x);
+  const float h = 0.5f * x;
+  const float e = fmaf(-h * y, y, 0.5f);
+  return fmaf(y, e, y);
+}
+
 template <typename R> struct PiC;
 template <> struct PiC<float> { static constexpr float pi = 3.14159265358979323846f; };
 template <> struct PiC<double> { static constexpr double pi = 3.14159265358979323846; };
@@ -136,7 +154,8 @@ __device__ __forceinline__ void quat_readback(R x, R y, R z, R w, R qn[4]) {
 template <typename R>
 __device__ __forceinline__ void readback_fused(R x, R y, R z, R w, R qn[4], R m[9]) {
   const R d = x * x + y * y + z * z + w * w;
-  const R s = R(2) / d;
+  R inv = g_rsqrt(d);            // 1/|q|
+  const R s = R(2) * (inv * inv);  // 2/|q|^2  (setRotation's s)
   const R xs = x * s, ys = y * s, zs = z * s;
   const R wx = w * xs, wy = w * ys, wz = w * zs;
   const R xx = x * xs, xy = x * ys, xz = x * zs;
@@ -152,7 +171,6 @@ __device__ __forceinline__ void readback_fused(R x, R y, R z, R w, R qn[4], R m[
     const int i = m[0] < m[4] ? (m[4] < m[8] ? 2 : 1) : (m[0] < m[8] ? 2 : 0);
     key = i == 0 ? x : (i == 1 ? y : z);
   }
-  R inv = R(1) / g_sqrt(d);
   inv = key < R(0) ? -inv : inv;
   qn[0] = x * inv; qn[1] = y * inv; qn[2] = z * inv; qn[3] = w * inv;
 }
@@ -205,6 +223,58 @@ __device__ __forceinline__ void quat_to_euler(const R q[4], R& roll, R& pitch, R
   }
 }
 
+// Attitude predicates of the reference evaluated WITHOUT atan2/asin.  getEulerZYX gives
+// pitch = asin(sarg) (or +-pi/2 in the gimbal branches) and roll = atan2(a, b) (0 in the
+// branches), with sarg = -2(xz - wy), a = 2(yz + wx), b = w^2 - x^2 - y^2 + z^2.  Because asin
+// and atan2 are monotonic in the relevant argument, the comparisons below are the reference's
+// comparisons up to rounding exactly at the threshold.
+template <typename R>
+struct AttitudeArgs {
+  R sarg, a, b;
+  bool gimbal;  // |sarg| >= 0.99999: pitch = +-pi/2, roll = 0
+};
+template <typename R>
+__device__ __forceinline__ AttitudeArgs<R> attitude_args(const R q[4]) {
+  const R x = q[0], y = q[1], z = q[2], w = q[3];
+  AttitudeArgs<R> t;
+  t.sarg = R(-2) * (x * z - w * y);
+  t.a = R(2) * (y * z + w * x);
+  t.b = w * w - x * x - y * y + z * z;
+  t.gimbal = t.sarg <= R(-0.99999) || t.sarg >= R(0.99999);
+  return t;
+}
+// |roll| > lim or |pitch| > lim, 0 < lim < pi/2 (HoverAviary.py:112, MultiHoverAviary.py:121)
+template <typename R>
+__device__ __forceinline__ bool tilted_beyond(const AttitudeArgs<R>& t, R sin_lim, R tan_lim) {
+  if (t.gimbal) return true;                      // |pitch| = pi/2
+  if (g_abs(t.sarg) > sin_lim) return true;       // |asin(sarg)| > lim
+  if (t.b > R(0)) return g_abs(t.a) > tan_lim * t.b;
+  return !(t.b == R(0) && t.a == R(0) && !signbit(t.b));  // |atan2| >= pi/2 except atan2(+-0, +0)
+}
+// |roll| < pi/2 and |pitch| < pi/2 (the _groundEffect condition, BaseAviary.py:742)
+template <typename R>
+__device__ __forceinline__ bool upright(const AttitudeArgs<R>& t) {
+  if (t.gimbal) return false;
+  return t.b > R(0) || (t.b == R(0) && t.a == R(0) && !signbit(t.b));
+}
+// float32 Euler angles for the float32 observation (the reference casts its float64 angles to
+// float32, BaseRLAviary.py:315); evaluated in float32 from the double-precision arguments.
+template <typename R>
+__device__ __forceinline__ void obs_euler_f32(const R q[4], const AttitudeArgs<R>& t, float& roll, float& pitch,
+                                              float& yaw) {
+  const R x = q[0], y = q[1], z = q[2], w = q[3];
+  if (t.sarg <= R(-0.99999)) {
+    pitch = -1.57079632679489661923f; roll = 0.0f; yaw = 2.0f * atan2f((float)x, (float)-y);
+  } else if (t.sarg >= R(0.99999)) {
+    pitch = 1.57079632679489661923f; roll = 0.0f; yaw = 2.0f * atan2f((float)-x, (float)y);
+  } else {
+    const R sa = t.sarg < R(-1) ? R(-1) : (t.sarg > R(1) ? R(1) : t.sarg);
+    pitch = asinf((float)sa);
+    roll = atan2f((float)t.a, (float)t.b);
+    yaw = atan2f((float)(R(2) * (x * y + w * z)), (float)(w * w + x * x - y * y - z * z));
+  }
+}
+
 // float32 RPM from a float32 action exactly as numpy 1.x evaluates
 // HOVER_RPM * (1 + 0.05*target) on a float32 array (BaseRLAviary.py:192, :225).
 // hipcc would otherwise contract 1 + 0.05*a into one FMA (even through __fmul_rn/__fadd_rn),
@@ -216,18 +286,14 @@ __device__ __forceinline__ float action_to_rpm(float hover_f32, float a) {
   return hover_f32 * u;
 }
 
-// ---------------------------------------------------------------- one DYN substep
-// BaseAviary._dynamics (:815-874) + _integrateQ (:876-889), evaluated on the readback
-// snapshot (pos/vel from the client copy, qn = re-normalised orientation, rpy = its Euler
-// angles), optionally with the aero force terms of _groundEffect/_drag/_downwash added as a
-// body wrench (see DESIGN.md §2 "new combination").
-//   rpm  : this ctrl step's clipped action (current substep)
-//   last : self.last_clipped_action (previous ctrl step's rpm on the first substep)
-//   dwsum: summed downwash force along body z (already reduced over the env's drones)
+// Thrust and body torques (BaseAviary.py:838-851, + _groundEffect :732-750).  Evaluated with FP
+// contraction OFF, like numpy: with contraction hipcc fuses r^2*kf into the following add, so
+// four equal RPMs (every ONE_D_RPM action, the hover equilibrium) would leave a residual
+// roll/pitch torque instead of the reference's exact zero.
 template <typename R>
-__device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R Rm[9], R roll, R pitch,
-                                            const R rpm[4], const R last[4], R dwsum,
-                                            const Consts<R>& c) {
+__device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bool gnd_upright, const R rpm[4],
+                                            const Consts<R>& c, R& fz_out, R& tx_out, R& ty_out, R& tz_out) {
+#pragma clang fp contract(off)
   R f[4], zt[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -253,7 +319,7 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R 
     tx = (((f[0] + f[1]) - f[2]) - f[3]) * c.Ls2;
     ty = (((-f[0] + f[1]) + f[2]) - f[3]) * c.Ls2;
   }
-  if ((c.flags & F_GND) && g_abs(roll) < PiC<R>::pi / R(2) && g_abs(pitch) < PiC<R>::pi / R(2)) {
+  if ((c.flags & F_GND) && gnd_upright) {
     // _groundEffect :732-750 — prop COM heights via forward kinematics, clipped, +z link force
     R g[4];
 #pragma unroll
@@ -270,6 +336,27 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R 
     tx = tx + gx;
     ty = ty + gy;
   }
+  fz_out = fz;
+  tx_out = tx;
+  ty_out = ty;
+  tz_out = tz;
+}
+
+// ---------------------------------------------------------------- one DYN substep
+// BaseAviary._dynamics (:815-874) + _integrateQ (:876-889), evaluated on the readback
+// snapshot (pos/vel from the client copy, qn = re-normalised orientation, rpy = its Euler
+// angles, of which the ground effect only needs |roll|,|pitch| < pi/2 -> `gnd_upright`),
+// optionally with the aero force terms of _groundEffect/_drag/_downwash added as a
+// body wrench (see DESIGN.md §2 "new combination").
+//   rpm  : this ctrl step's clipped action (current substep)
+//   last : self.last_clipped_action (previous ctrl step's rpm on the first substep)
+//   dwsum: summed downwash force along body z (already reduced over the env's drones)
+template <typename R>
+__device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R Rm[9], bool gnd_upright,
+                                            const R rpm[4], const R last[4], R dwsum,
+                                            const Consts<R>& c) {
+  R fz, tx, ty, tz;
+  body_wrench(s, Rm, gnd_upright, rpm, c, fz, tx, ty, tz);
   if (c.flags & F_DW) fz = fz + dwsum;                 // _downwash :801-811 (body z)
   // R·(0,0,fz) - (0,0,GRAVITY) [+ drag]                 :839-841
   R Fx = Rm[2] * fz, Fy = Rm[5] * fz, Fz = Rm[8] * fz;
@@ -298,12 +385,14 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R 
   s.pz = s.pz + c.dt * s.vz;
   // _integrateQ(quat, rpy_rates, dt)                  :876-889
   const R p = s.wx, q = s.wy, r = s.wz;
-  const R nrm = g_sqrt(p * p + q * q + r * r);
+  const R n2 = p * p + q * q + r * r;
+  const R rn = n2 > R(0) ? g_rsqrt(n2) : R(0);        // 1/|omega|
+  const R nrm = n2 * rn;                               // |omega|
   if (nrm > R(1e-8)) {                                 // np.isclose(norm, 0): |norm| <= 1e-8
     const R th = nrm * c.dt * R(0.5);
     R co, si;
     small_sincos(th, si, co);
-    const R k2 = R(2) / nrm;
+    const R k2 = R(2) * rn;                            // 2/|omega|
     const R P = (k2 * (R(0.5) * p)) * si, Q = (k2 * (R(0.5) * q)) * si, Rr = (k2 * (R(0.5) * r)) * si;
     const R x = qn[0], y = qn[1], z = qn[2], w = qn[3];
     s.qx = ((co * x + Rr * y) - Q * z) + P * w;

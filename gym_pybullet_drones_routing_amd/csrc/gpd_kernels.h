@@ -103,8 +103,8 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
                                               R* sx, R* sy, R* sz, int tid, int base, int D) {
   R qn[4], Rm[9];
   readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);  // :346-347 -> :517, :836
-  R roll = R(0), pitch = R(0), yaw;
-  if (c.flags & F_GND) quat_to_euler(qn, roll, pitch, yaw);  // self.rpy used by :742
+  bool up = true;
+  if (c.flags & F_GND) up = upright(attitude_args(qn));  // |self.rpy[0,1]| < pi/2, :742
   R dw = R(0);
   if (MULTI && (c.flags & F_DW)) {
     sx[tid] = s.px; sy[tid] = s.py; sz[tid] = s.pz;
@@ -112,7 +112,7 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
     dw = downwash_sum(s.px, s.py, s.pz, sx, sy, sz, base, D, c);
     __syncthreads();
   }
-  dyn_substep(s, qn, Rm, roll, pitch, rpm, last, dw, c);
+  dyn_substep(s, qn, Rm, up, rpm, last, dw, c);
 }
 
 // Bytes of dynamic LDS the step kernel needs for its observation tile.
@@ -156,34 +156,39 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
     a[0] = io.actions[nn];
   }
 
-  // ---- prefetch the L-1 oldest actions of the history ring into the tile (LDS-DMA); they are
-  //      only needed for the observation, so their latency hides under the substeps below.
-  const int nh = v.ring_len - 1;
-  const long long slot_stride = v.npad * A;
-  for (int k = 0; k < nh; ++k) {
-    int slot = head + 1 + k;
-    slot -= slot >= v.ring_len ? v.ring_len : 0;
-    const float* src = v.ring + (long long)slot * slot_stride + nn * A;
-    if (A == 4)
-      __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tile4 + (3 + k) * kPad), 16, 0, 0);
-    else
-      __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tilef + (12 + k) * kPad), 4, 0, 0);
-  }
-
   // _preprocessAction: rpm = HOVER_RPM*(1+0.05*a)  (BaseRLAviary.py:191-192, :224-225)
   R rpm[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) rpm[k] = (R)action_to_rpm(c.hover_f32, a[A == 4 ? k : 0]);
 
+  const int nh = v.ring_len - 1;
+  const long long slot_stride = v.npad * A;
   for (int it = 0; it < c.nsub; ++it) {
     substep_block<R, MULTI>(s, rpm, last, c, sx, sy, sz, tid, base, D);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
+    if (it == 0) {
+      // ---- prefetch the L-1 oldest actions of the history ring into the obs tile (LDS-DMA).
+      // Issued only now: hipcc waits vmcnt(0) at the next use of an ordinary load while an
+      // LDS-DMA is in flight, so issuing it before the state/action loads were consumed would
+      // put the DMA round trip on the critical path.  Here it overlaps substeps 1..7.
+      for (int k = 0; k < nh; ++k) {
+        int slot = head + 1 + k;
+        slot -= slot >= v.ring_len ? v.ring_len : 0;
+        const float* src = v.ring + (long long)slot * slot_stride + nn * A;
+        if (A == 4)
+          __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tile4 + (3 + k) * kPad), 16, 0, 0);
+        else
+          __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tilef + (12 + k) * kPad), 4, 0, 0);
+      }
+    }
   }
   // final readback (:374) -> obs / reward / done
-  R qn[4], Rm[9], roll, pitch, yaw;
+  R qn[4], Rm[9];
   readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
-  quat_to_euler(qn, roll, pitch, yaw);
+  const AttitudeArgs<R> att = attitude_args(qn);
+  float roll, pitch, yaw;
+  obs_euler_f32(qn, att, roll, pitch, yaw);
 
   // ---- task hooks, evaluated before step_counter += PYB_STEPS_PER_CTRL (:376-382)
   float reward = -1.0f;
@@ -195,7 +200,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
     R r = R(2) - d2 * d2;
     r = r > R(0) ? r : R(0);
     const bool oob = g_abs(s.px) > v.bound_xy || g_abs(s.py) > v.bound_xy || s.pz > R(2) ||
-                     g_abs(roll) > R(0.4) || g_abs(pitch) > R(0.4);
+                     tilted_beyond(att, R(0.38941834230865049), R(0.42279321873816178));  // sin/tan(0.4)
     if (MULTI) {
       srew[tid] = (float)r;
       sdist[tid] = (float)dist;
@@ -233,7 +238,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
     else ring_cur[0] = a[0];
   }
 
-  float row12[12] = {(float)s.px, (float)s.py, (float)s.pz, (float)roll, (float)pitch, (float)yaw,
+  float row12[12] = {(float)s.px, (float)s.py, (float)s.pz, roll, pitch, yaw,
                      (float)s.vx, (float)s.vy, (float)s.vz, (float)s.ax, (float)s.ay, (float)s.az};
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // history DMA has landed in the tile
 
@@ -283,21 +288,51 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
   }
   __syncthreads();
   {
+    // lane tid streams tile elements g = tid, tid+64, ... (row-major over the block's rows), six
+    // LDS reads in flight per batch so the LDS latency is paid once per batch, not per store
     const int NC = A == 4 ? 3 + v.ring_len : 12 + v.ring_len;  // tile columns (float4 / float)
     const int total = nact * NC;
     const int drow = kWave / NC, dcol = kWave - drow * NC;
     int row = tid / NC, col = tid - (tid / NC) * NC;
-    if (A == 4) {
-      float4* dst = reinterpret_cast<float4*>(io.obs) + n0 * NC;
-      for (int g = tid; g < total; g += kWave) {
-        dst[g] = tile4[col * kPad + row];
+    constexpr int U = 6;
+    if (nact == kWave) {
+      // full block: every lane owns exactly NC elements, no guards -> reads batch freely
+      int j = 0;
+      for (; j + U <= NC; j += U) {
+        if (A == 4) {
+          float4 val[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            val[u] = tile4[col * kPad + row];
+            col += dcol; row += drow;
+            if (col >= NC) { col -= NC; ++row; }
+          }
+          float4* dst = reinterpret_cast<float4*>(io.obs) + n0 * NC + tid + j * kWave;
+#pragma unroll
+          for (int u = 0; u < U; ++u) dst[u * kWave] = val[u];
+        } else {
+          float val[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            val[u] = tilef[col * kPad + row];
+            col += dcol; row += drow;
+            if (col >= NC) { col -= NC; ++row; }
+          }
+          float* dst = io.obs + n0 * NC + tid + j * kWave;
+#pragma unroll
+          for (int u = 0; u < U; ++u) dst[u * kWave] = val[u];
+        }
+      }
+      for (; j < NC; ++j) {
+        if (A == 4) reinterpret_cast<float4*>(io.obs)[n0 * NC + tid + j * kWave] = tile4[col * kPad + row];
+        else io.obs[n0 * NC + tid + j * kWave] = tilef[col * kPad + row];
         col += dcol; row += drow;
         if (col >= NC) { col -= NC; ++row; }
       }
     } else {
-      float* dst = io.obs + n0 * NC;
-      for (int g = tid; g < total; g += kWave) {
-        dst[g] = tilef[col * kPad + row];
+      for (int g = tid; g < total; g += kWave) {  // partial last block
+        if (A == 4) reinterpret_cast<float4*>(io.obs)[n0 * NC + g] = tile4[col * kPad + row];
+        else io.obs[n0 * NC + g] = tilef[col * kPad + row];
         col += dcol; row += drow;
         if (col >= NC) { col -= NC; ++row; }
       }

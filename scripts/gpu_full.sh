@@ -1,0 +1,17 @@
+# Full GPU round: tests, smoke, bench, rocprofv3 summaries.  Every GPU step has its own
+# timeout and the chain stops at the first failure that is not a plain test failure.
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+OUT=gpurun_out/${RUN_TAG:-r1}
+mkdir -p $OUT
+timeout -k 10 900 python -m pytest tests -m gpu -q -s -p no:cacheprovider > $OUT/gpu_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> $OUT/gpu_tests.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
+timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_bench -o bench --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/prof_bench_stdout.json 2> $OUT/prof_bench.err || exit $?
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_4096 -o fetch --output-format csv -- python3 scripts/prof_step.py --envs 4096 --steps 50 > /dev/null 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write_4096 -o write --output-format csv -- python3 scripts/prof_step.py --envs 4096 --steps 50 > /dev/null 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_4m -o fetch --output-format csv -- python3 scripts/prof_step.py --envs 4194304 --steps 10 > /dev/null 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write_4m -o write --output-format csv -- python3 scripts/prof_step.py --envs 4194304 --steps 10 > /dev/null 2>&1 || exit $?
+echo ALLDONE

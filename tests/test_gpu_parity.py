@@ -266,3 +266,26 @@ def test_graph_replay_matches_eager():
     assert torch.equal(a.step_counters(), b.step_counters())
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_gpu_kat_hover_and_symmetric_thrust(prec):
+    """KAT-1 on the GPU (hover from rest stays put) and the symmetry the reference has exactly:
+    four equal RPMs (any ONE_D_RPM action) give zero roll/pitch torque, so x, y, roll, pitch
+    and the body rates stay exactly 0 while z moves."""
+    n, T = 8, 1200
+    sim = _sim(n_envs=n, task="none", precision=prec)
+    traj = sim.integrate(np.full((T, n, 4), HOVER), record=True).cpu().numpy()
+    s0 = traj[0, 0]
+    # float32 cannot represent the hover equilibrium exactly (4*kf*rpm^2 - M*G ~ 1e-9 N), so
+    # the fp32 drone drifts by ~0.5*a*t^2 ~ 1e-5 m in 5 s; fp64 stays put to 1e-12.
+    tol = 1e-12 if prec == "f64" else 1e-4
+    assert np.abs(traj[..., :16] - s0[:16]).max() <= tol
+    sim.close()
+    rng = np.random.default_rng(9)
+    rpm = np.repeat(rpm_from_action(HOVER, rng.uniform(-1, 1, (T, n, 1)).astype(np.float32)), 4, axis=2)
+    sim = _sim(n_envs=n, task="none", precision=prec)
+    traj = sim.integrate(rpm, record=True).cpu().numpy()
+    for col in (0, 1, 7, 8, 13, 14):   # x, y, roll, pitch, ang_v x, ang_v y
+        assert np.abs(traj[..., col]).max() == 0.0, col
+    sim.close()
