@@ -44,6 +44,25 @@ def alg_bytes_per_drone_step(act="rpm", real_bytes=8):
     return 13 * real_bytes + 4 * A + 14 * 4 * A + 13 * real_bytes + 4 * real_bytes + (12 + 15 * A) * 4 + 6
 
 
+def pmc_traffic(grid, precision):
+    """HBM bytes per step-kernel launch measured by rocprofv3 PMC passes (FETCH_SIZE x2 gfx950
+    correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM) in the newest profiles/*_summary.json that
+    covers this grid; None when no such measurement is committed."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("precision", "f64") != precision:
+            continue
+        for row in d.get("pmc", []):
+            if row.get("grid") == grid:
+                best = (row["traffic_bytes"], os.path.relpath(f, ROOT))
+    return best
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -235,11 +254,15 @@ def main():
                   "kernel_us_per_launch_events": eager_kern_us},
         "ctrl_steps_per_s": world * E * args.steps / wall,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "traffic_unit": "bytes per launch",
                      "kernel": "gpd::step_kernel<%s,%d,false>" % ("double" if rbytes == 8 else "float", A),
                      "alg_bytes_per_launch": alg},
     }
 
+    tr = pmc_traffic(E, args.precision)
+    if tr is not None:
+        result["roofline"]["traffic"] = tr[0]
+        result["roofline"]["traffic_source"] = tr[1] + " (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate passes)"
     if world > 1:
         # config 5: RCCL all-gather of the observation batch (+ reward / done) to the learner
         obs_all = torch.empty((world * E,) + tuple(sim.obs.shape[1:]), dtype=sim.obs.dtype, device=device)

@@ -9,9 +9,13 @@ rc=$?; echo "pytest rc=$rc" >> $OUT/gpu_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
 timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit $?
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_bench -o bench --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/prof_bench_stdout.json 2> $OUT/prof_bench.err || exit $?
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_4096 -o fetch --output-format csv -- python3 scripts/prof_step.py --envs 4096 --steps 50 > /dev/null 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write_4096 -o write --output-format csv -- python3 scripts/prof_step.py --envs 4096 --steps 50 > /dev/null 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_4m -o fetch --output-format csv -- python3 scripts/prof_step.py --envs 4194304 --steps 10 > /dev/null 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write_4m -o write --output-format csv -- python3 scripts/prof_step.py --envs 4194304 --steps 10 > /dev/null 2>&1 || exit $?
+# kernel trace of the bench command (bench config only, then with the large-N sweep)
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_bench -o bench --output-format csv -- python3 bench.py --no-cpu-baseline --no-sweep > $OUT/prof_bench_stdout.json 2> $OUT/prof_bench.err || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_sweep -o sweep --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/prof_sweep_stdout.json 2> $OUT/prof_sweep.err || exit $?
+# PMC: FETCH_SIZE and WRITE_SIZE in separate passes (TCC slots), kernel-trace only
+for E in 4096 65536 1048576 4194304; do
+  S=50; [ $E -ge 1048576 ] && S=10
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_$E -o fetch --output-format csv -- python3 scripts/prof_step.py --envs $E --steps $S > /dev/null 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write_$E -o write --output-format csv -- python3 scripts/prof_step.py --envs $E --steps $S > /dev/null 2>&1 || exit $?
+done
 echo ALLDONE

@@ -36,7 +36,7 @@ def pmc_groups(pmc_csv, counter, name="step_kernel"):
 
 def main(rdir, out_md):
     lines = [f"# rocprofv3 summary — {os.path.basename(rdir.rstrip('/'))}", ""]
-    summary = {"kernels": [], "pmc": []}
+    summary = {"kernels": [], "pmc": [], "precision": os.environ.get("GPD_PROFILE_PRECISION", "f64")}
     for trace in sorted(glob.glob(os.path.join(rdir, "**", "*_kernel_trace.csv"), recursive=True)):
         lines += [f"## {os.path.relpath(trace, rdir)}", "", "| kernel | grid (lanes) | launches | mean us | median us | min us |",
                   "|---|---|---|---|---|---|"]
