@@ -29,22 +29,24 @@ def needs_build():
     return any(src.stat().st_mtime > t for src in SOURCES)
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, stamps=False):
     """Compile csrc/gpd.hip into libgpd.so for gfx950 (code object v5, loadable by the
-    HIP runtime that ships inside the torch wheel)."""
-    if not force and not needs_build():
+    HIP runtime that ships inside the torch wheel).  stamps=True builds the diagnostic
+    libgpd_stamps.so (phase timestamps, never loaded unless GPD_LIB points at it)."""
+    out = PKG_DIR / "libgpd_stamps.so" if stamps else LIB_PATH
+    if not force and not stamps and not needs_build():
         return LIB_PATH
-    tmp = LIB_PATH.with_suffix(".so.tmp")
+    tmp = out.with_suffix(".so.tmp")
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-mcode-object-version=5", "-O3", "-std=c++17",
            "-fPIC", "-shared", "-Wall", "-Wno-unused-result", f"-I{INCLUDE}", "-o", str(tmp),
-           str(CSRC / "gpd.hip")]
+           str(CSRC / "gpd.hip")] + (["-DGPD_STAMPS"] if stamps else [])
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError("hipcc failed:\n" + " ".join(cmd) + "\n" + res.stdout + res.stderr)
     if verbose and (res.stdout or res.stderr):
         print(res.stdout + res.stderr)
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

@@ -5,13 +5,14 @@ There is deliberately NO CPU fallback: if ``libgpd.so`` is missing or fails to l
 every entry point raises ``GpdLibraryError``.
 """
 import ctypes
+import os
 import pathlib
 
 # The HIP runtime must be the one torch already loaded (same SONAME libamdhip64.so.7):
 # import torch first so that libgpd.so binds to it instead of a second runtime copy.
 import torch  # noqa: F401  (imported for its side effect on the dynamic linker)
 
-LIB_PATH = pathlib.Path(__file__).resolve().parent / "libgpd.so"
+LIB_PATH = pathlib.Path(os.environ.get("GPD_LIB") or (pathlib.Path(__file__).resolve().parent / "libgpd.so"))
 
 GPD_OK = 0
 GPD_EINVAL = -1

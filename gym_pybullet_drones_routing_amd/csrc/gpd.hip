@@ -7,8 +7,10 @@
 // kernels of gpd_kernels.h on the caller's stream.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -139,6 +141,7 @@ Consts<R> make_consts(const gpd_sim* s) {
     c.ry[k] = (R)P.prop_pos[k][1];
     c.rz[k] = (R)P.prop_pos[k][2];
   }
+  for (int k = 0; k < 10; ++k) c.init0[k] = (R)s->init_tmpl[k];
   c.hover_f32 = (float)s->K.hover_rpm;
   c.model = P.model;
   c.flags = s->cfg.physics_flags;
@@ -173,8 +176,10 @@ int upload_tables(gpd_sim* s) {
   HIP_TRY(hipMemcpy(s->d_consts, &c, sizeof(c), hipMemcpyHostToDevice));
   // the observation tile can exceed the 64 KiB default dynamic-LDS limit for long histories
   if (s->tile_bytes > 65536) {
-    const void* fns[4] = {(const void*)step_kernel<R, 4, true>, (const void*)step_kernel<R, 4, false>,
-                          (const void*)step_kernel<R, 1, true>, (const void*)step_kernel<R, 1, false>};
+    const void* fns[8] = {(const void*)step_kernel<R, 4, true, true>, (const void*)step_kernel<R, 4, false, true>,
+                          (const void*)step_kernel<R, 1, true, true>, (const void*)step_kernel<R, 1, false, true>,
+                          (const void*)step_kernel<R, 4, true, false>, (const void*)step_kernel<R, 4, false, false>,
+                          (const void*)step_kernel<R, 1, true, false>, (const void*)step_kernel<R, 1, false, false>};
     for (const void* f : fns)
       HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, s->tile_bytes));
   }
@@ -196,13 +201,17 @@ int launch_step(gpd_sim* s, const float* actions, float* obs, float* reward, uin
   const unsigned grid = grid_for(s->N, s->tpb);
   const bool multi = s->D > 1;
   const size_t lds = (size_t)s->tile_bytes;
+  const bool fast = s->cfg.physics_flags == 0;
+#define GPD_LAUNCH_STEP(A_, M_, F_) \
+  hipLaunchKernelGGL((step_kernel<R, A_, M_, F_>), dim3(grid), dim3(kWave), lds, st, v, io, c)
   if (s->A == 4) {
-    if (multi) hipLaunchKernelGGL((step_kernel<R, 4, true>), dim3(grid), dim3(kWave), lds, st, v, io, c);
-    else hipLaunchKernelGGL((step_kernel<R, 4, false>), dim3(grid), dim3(kWave), lds, st, v, io, c);
+    if (multi) { if (fast) GPD_LAUNCH_STEP(4, true, true); else GPD_LAUNCH_STEP(4, true, false); }
+    else { if (fast) GPD_LAUNCH_STEP(4, false, true); else GPD_LAUNCH_STEP(4, false, false); }
   } else {
-    if (multi) hipLaunchKernelGGL((step_kernel<R, 1, true>), dim3(grid), dim3(kWave), lds, st, v, io, c);
-    else hipLaunchKernelGGL((step_kernel<R, 1, false>), dim3(grid), dim3(kWave), lds, st, v, io, c);
+    if (multi) { if (fast) GPD_LAUNCH_STEP(1, true, true); else GPD_LAUNCH_STEP(1, true, false); }
+    else { if (fast) GPD_LAUNCH_STEP(1, false, true); else GPD_LAUNCH_STEP(1, false, false); }
   }
+#undef GPD_LAUNCH_STEP
   HIP_TRY(hipGetLastError());
   return GPD_OK;
 }
@@ -336,7 +345,19 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   s->W = 12 + s->ring_len * s->A;
   s->nsub = C.pyb_freq / C.ctrl_freq;
   s->prec = C.precision;
-  s->tpb = (kWave / s->D) * s->D;
+  // Drones per 64-lane block.  A wave's time is set by its serial instruction stream, not by
+  // how many of its lanes are active, while a CU streams the observation rows of its blocks at
+  // a limited store-issue rate; so when there are too few drones to give every CU a full wave,
+  // blocks are thinned (down to 16 drones) to spread the rows over all 256 CUs.
+  {
+    const int full = (kWave / s->D) * s->D;
+    const long long per_cu = (Nll + 255) / 256;
+    int want = (int)std::min<long long>(full, std::max<long long>(16, per_cu));
+    want = std::max(s->D, (want / s->D) * s->D);
+    const char* ov = std::getenv("GPD_DRONES_PER_BLOCK");
+    if (ov) want = std::max(s->D, std::min(full, (std::atoi(ov) / s->D) * s->D));
+    s->tpb = want;
+  }
   s->npad = ((long long)s->N + 63) / 64 * 64;
   s->bound_xy = C.task == GPD_TASK_MULTIHOVER ? 2.0 : 1.5;
   s->tile_bytes = step_tile_bytes(s->A, s->ring_len);
@@ -547,5 +568,16 @@ int gpd_load_state(gpd_sim* sim, const void* blob_host, void* stream) {
   HIP_TRY(hipStreamSynchronize(st));
   return GPD_OK;
 }
+
+#ifdef GPD_STAMPS
+// diagnostic build only: copy the phase stamps of the last step launches to the host
+int gpd_debug_stamps(unsigned long long* out_host, int n_blocks) {
+  if (n_blocks > 65536) n_blocks = 65536;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_stamps), (size_t)n_blocks * kStampPhases * 8, 0,
+                              hipMemcpyDeviceToHost));
+  return GPD_OK;
+}
+#endif
 
 }  // extern "C"

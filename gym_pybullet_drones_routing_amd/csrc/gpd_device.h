@@ -68,6 +68,8 @@ struct Consts {
   R rx[4], ry[4], rz[4];                   // prop link origins (cf2x.urdf:42,54,66,78)
   R inv_m;                 // 1/M      (F/M as a multiply; differs from the division by <= 1 ulp)
   R rpm2rad;               // 2*pi/60  (drag: sum(2*pi*rpm/60))
+  R init0[10];             // reset template of drone 0 (pos, stored quat, rpy): single-drone envs
+                           // read it with scalar loads instead of a dependent per-lane load
   float hover_f32;         // float32(HOVER_RPM) (numpy 1.x casting, BaseRLAviary.py:192)
   int model, flags, nsub;
 };
@@ -151,11 +153,24 @@ __device__ __forceinline__ void quat_readback(R x, R y, R z, R w, R qn[4]) {
 // largest diagonal entry is positive, and mat(q/|q|) == mat(q) because setRotation divides by
 // |q|^2.  Computing it this way saves a second matrix build and a square-root branch per
 // substep; the results differ from the literal Bullet sequence only by rounding (~1 ulp).
+template <typename R> struct UnitTol;
+template <> struct UnitTol<double> { static constexpr double v = 1e-9; };
+template <> struct UnitTol<float> { static constexpr float v = 1e-4f; };
+
 template <typename R>
 __device__ __forceinline__ void readback_fused(R x, R y, R z, R w, R qn[4], R m[9]) {
   const R d = x * x + y * y + z * z + w * w;
-  R inv = g_rsqrt(d);            // 1/|q|
-  const R s = R(2) * (inv * inv);  // 2/|q|^2  (setRotation's s)
+  R inv, s;
+  if (g_abs(d - R(1)) < UnitTol<R>::v) {
+    // |q| = 1 +- eps (every quaternion _integrateQ produces from a unit one: its update matrix
+    // is orthogonal): one Newton step from 1 gives 1/sqrt(d) and 2/d with errors 3eps^2/8 and
+    // 2eps^2, below the last bit for |eps| < 1e-9 (double) / 1e-4 (float).
+    inv = R(1.5) - R(0.5) * d;
+    s = R(2) * (R(2) - d);
+  } else {
+    inv = g_rsqrt(d);             // 1/|q|
+    s = R(2) * (inv * inv);       // 2/|q|^2  (setRotation's s)
+  }
   const R xs = x * s, ys = y * s, zs = z * s;
   const R wx = w * xs, wy = w * ys, wz = w * zs;
   const R xx = x * xs, xy = x * ys, xz = x * zs;
@@ -290,7 +305,7 @@ __device__ __forceinline__ float action_to_rpm(float hover_f32, float a) {
 // contraction OFF, like numpy: with contraction hipcc fuses r^2*kf into the following add, so
 // four equal RPMs (every ONE_D_RPM action, the hover equilibrium) would leave a residual
 // roll/pitch torque instead of the reference's exact zero.
-template <typename R>
+template <typename R, bool FAST>
 __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bool gnd_upright, const R rpm[4],
                                             const Consts<R>& c, R& fz_out, R& tx_out, R& ty_out, R& tz_out) {
 #pragma clang fp contract(off)
@@ -308,7 +323,7 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
   R fz = ((f[0] + f[1]) + f[2]) + f[3];                // np.sum(forces) :839
   const R tz = ((-zt[0] + zt[1]) - zt[2]) + zt[3];     // :845
   R tx, ty;
-  if (c.flags & F_GEOM) {                              // _physics: forces at prop links :698-705
+  if (!FAST && (c.flags & F_GEOM)) {                   // _physics: forces at prop links :698-705
     tx = R(0); ty = R(0);
 #pragma unroll
     for (int k = 0; k < 4; ++k) { tx = tx + c.ry[k] * f[k]; ty = ty - c.rx[k] * f[k]; }
@@ -319,7 +334,7 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
     tx = (((f[0] + f[1]) - f[2]) - f[3]) * c.Ls2;
     ty = (((-f[0] + f[1]) + f[2]) - f[3]) * c.Ls2;
   }
-  if ((c.flags & F_GND) && gnd_upright) {
+  if (!FAST && (c.flags & F_GND) && gnd_upright) {
     // _groundEffect :732-750 — prop COM heights via forward kinematics, clipped, +z link force
     R g[4];
 #pragma unroll
@@ -351,16 +366,16 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
 //   rpm  : this ctrl step's clipped action (current substep)
 //   last : self.last_clipped_action (previous ctrl step's rpm on the first substep)
 //   dwsum: summed downwash force along body z (already reduced over the env's drones)
-template <typename R>
+template <typename R, bool FAST>
 __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R Rm[9], bool gnd_upright,
                                             const R rpm[4], const R last[4], R dwsum,
                                             const Consts<R>& c) {
   R fz, tx, ty, tz;
-  body_wrench(s, Rm, gnd_upright, rpm, c, fz, tx, ty, tz);
-  if (c.flags & F_DW) fz = fz + dwsum;                 // _downwash :801-811 (body z)
+  body_wrench<R, FAST>(s, Rm, gnd_upright, rpm, c, fz, tx, ty, tz);
+  if (!FAST && (c.flags & F_DW)) fz = fz + dwsum;      // _downwash :801-811 (body z)
   // R·(0,0,fz) - (0,0,GRAVITY) [+ drag]                 :839-841
   R Fx = Rm[2] * fz, Fy = Rm[5] * fz, Fz = Rm[8] * fz;
-  if (c.flags & F_DRAG) {                              // _drag :773-774 with last_clipped_action
+  if (!FAST && (c.flags & F_DRAG)) {                   // _drag :773-774 with last_clipped_action
     const R S = ((last[0] * c.rpm2rad + last[1] * c.rpm2rad) + last[2] * c.rpm2rad) + last[3] * c.rpm2rad;
     Fx = Fx + (-c.drag_xy * S) * s.vx;
     Fy = Fy + (-c.drag_xy * S) * s.vy;

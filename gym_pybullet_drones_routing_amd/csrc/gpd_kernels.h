@@ -34,6 +34,24 @@ constexpr int kPad = kWave + 1;  // tile column stride (elements)
 
 enum : int { TASK_NONE = 0, TASK_HOVER = 1, TASK_MULTIHOVER = 2 };
 
+// Diagnostic build only (-DGPD_STAMPS, libgpd_stamps.so): lane 0 of every block records the
+// shader clock at phase boundaries of step_kernel into g_stamps[block][phase].  The shipped
+// library executes no stamp.
+#ifdef GPD_STAMPS
+constexpr int kStampPhases = 8;
+__device__ unsigned long long g_stamps[65536 * kStampPhases];
+#define GPD_STAMP(k)                                                                      \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    unsigned long long t_;                                                                \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) g_stamps[blockIdx.x * kStampPhases + (k)] = t_; \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+  } while (0)
+#else
+#define GPD_STAMP(k) do {} while (0)
+#endif
+
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 typedef __attribute__((address_space(1))) void* gbl_void_ptr;
 
@@ -98,37 +116,41 @@ __device__ __forceinline__ void store_drone(const SimView<R>& v, long long n, co
 
 // One physics substep of every drone of the block, including the readback that precedes it
 // (BaseAviary.py:343-372 loop body).  MULTI: envs have D > 1 drones and may need downwash.
-template <typename R, bool MULTI>
+template <typename R, bool MULTI, bool FAST>
 __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const R last[4], const Consts<R>& c,
                                               R* sx, R* sy, R* sz, int tid, int base, int D) {
   R qn[4], Rm[9];
   readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);  // :346-347 -> :517, :836
   bool up = true;
-  if (c.flags & F_GND) up = upright(attitude_args(qn));  // |self.rpy[0,1]| < pi/2, :742
+  if (!FAST && (c.flags & F_GND)) up = upright(attitude_args(qn));  // |self.rpy[0,1]| < pi/2, :742
   R dw = R(0);
-  if (MULTI && (c.flags & F_DW)) {
+  if (MULTI && !FAST && (c.flags & F_DW)) {
     sx[tid] = s.px; sy[tid] = s.py; sz[tid] = s.pz;
     __syncthreads();
     dw = downwash_sum(s.px, s.py, s.pz, sx, sy, sz, base, D, c);
     __syncthreads();
   }
-  dyn_substep(s, qn, Rm, up, rpm, last, dw, c);
+  dyn_substep<R, FAST>(s, qn, Rm, up, rpm, last, dw, c);
 }
 
-// Bytes of dynamic LDS the step kernel needs for its observation tile.
+// Bytes of dynamic LDS the step kernel needs for its observation tile: the row's columns
+// (state, history, current action) plus the first 12 floats of the terminal row (pre-reset
+// state of envs that finish this step; the rest of a terminal row equals the reset row).
 __host__ __device__ inline int step_tile_bytes(int A, int ring_len) {
-  return A == 4 ? (3 + ring_len) * kPad * 16 : (12 + ring_len) * kPad * 4;
+  return A == 4 ? (3 + ring_len + 3) * kPad * 16 : (12 + ring_len + 12) * kPad * 4;
 }
 
 // ---------------------------------------------------------------------------------------
 // gpd_step: one env.step() for every env (BaseAviary.py:259-383) in ONE launch.
-template <typename R, int A, bool MULTI>
+// FAST: physics_flags == 0 (plain DYN, the bench path) - the aero / PYB-wrench code is compiled out.
+template <typename R, int A, bool MULTI, bool FAST>
 __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io, const Consts<R>* __restrict__ cp) {
   extern __shared__ float4 tile4[];          // A == 4: [3+L][kPad] float4
   float* tilef = reinterpret_cast<float*>(tile4);  // A == 1: [12+L][kPad] float
   __shared__ R sx[MULTI ? 2 * kWave : 1], sy[MULTI ? 2 * kWave : 1], sz[MULTI ? 2 * kWave : 1];
   __shared__ float srew[MULTI ? 2 * kWave : 1], sdist[MULTI ? 2 * kWave : 1];
   __shared__ int sflag[MULTI ? 2 * kWave : 1];
+  GPD_STAMP(0);
   const Consts<R>& c = *cp;
   const int tid = threadIdx.x;
   const int D = MULTI ? v.D : 1;
@@ -140,7 +162,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
   const bool active = tid < nact;
   const long long nn = active ? n : 0;  // inactive lanes compute on drone 0 and store nothing
   const long long e = MULTI ? nn / D : nn;
-  const bool drag = (c.flags & F_DRAG) != 0;
+  const bool drag = !FAST && (c.flags & F_DRAG) != 0;
 
   Drone<R> s;
   R last[4];
@@ -164,10 +186,11 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
   const int nh = v.ring_len - 1;
   const long long slot_stride = v.npad * A;
   for (int it = 0; it < c.nsub; ++it) {
-    substep_block<R, MULTI>(s, rpm, last, c, sx, sy, sz, tid, base, D);
+    substep_block<R, MULTI, FAST>(s, rpm, last, c, sx, sy, sz, tid, base, D);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
     if (it == 0) {
+      GPD_STAMP(1);
       // ---- prefetch the L-1 oldest actions of the history ring into the obs tile (LDS-DMA).
       // Issued only now: hipcc waits vmcnt(0) at the next use of an ordinary load while an
       // LDS-DMA is in flight, so issuing it before the state/action loads were consumed would
@@ -183,6 +206,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
       }
     }
   }
+  GPD_STAMP(2);
   // final readback (:374) -> obs / reward / done
   R qn[4], Rm[9];
   readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
@@ -240,28 +264,24 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
 
   float row12[12] = {(float)s.px, (float)s.py, (float)s.pz, roll, pitch, yaw,
                      (float)s.vx, (float)s.vy, (float)s.vz, (float)s.ax, (float)s.ay, (float)s.az};
+  GPD_STAMP(3);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // history DMA has landed in the tile
+  GPD_STAMP(4);
 
+  const int NC = A == 4 ? 3 + v.ring_len : 12 + v.ring_len;  // tile columns (float4 / float)
   if (do_reset) {
-    // terminal row (rare) straight to terminal_obs, then back to INIT_XYZS / INIT_RPYS
+    // the terminal row's state part goes to the tile's extra columns (the history and action
+    // columns are shared with the reset row); the env goes back to INIT_XYZS / INIT_RPYS
     // (_housekeeping :458-477; SB3 DummyVecEnv keeps the last obs as terminal_observation)
-    if (io.terminal_obs && active) {
-      float* trow = io.terminal_obs + n * v.W;
+    if (A == 4) {
+      tile4[(NC + 0) * kPad + tid] = make_float4(row12[0], row12[1], row12[2], row12[3]);
+      tile4[(NC + 1) * kPad + tid] = make_float4(row12[4], row12[5], row12[6], row12[7]);
+      tile4[(NC + 2) * kPad + tid] = make_float4(row12[8], row12[9], row12[10], row12[11]);
+    } else {
 #pragma unroll
-      for (int k = 0; k < 12; ++k) trow[k] = row12[k];
-      for (int k = 0; k < nh; ++k) {
-        if (A == 4) {
-          const float4 h = tile4[(3 + k) * kPad + tid];
-          trow[12 + 4 * k + 0] = h.x; trow[12 + 4 * k + 1] = h.y;
-          trow[12 + 4 * k + 2] = h.z; trow[12 + 4 * k + 3] = h.w;
-        } else {
-          trow[12 + k] = tilef[(12 + k) * kPad + tid];
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < A; ++j) trow[12 + nh * A + j] = a[j];
+      for (int k = 0; k < 12; ++k) tilef[(NC + k) * kPad + tid] = row12[k];
     }
-    const R* ini = v.init + d * 10;
+    const R* ini = MULTI ? v.init + d * 10 : c.init0;
     s.px = ini[0]; s.py = ini[1]; s.pz = ini[2];
     s.qx = ini[3]; s.qy = ini[4]; s.qz = ini[5]; s.qw = ini[6];
     s.vx = s.vy = s.vz = R(0);
@@ -274,7 +294,10 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
 #pragma unroll
     for (int k = 6; k < 12; ++k) row12[k] = 0.0f;
   }
+  // bit r set <=> tile row r belongs to an env that finished this step (tile rows are lanes)
+  const unsigned long long done_rows = __ballot(do_reset && active && io.terminal_obs != nullptr);
 
+  GPD_STAMP(5);
   // ---- state columns + current action into the tile, then coalesced copy-out of the rows
   if (A == 4) {
     tile4[0 * kPad + tid] = make_float4(row12[0], row12[1], row12[2], row12[3]);
@@ -287,57 +310,75 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
     tilef[(12 + nh) * kPad + tid] = a[0];
   }
   __syncthreads();
+  GPD_STAMP(6);
   {
     // lane tid streams tile elements g = tid, tid+64, ... (row-major over the block's rows), six
-    // LDS reads in flight per batch so the LDS latency is paid once per batch, not per store
-    const int NC = A == 4 ? 3 + v.ring_len : 12 + v.ring_len;  // tile columns (float4 / float)
+    // LDS reads in flight per batch.  Branch-free for obs: a lane whose element index passes the
+    // end re-stores the last element (same address, same value).  Rows of envs that finished
+    // this step are also written to terminal_obs (state columns from the extra tile columns).
     const int total = nact * NC;
     const int drow = kWave / NC, dcol = kWave - drow * NC;
     int row = tid / NC, col = tid - (tid / NC) * NC;
     constexpr int U = 6;
-    if (nact == kWave) {
-      // full block: every lane owns exactly NC elements, no guards -> reads batch freely
-      int j = 0;
-      for (; j + U <= NC; j += U) {
-        if (A == 4) {
-          float4 val[U];
+    const int last_row = nact - 1, last_col = NC - 1;
+    const int ncs = A == 4 ? 3 : 12;  // state columns
+    for (int g0 = tid; g0 - tid < total; g0 += U * kWave) {
+      if (A == 4) {
+        float4 val[U];
+        long long idx[U];
+        int rr[U], cc[U];
 #pragma unroll
-          for (int u = 0; u < U; ++u) {
-            val[u] = tile4[col * kPad + row];
-            col += dcol; row += drow;
-            if (col >= NC) { col -= NC; ++row; }
-          }
-          float4* dst = reinterpret_cast<float4*>(io.obs) + n0 * NC + tid + j * kWave;
-#pragma unroll
-          for (int u = 0; u < U; ++u) dst[u * kWave] = val[u];
-        } else {
-          float val[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            val[u] = tilef[col * kPad + row];
-            col += dcol; row += drow;
-            if (col >= NC) { col -= NC; ++row; }
-          }
-          float* dst = io.obs + n0 * NC + tid + j * kWave;
-#pragma unroll
-          for (int u = 0; u < U; ++u) dst[u * kWave] = val[u];
+        for (int u = 0; u < U; ++u) {
+          const bool ok = g0 + u * kWave < total;
+          rr[u] = ok ? row : last_row;
+          cc[u] = ok ? col : last_col;
+          val[u] = tile4[cc[u] * kPad + rr[u]];
+          idx[u] = ok ? (long long)(g0 + u * kWave) : (long long)(total - 1);
+          col += dcol; row += drow;
+          if (col >= NC) { col -= NC; ++row; }
         }
-      }
-      for (; j < NC; ++j) {
-        if (A == 4) reinterpret_cast<float4*>(io.obs)[n0 * NC + tid + j * kWave] = tile4[col * kPad + row];
-        else io.obs[n0 * NC + tid + j * kWave] = tilef[col * kPad + row];
-        col += dcol; row += drow;
-        if (col >= NC) { col -= NC; ++row; }
-      }
-    } else {
-      for (int g = tid; g < total; g += kWave) {  // partial last block
-        if (A == 4) reinterpret_cast<float4*>(io.obs)[n0 * NC + g] = tile4[col * kPad + row];
-        else io.obs[n0 * NC + g] = tilef[col * kPad + row];
-        col += dcol; row += drow;
-        if (col >= NC) { col -= NC; ++row; }
+        float4* dst = reinterpret_cast<float4*>(io.obs) + n0 * NC;
+#pragma unroll
+        for (int u = 0; u < U; ++u) dst[idx[u]] = val[u];
+        if (done_rows) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if ((done_rows >> rr[u]) & 1ull) {
+              const float4 tv = cc[u] < ncs ? tile4[(NC + cc[u]) * kPad + rr[u]] : val[u];
+              reinterpret_cast<float4*>(io.terminal_obs)[n0 * NC + idx[u]] = tv;
+            }
+          }
+        }
+      } else {
+        float val[U];
+        long long idx[U];
+        int rr[U], cc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const bool ok = g0 + u * kWave < total;
+          rr[u] = ok ? row : last_row;
+          cc[u] = ok ? col : last_col;
+          val[u] = tilef[cc[u] * kPad + rr[u]];
+          idx[u] = ok ? (long long)(g0 + u * kWave) : (long long)(total - 1);
+          col += dcol; row += drow;
+          if (col >= NC) { col -= NC; ++row; }
+        }
+        float* dst = io.obs + n0 * NC;
+#pragma unroll
+        for (int u = 0; u < U; ++u) dst[idx[u]] = val[u];
+        if (done_rows) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if ((done_rows >> rr[u]) & 1ull) {
+              const float tv = cc[u] < ncs ? tilef[(NC + cc[u]) * kPad + rr[u]] : val[u];
+              io.terminal_obs[n0 * NC + idx[u]] = tv;
+            }
+          }
+        }
       }
     }
   }
+  GPD_STAMP(7);
   if (!active) return;
   store_drone(v, n, s, last);
   if (d == 0) {
@@ -371,7 +412,7 @@ __global__ __launch_bounds__(kWave) void integrate_kernel(SimView<R> v, const Co
     R rpm[4];
     const R* src = rpm_in + ((long long)t * N + nn) * 4;
     rpm[0] = src[0]; rpm[1] = src[1]; rpm[2] = src[2]; rpm[3] = src[3];
-    substep_block<R, MULTI>(s, rpm, last, c, sx, sy, sz, tid, base, D);
+    substep_block<R, MULTI, false>(s, rpm, last, c, sx, sy, sz, tid, base, D);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];
     if (traj && active) {

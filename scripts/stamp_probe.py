@@ -1,0 +1,33 @@
+"""Phase timing of step_kernel from the diagnostic build (GPD_LIB=.../libgpd_stamps.so).
+
+Phases (lane 0 of every block, s_memtime shader clocks):
+ 0 entry -> 1 state/action loads consumed + first substep -> 2 all substeps ->
+ 3 task hooks / obs angles -> 4 history DMA landed -> 5 reset/terminal rows -> 6 tile written +
+ barrier -> 7 tile copy-out issued."""
+import ctypes, os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ["GPD_LIB"] = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                     "gym_pybullet_drones_routing_amd", "libgpd_stamps.so")
+import numpy as np, torch
+from gym_pybullet_drones_routing_amd import _lib
+from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+lib = _lib.load()
+lib.gpd_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+for prec in ("f64", "f32"):
+    for E in (4096, 1 << 20):
+        sim = BatchedAviarySim(n_envs=E, task="hover", precision=prec, device="cuda:0")
+        scale = float(os.environ.get("ACT_SCALE", "1.0"))
+        acts = [((torch.rand((E, 1, 4), device="cuda:0") * 2 - 1) * scale).contiguous() for _ in range(16)]
+        g = sim.capture_graph(acts)
+        for _ in range(4): g.replay()
+        torch.cuda.synchronize()
+        nb = min(65536, (E + 63) // 64)
+        buf = np.zeros((nb, 8), np.uint64)
+        assert lib.gpd_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), nb) == 0
+        t = buf[:, :8].astype(np.int64)
+        d = np.diff(t, axis=1)
+        start = t[:, 0] - t[:, 0].min()
+        print(f"{prec} E={E}: per-block phase cycles (median) " +
+              " ".join(f"{k}->{k+1}:{int(np.median(d[:, k]))}" for k in range(7)) +
+              f" | total median {int(np.median(t[:,7]-t[:,0]))}", flush=True)
+        sim.close()
