@@ -142,6 +142,7 @@ Consts<R> make_consts(const gpd_sim* s) {
     c.rz[k] = (R)P.prop_pos[k][2];
   }
   for (int k = 0; k < 10; ++k) c.init0[k] = (R)s->init_tmpl[k];
+  for (int k = 0; k < 3; ++k) c.target0[k] = (R)s->target[k];
   c.hover_f32 = (float)s->K.hover_rpm;
   c.model = P.model;
   c.flags = s->cfg.physics_flags;

@@ -69,6 +69,7 @@ struct Consts {
   R inv_m;                 // 1/M      (F/M as a multiply; differs from the division by <= 1 ulp)
   R rpm2rad;               // 2*pi/60  (drag: sum(2*pi*rpm/60))
   R init0[10];             // reset template of drone 0 (pos, stored quat, rpy): single-drone envs
+  R target0[3];            // task target of drone 0 (single-drone envs: no dependent global load)
                            // read it with scalar loads instead of a dependent per-lane load
   float hover_f32;         // float32(HOVER_RPM) (numpy 1.x casting, BaseRLAviary.py:192)
   int model, flags, nsub;
@@ -366,7 +367,9 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
 //   rpm  : this ctrl step's clipped action (current substep)
 //   last : self.last_clipped_action (previous ctrl step's rpm on the first substep)
 //   dwsum: summed downwash force along body z (already reduced over the env's drones)
-template <typename R, bool FAST>
+// ANGV: also update the world-frame ang_v (write-only for the dynamics: only the value after the
+// last substep of a control step is ever observed, so earlier substeps skip it).
+template <typename R, bool FAST, bool ANGV = true>
 __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R Rm[9], bool gnd_upright,
                                             const R rpm[4], const R last[4], R dwsum,
                                             const Consts<R>& c) {
@@ -418,6 +421,7 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R 
     s.qx = qn[0]; s.qy = qn[1]; s.qz = qn[2]; s.qw = qn[3];
   }
   // resetBaseVelocity(..., np.dot(rotation, rpy_rates))  :868-872
+  if (!ANGV) return;
   s.ax = (Rm[0] * s.wx + Rm[1] * s.wy) + Rm[2] * s.wz;
   s.ay = (Rm[3] * s.wx + Rm[4] * s.wy) + Rm[5] * s.wz;
   s.az = (Rm[6] * s.wx + Rm[7] * s.wy) + Rm[8] * s.wz;

@@ -116,7 +116,7 @@ __device__ __forceinline__ void store_drone(const SimView<R>& v, long long n, co
 
 // One physics substep of every drone of the block, including the readback that precedes it
 // (BaseAviary.py:343-372 loop body).  MULTI: envs have D > 1 drones and may need downwash.
-template <typename R, bool MULTI, bool FAST>
+template <typename R, bool MULTI, bool FAST, bool ANGV = true>
 __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const R last[4], const Consts<R>& c,
                                               R* sx, R* sy, R* sz, int tid, int base, int D) {
   R qn[4], Rm[9];
@@ -130,7 +130,7 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
     dw = downwash_sum(s.px, s.py, s.pz, sx, sy, sz, base, D, c);
     __syncthreads();
   }
-  dyn_substep<R, FAST>(s, qn, Rm, up, rpm, last, dw, c);
+  dyn_substep<R, FAST, ANGV>(s, qn, Rm, up, rpm, last, dw, c);
 }
 
 // Bytes of dynamic LDS the step kernel needs for its observation tile: the row's columns
@@ -185,27 +185,35 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
 
   const int nh = v.ring_len - 1;
   const long long slot_stride = v.npad * A;
-  for (int it = 0; it < c.nsub; ++it) {
-    substep_block<R, MULTI, FAST>(s, rpm, last, c, sx, sy, sz, tid, base, D);
+  // history ring -> obs tile: the L-1 oldest actions (LDS-DMA).  Issued after the first
+  // substep: hipcc waits vmcnt(0) at the next use of an ordinary load while an LDS-DMA is in
+  // flight, so issuing it before the state/action loads were consumed would put the DMA round
+  // trip on the critical path.  Issued there it overlaps the remaining substeps.
+  auto history_dma = [&]() {
+    for (int k = 0; k < nh; ++k) {
+      int slot = head + 1 + k;
+      slot -= slot >= v.ring_len ? v.ring_len : 0;
+      const float* src = v.ring + (long long)slot * slot_stride + nn * A;
+      if (A == 4)
+        __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tile4 + (3 + k) * kPad), 16, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tilef + (12 + k) * kPad), 4, 0, 0);
+    }
+  };
+  // substeps 1..nsub-1 skip the (write-only) world ang_v; the last one produces it
+  for (int it = 0; it < c.nsub - 1; ++it) {
+    substep_block<R, MULTI, FAST, false>(s, rpm, last, c, sx, sy, sz, tid, base, D);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
     if (it == 0) {
       GPD_STAMP(1);
-      // ---- prefetch the L-1 oldest actions of the history ring into the obs tile (LDS-DMA).
-      // Issued only now: hipcc waits vmcnt(0) at the next use of an ordinary load while an
-      // LDS-DMA is in flight, so issuing it before the state/action loads were consumed would
-      // put the DMA round trip on the critical path.  Here it overlaps substeps 1..7.
-      for (int k = 0; k < nh; ++k) {
-        int slot = head + 1 + k;
-        slot -= slot >= v.ring_len ? v.ring_len : 0;
-        const float* src = v.ring + (long long)slot * slot_stride + nn * A;
-        if (A == 4)
-          __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tile4 + (3 + k) * kPad), 16, 0, 0);
-        else
-          __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tilef + (12 + k) * kPad), 4, 0, 0);
-      }
+      history_dma();
     }
   }
+  substep_block<R, MULTI, FAST, true>(s, rpm, last, c, sx, sy, sz, tid, base, D);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) last[k] = rpm[k];
+  if (c.nsub == 1) history_dma();
   GPD_STAMP(2);
   // final readback (:374) -> obs / reward / done
   R qn[4], Rm[9];
@@ -218,7 +226,8 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
   float reward = -1.0f;
   bool term = false, trunc = false;
   if (v.task != TASK_NONE) {
-    const R tx = v.target[d * 3 + 0] - s.px, ty = v.target[d * 3 + 1] - s.py, tz = v.target[d * 3 + 2] - s.pz;
+    const R* tg = MULTI ? v.target + d * 3 : c.target0;
+    const R tx = tg[0] - s.px, ty = tg[1] - s.py, tz = tg[2] - s.pz;
     const R dist = g_sqrt(tx * tx + ty * ty + tz * tz);
     const R d2 = dist * dist;
     R r = R(2) - d2 * d2;
