@@ -11,7 +11,7 @@ PKG_DIR = pathlib.Path(__file__).resolve().parent
 CSRC = PKG_DIR / "csrc"
 INCLUDE = PKG_DIR.parent / "include"
 LIB_PATH = PKG_DIR / "libgpd.so"
-SOURCES = [CSRC / "gpd.hip", CSRC / "gpd_kernels.h", CSRC / "gpd_device.h", INCLUDE / "gpd.h"]
+SOURCES = [CSRC / "gpd.hip", CSRC / "gpd_kernels.h", CSRC / "gpd_device.h", CSRC / "gpd_ctrl.h", INCLUDE / "gpd.h"]
 ARCH = os.environ.get("GPD_OFFLOAD_ARCH", "gfx950")
 
 

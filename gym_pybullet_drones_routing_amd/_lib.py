@@ -21,7 +21,9 @@ GPD_ENOMEM = -3
 GPD_EUNSUPPORTED = -4
 
 GPD_MODEL_CF2X, GPD_MODEL_CF2P, GPD_MODEL_RACE = 0, 1, 2
-GPD_ACT_RPM, GPD_ACT_ONE_D_RPM = 0, 1
+GPD_ACT_RPM, GPD_ACT_ONE_D_RPM, GPD_ACT_PID, GPD_ACT_VEL, GPD_ACT_ONE_D_PID = 0, 1, 2, 3, 4
+GPD_ABI_VERSION = 2
+CTRL_COMPS = 9  # integral_pos_e(3) integral_rpy_e(3) last_rpy(3)
 GPD_TASK_NONE, GPD_TASK_HOVER, GPD_TASK_MULTIHOVER = 0, 1, 2
 GPD_F_GND, GPD_F_DRAG, GPD_F_DW, GPD_F_GEOM_WRENCH = 1, 2, 4, 8
 GPD_F32, GPD_F64 = 0, 1
@@ -30,7 +32,8 @@ GPD_F32, GPD_F64 = 0, 1
 EXPORTED = ("gpd_abi_version", "gpd_last_error", "gpd_default_params", "gpd_create", "gpd_destroy",
             "gpd_get_constants", "gpd_reset", "gpd_step", "gpd_integrate", "gpd_get_state20",
             "gpd_get_raw_state", "gpd_set_raw_state", "gpd_get_step_counters",
-            "gpd_set_step_counters", "gpd_state_bytes", "gpd_save_state", "gpd_load_state")
+            "gpd_set_step_counters", "gpd_state_bytes", "gpd_save_state", "gpd_load_state",
+            "gpd_default_pid_params", "gpd_set_pid_params", "gpd_get_ctrl_state", "gpd_set_ctrl_state")
 
 
 class GpdLibraryError(RuntimeError):
@@ -49,6 +52,13 @@ class DroneParams(ctypes.Structure):
         "collision_h", "collision_r", "collision_z_offset", "max_speed_kmh",
         "gnd_eff_coeff", "prop_radius", "drag_coeff_xy", "drag_coeff_z",
         "dw_coeff_1", "dw_coeff_2", "dw_coeff_3")] + [("prop_pos", (ctypes.c_double * 3) * 4)]
+
+
+class PidParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double * 3) for n in (
+        "p_coeff_for", "i_coeff_for", "d_coeff_for", "p_coeff_tor", "i_coeff_tor", "d_coeff_tor")] + \
+        [(n, ctypes.c_double) for n in ("pwm2rpm_scale", "pwm2rpm_const", "min_pwm", "max_pwm")] + \
+        [("mixer", (ctypes.c_double * 3) * 4)] + [(n, ctypes.c_double) for n in ("gravity", "kf")]
 
 
 class Config(ctypes.Structure):
@@ -102,11 +112,17 @@ def load():
         "gpd_state_bytes": (ctypes.c_size_t, [vp]),
         "gpd_save_state": (ci, [vp, vp, vp]),
         "gpd_load_state": (ci, [vp, vp, vp]),
+        "gpd_default_pid_params": (ci, [ctypes.POINTER(PidParams)]),
+        "gpd_set_pid_params": (ci, [vp, ctypes.POINTER(PidParams)]),
+        "gpd_get_ctrl_state": (ci, [vp, vp, vp]),
+        "gpd_set_ctrl_state": (ci, [vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.gpd_abi_version() != GPD_ABI_VERSION:
+        raise GpdLibraryError(f"{LIB_PATH} has ABI {lib.gpd_abi_version()}, this binding expects {GPD_ABI_VERSION}: rebuild it")
     _lib = lib
     return lib
 
@@ -115,6 +131,13 @@ def check(fn_name, rc):
     if rc != GPD_OK:
         raise GpdError(fn_name, rc, _lib.gpd_last_error().decode(errors="replace"))
     return rc
+
+
+def default_pid_params():
+    lib = load()
+    q = PidParams()
+    check("gpd_default_pid_params", lib.gpd_default_pid_params(ctypes.byref(q)))
+    return q
 
 
 def default_params(model):

@@ -20,6 +20,11 @@
 
 using namespace gpd;
 
+static_assert(GPD_ACT_RPM == ACT_RPM && GPD_ACT_ONE_D_RPM == ACT_ONE_D_RPM && GPD_ACT_PID == ACT_PID &&
+                  GPD_ACT_VEL == ACT_VEL && GPD_ACT_ONE_D_PID == ACT_ONE_D_PID,
+              "action type codes of gpd.h and the kernels must agree");
+constexpr int kCtrlComps = 9;
+
 namespace {
 
 thread_local std::string g_err;
@@ -96,11 +101,13 @@ void h_quat_from_euler(const double rpy[3], double q[4]) {  // btQuaternion::set
 
 struct gpd_sim {
   gpd_drone_params P;
+  gpd_pid_params pid;
   gpd_config cfg;
   gpd_constants K;
   int E, D, N, A, W, nsub, ring_len, prec, tpb;
   long long npad;
   void* d_state = nullptr;
+  void* d_ctrl = nullptr;         // [9][npad] DSLPIDControl state (PID action types)
   float* d_ring = nullptr;
   int2* d_ctr = nullptr;          // [E] {step_counter, ring head}
   void* d_init = nullptr;
@@ -147,6 +154,19 @@ Consts<R> make_consts(const gpd_sim* s) {
   c.model = P.model;
   c.flags = s->cfg.physics_flags;
   c.nsub = s->nsub;
+  const gpd_pid_params& Q = s->pid;
+  PidConsts<R>& k = c.pid;
+  for (int i = 0; i < 3; ++i) {
+    k.p_for[i] = (R)Q.p_coeff_for[i]; k.i_for[i] = (R)Q.i_coeff_for[i]; k.d_for[i] = (R)Q.d_coeff_for[i];
+    k.p_tor[i] = (R)Q.p_coeff_tor[i]; k.i_tor[i] = (R)Q.i_coeff_tor[i]; k.d_tor[i] = (R)Q.d_coeff_tor[i];
+  }
+  k.pwm2rpm_scale = (R)Q.pwm2rpm_scale; k.pwm2rpm_const = (R)Q.pwm2rpm_const;
+  k.min_pwm = (R)Q.min_pwm; k.max_pwm = (R)Q.max_pwm;
+  for (int j = 0; j < 4; ++j)
+    for (int i = 0; i < 3; ++i) k.mixer[j * 3 + i] = (R)Q.mixer[j][i];
+  k.gravity = (R)Q.gravity; k.kf = (R)Q.kf;
+  k.ctrl_dt = (R)s->K.ctrl_timestep;
+  k.speed_limit = 0.03 * P.max_speed_kmh * (1000.0 / 3600.0);
   return c;
 }
 
@@ -154,6 +174,7 @@ template <typename R>
 SimView<R> make_view(const gpd_sim* s) {
   SimView<R> v;
   v.state = (R*)s->d_state;
+  v.ctrl = (R*)s->d_ctrl;
   v.ring = s->d_ring;
   v.ctr = s->d_ctr;
   v.init = (const R*)s->d_init;
@@ -167,6 +188,30 @@ SimView<R> make_view(const gpd_sim* s) {
   return v;
 }
 
+// The step_kernel instantiation of a sim: action type x (D > 1) x (plain DYN fast path).  The
+// fast specialisation exists for the RPM action types only (the bench path).
+template <typename R, int ACT>
+const void* step_fn_act(bool multi, bool fast) {
+  if (multi) return fast ? (const void*)step_kernel<R, ACT, true, true> : (const void*)step_kernel<R, ACT, true, false>;
+  return fast ? (const void*)step_kernel<R, ACT, false, true> : (const void*)step_kernel<R, ACT, false, false>;
+}
+template <typename R, int ACT>
+const void* step_fn_pid(bool multi) {
+  return multi ? (const void*)step_kernel<R, ACT, true, false> : (const void*)step_kernel<R, ACT, false, false>;
+}
+template <typename R>
+const void* step_kernel_fn(const gpd_sim* s) {
+  const bool multi = s->D > 1;
+  const bool fast = s->cfg.physics_flags == 0;
+  switch (s->cfg.act_type) {
+    case GPD_ACT_RPM: return step_fn_act<R, ACT_RPM>(multi, fast);
+    case GPD_ACT_ONE_D_RPM: return step_fn_act<R, ACT_ONE_D_RPM>(multi, fast);
+    case GPD_ACT_PID: return step_fn_pid<R, ACT_PID>(multi);
+    case GPD_ACT_VEL: return step_fn_pid<R, ACT_VEL>(multi);
+    default: return step_fn_pid<R, ACT_ONE_D_PID>(multi);
+  }
+}
+
 template <typename R>
 int upload_tables(gpd_sim* s) {
   std::vector<R> ini(s->init_tmpl.begin(), s->init_tmpl.end());
@@ -177,12 +222,8 @@ int upload_tables(gpd_sim* s) {
   HIP_TRY(hipMemcpy(s->d_consts, &c, sizeof(c), hipMemcpyHostToDevice));
   // the observation tile can exceed the 64 KiB default dynamic-LDS limit for long histories
   if (s->tile_bytes > 65536) {
-    const void* fns[8] = {(const void*)step_kernel<R, 4, true, true>, (const void*)step_kernel<R, 4, false, true>,
-                          (const void*)step_kernel<R, 1, true, true>, (const void*)step_kernel<R, 1, false, true>,
-                          (const void*)step_kernel<R, 4, true, false>, (const void*)step_kernel<R, 4, false, false>,
-                          (const void*)step_kernel<R, 1, true, false>, (const void*)step_kernel<R, 1, false, false>};
-    for (const void* f : fns)
-      HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, s->tile_bytes));
+    const void* f = step_kernel_fn<R>(s);
+    HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, s->tile_bytes));
   }
   return GPD_OK;
 }
@@ -200,19 +241,10 @@ int launch_step(gpd_sim* s, const float* actions, float* obs, float* reward, uin
   const SimView<R> v = make_view<R>(s);
   const Consts<R>* c = (const Consts<R>*)s->d_consts;
   const unsigned grid = grid_for(s->N, s->tpb);
-  const bool multi = s->D > 1;
   const size_t lds = (size_t)s->tile_bytes;
-  const bool fast = s->cfg.physics_flags == 0;
-#define GPD_LAUNCH_STEP(A_, M_, F_) \
-  hipLaunchKernelGGL((step_kernel<R, A_, M_, F_>), dim3(grid), dim3(kWave), lds, st, v, io, c)
-  if (s->A == 4) {
-    if (multi) { if (fast) GPD_LAUNCH_STEP(4, true, true); else GPD_LAUNCH_STEP(4, true, false); }
-    else { if (fast) GPD_LAUNCH_STEP(4, false, true); else GPD_LAUNCH_STEP(4, false, false); }
-  } else {
-    if (multi) { if (fast) GPD_LAUNCH_STEP(1, true, true); else GPD_LAUNCH_STEP(1, true, false); }
-    else { if (fast) GPD_LAUNCH_STEP(1, false, true); else GPD_LAUNCH_STEP(1, false, false); }
-  }
-#undef GPD_LAUNCH_STEP
+  typedef void (*StepFn)(SimView<R>, StepIO<R>, const Consts<R>*);
+  const StepFn f = (StepFn)step_kernel_fn<R>(s);
+  hipLaunchKernelGGL(f, dim3(grid), dim3(kWave), lds, st, v, io, c);
   HIP_TRY(hipGetLastError());
   return GPD_OK;
 }
@@ -257,6 +289,7 @@ int launch_set_raw(gpd_sim* s, const void* in, hipStream_t st) {
 void free_sim(gpd_sim* s) {
   if (!s) return;
   if (s->d_state) (void)hipFree(s->d_state);
+  if (s->d_ctrl) (void)hipFree(s->d_ctrl);
   if (s->d_ring) (void)hipFree(s->d_ring);
   if (s->d_ctr) (void)hipFree(s->d_ctr);
   if (s->d_init) (void)hipFree(s->d_init);
@@ -320,8 +353,11 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     return fail(GPD_EINVAL, "[ERROR] in BaseAviary.__init__(), pyb_freq is not divisible by env_freq.");
   if (C.ctrl_freq / 2 < 1)
     return fail(GPD_EUNSUPPORTED, "gpd_create: ctrl_freq//2 == 0 gives an empty action buffer (unsupported)");
-  if (C.act_type != GPD_ACT_RPM && C.act_type != GPD_ACT_ONE_D_RPM)
-    return fail(GPD_EUNSUPPORTED, "gpd_create: only ActionType.RPM / ONE_D_RPM run on this path");
+  if (C.act_type < GPD_ACT_RPM || C.act_type > GPD_ACT_ONE_D_PID) return fail(GPD_EINVAL, "gpd_create: bad act_type");
+  const bool pid = act_is_pid(C.act_type);
+  if (pid && params->model != GPD_MODEL_CF2X && params->model != GPD_MODEL_CF2P)  // BaseRLAviary.py:75-78
+    return fail(GPD_EUNSUPPORTED,
+                "[ERROR] in BaseRLAviary.__init()__, no controller is available for the specified drone_model");
   if (C.task < GPD_TASK_NONE || C.task > GPD_TASK_MULTIHOVER) return fail(GPD_EINVAL, "gpd_create: bad task");
   if (C.task == GPD_TASK_HOVER && C.drones_per_env != 1)
     return fail(GPD_EINVAL, "gpd_create: HoverAviary is single-drone (drones_per_env must be 1)");
@@ -341,7 +377,8 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   s->E = C.n_envs;
   s->D = C.drones_per_env;
   s->N = (int)Nll;
-  s->A = C.act_type == GPD_ACT_RPM ? 4 : 1;
+  s->A = act_width(C.act_type);
+  gpd_default_pid_params(&s->pid);
   s->ring_len = C.ctrl_freq / 2;  // ACTION_BUFFER_SIZE = int(ctrl_freq//2)  BaseRLAviary.py:66
   s->W = 12 + s->ring_len * s->A;
   s->nsub = C.pyb_freq / C.ctrl_freq;
@@ -434,8 +471,9 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   hipError_t e4 = hipMalloc(&s->d_init, (size_t)s->D * 10 * rs);
   hipError_t e5 = hipMalloc(&s->d_target, (size_t)s->D * 3 * rs);
   hipError_t e6 = hipMalloc(&s->d_consts, s->prec == GPD_F64 ? sizeof(Consts<double>) : sizeof(Consts<float>));
+  hipError_t e7 = pid ? hipMalloc(&s->d_ctrl, (size_t)kCtrlComps * s->npad * rs) : hipSuccess;
   if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess ||
-      e6 != hipSuccess) {
+      e6 != hipSuccess || e7 != hipSuccess) {
     free_sim(s);
     (void)hipGetLastError();
     return fail(GPD_ENOMEM, "gpd_create: hipMalloc failed");
@@ -444,7 +482,8 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   if (rc != GPD_OK) { free_sim(s); return rc; }
   if (hipMemset(s->d_state, 0, (size_t)kStateComps * s->npad * rs) != hipSuccess ||
       hipMemset(s->d_ring, 0, (size_t)s->ring_len * s->npad * s->A * sizeof(float)) != hipSuccess ||
-      hipMemset(s->d_ctr, 0, (size_t)s->E * sizeof(int2)) != hipSuccess) {
+      hipMemset(s->d_ctr, 0, (size_t)s->E * sizeof(int2)) != hipSuccess ||
+      (pid && hipMemset(s->d_ctrl, 0, (size_t)kCtrlComps * s->npad * rs) != hipSuccess)) {
     free_sim(s);
     return fail(GPD_EHIP, "gpd_create: hipMemset failed");
   }
@@ -514,6 +553,64 @@ int gpd_set_raw_state(gpd_sim* sim, const void* in, void* stream) {
   return sim->prec == GPD_F64 ? launch_set_raw<double>(sim, in, st) : launch_set_raw<float>(sim, in, st);
 }
 
+int gpd_default_pid_params(gpd_pid_params* out) {
+  if (!out) return fail(GPD_EINVAL, "gpd_default_pid_params: out is NULL");
+  gpd_pid_params q;
+  std::memset(&q, 0, sizeof(q));
+  const double pf[3] = {.4, .4, 1.25}, iff[3] = {.05, .05, .05}, df[3] = {.2, .2, .5};       // :37-39
+  const double pt[3] = {70000., 70000., 60000.}, it[3] = {.0, .0, 500.}, dtq[3] = {20000., 20000., 12000.};  // :40-42
+  const double mix[4][3] = {{-.5, -.5, -1}, {-.5, .5, 1}, {.5, .5, -1}, {.5, -.5, 1}};     // :48-53 (CF2X)
+  for (int i = 0; i < 3; ++i) {
+    q.p_coeff_for[i] = pf[i]; q.i_coeff_for[i] = iff[i]; q.d_coeff_for[i] = df[i];
+    q.p_coeff_tor[i] = pt[i]; q.i_coeff_tor[i] = it[i]; q.d_coeff_tor[i] = dtq[i];
+  }
+  q.pwm2rpm_scale = 0.2685; q.pwm2rpm_const = 4070.3; q.min_pwm = 20000; q.max_pwm = 65535;  // :43-46
+  std::memcpy(q.mixer, mix, sizeof(mix));
+  q.gravity = 9.8 * 0.027;  // g * m of cf2x.urdf:11 (BaseControl.py:35)
+  q.kf = 3.16e-10;          // cf2x.urdf:5 (BaseControl.py:37)
+  *out = q;
+  return GPD_OK;
+}
+
+int gpd_set_pid_params(gpd_sim* sim, const gpd_pid_params* params) {
+  if (!sim || !params) return fail(GPD_EINVAL, "gpd_set_pid_params: NULL argument");
+  if (!act_is_pid(sim->cfg.act_type))
+    return fail(GPD_EINVAL, "gpd_set_pid_params: the sim's action type has no controller");
+  sim->pid = *params;
+  HIP_TRY(hipDeviceSynchronize());
+  return sim->prec == GPD_F64 ? upload_tables<double>(sim) : upload_tables<float>(sim);
+}
+
+int gpd_get_ctrl_state(gpd_sim* sim, void* out, void* stream) {
+  if (!sim || !out) return fail(GPD_EINVAL, "gpd_get_ctrl_state: NULL argument");
+  if (!sim->d_ctrl) return fail(GPD_EINVAL, "gpd_get_ctrl_state: the sim's action type has no controller");
+  const unsigned g = grid_for(sim->N, 256);
+  hipStream_t st = (hipStream_t)stream;
+  if (sim->prec == GPD_F64)
+    hipLaunchKernelGGL((soa_to_rows_kernel<double>), dim3(g), dim3(256), 0, st, (const double*)sim->d_ctrl, sim->npad,
+                       kCtrlComps, sim->N, (double*)out);
+  else
+    hipLaunchKernelGGL((soa_to_rows_kernel<float>), dim3(g), dim3(256), 0, st, (const float*)sim->d_ctrl, sim->npad,
+                       kCtrlComps, sim->N, (float*)out);
+  HIP_TRY(hipGetLastError());
+  return GPD_OK;
+}
+
+int gpd_set_ctrl_state(gpd_sim* sim, const void* in, void* stream) {
+  if (!sim || !in) return fail(GPD_EINVAL, "gpd_set_ctrl_state: NULL argument");
+  if (!sim->d_ctrl) return fail(GPD_EINVAL, "gpd_set_ctrl_state: the sim's action type has no controller");
+  const unsigned g = grid_for(sim->N, 256);
+  hipStream_t st = (hipStream_t)stream;
+  if (sim->prec == GPD_F64)
+    hipLaunchKernelGGL((rows_to_soa_kernel<double>), dim3(g), dim3(256), 0, st, (const double*)in, sim->npad, kCtrlComps,
+                       sim->N, (double*)sim->d_ctrl);
+  else
+    hipLaunchKernelGGL((rows_to_soa_kernel<float>), dim3(g), dim3(256), 0, st, (const float*)in, sim->npad, kCtrlComps,
+                       sim->N, (float*)sim->d_ctrl);
+  HIP_TRY(hipGetLastError());
+  return GPD_OK;
+}
+
 int gpd_get_step_counters(gpd_sim* sim, int32_t* out, void* stream) {
   if (!sim || !out) return fail(GPD_EINVAL, "gpd_get_step_counters: NULL argument");
   HIP_TRY(hipMemcpy2DAsync(out, sizeof(int32_t), sim->d_ctr, sizeof(int2), sizeof(int32_t), (size_t)sim->E,
@@ -528,25 +625,40 @@ int gpd_set_step_counters(gpd_sim* sim, const int32_t* in, void* stream) {
   return GPD_OK;
 }
 
+namespace {
+// checkpoint sections: state, controller state (PID types), action ring, counters
+struct Section { void* dev; size_t bytes; };
+int sections(gpd_sim* sim, Section out[4]) {
+  out[0] = {sim->d_state, (size_t)kStateComps * sim->npad * real_size(sim)};
+  out[1] = {sim->d_ctrl, sim->d_ctrl ? (size_t)kCtrlComps * sim->npad * real_size(sim) : 0};
+  out[2] = {sim->d_ring, (size_t)sim->ring_len * sim->npad * sim->A * sizeof(float)};
+  out[3] = {sim->d_ctr, (size_t)sim->E * sizeof(int2)};
+  return 4;
+}
+}  // namespace
+
 size_t gpd_state_bytes(const gpd_sim* sim) {
   if (!sim) return 0;
-  return 16 + (size_t)kStateComps * sim->npad * real_size(sim) +
-         (size_t)sim->ring_len * sim->npad * sim->A * sizeof(float) + (size_t)sim->E * sizeof(int2);
+  Section sec[4];
+  const int ns = sections(const_cast<gpd_sim*>(sim), sec);
+  size_t total = 32;
+  for (int i = 0; i < ns; ++i) total += sec[i].bytes;
+  return total;
 }
 
 int gpd_save_state(gpd_sim* sim, void* blob_host, void* stream) {
   if (!sim || !blob_host) return fail(GPD_EINVAL, "gpd_save_state: NULL argument");
   hipStream_t st = (hipStream_t)stream;
   char* b = (char*)blob_host;
-  int64_t hdr[2] = {(int64_t)GPD_ABI_VERSION, (int64_t)sim->N};
-  std::memcpy(b, hdr, 16);
-  size_t off = 16;
-  const size_t s1 = (size_t)kStateComps * sim->npad * real_size(sim);
-  const size_t s2 = (size_t)sim->ring_len * sim->npad * sim->A * sizeof(float);
-  const size_t s3 = (size_t)sim->E * sizeof(int2);
-  HIP_TRY(hipMemcpyAsync(b + off, sim->d_state, s1, hipMemcpyDeviceToHost, st)); off += s1;
-  HIP_TRY(hipMemcpyAsync(b + off, sim->d_ring, s2, hipMemcpyDeviceToHost, st)); off += s2;
-  HIP_TRY(hipMemcpyAsync(b + off, sim->d_ctr, s3, hipMemcpyDeviceToHost, st));
+  const int64_t hdr[4] = {(int64_t)GPD_ABI_VERSION, (int64_t)sim->N, (int64_t)sim->cfg.act_type, (int64_t)sim->prec};
+  std::memcpy(b, hdr, 32);
+  size_t off = 32;
+  Section sec[4];
+  const int ns = sections(sim, sec);
+  for (int i = 0; i < ns; ++i) {
+    if (sec[i].bytes) HIP_TRY(hipMemcpyAsync(b + off, sec[i].dev, sec[i].bytes, hipMemcpyDeviceToHost, st));
+    off += sec[i].bytes;
+  }
   HIP_TRY(hipStreamSynchronize(st));
   return GPD_OK;
 }
@@ -555,17 +667,17 @@ int gpd_load_state(gpd_sim* sim, const void* blob_host, void* stream) {
   if (!sim || !blob_host) return fail(GPD_EINVAL, "gpd_load_state: NULL argument");
   hipStream_t st = (hipStream_t)stream;
   const char* b = (const char*)blob_host;
-  int64_t hdr[2];
-  std::memcpy(hdr, b, 16);
-  if (hdr[1] != sim->N || hdr[0] != GPD_ABI_VERSION)
+  int64_t hdr[4];
+  std::memcpy(hdr, b, 32);
+  if (hdr[0] != GPD_ABI_VERSION || hdr[1] != sim->N || hdr[2] != sim->cfg.act_type || hdr[3] != sim->prec)
     return fail(GPD_EINVAL, "gpd_load_state: blob does not match this sim");
-  size_t off = 16;
-  const size_t s1 = (size_t)kStateComps * sim->npad * real_size(sim);
-  const size_t s2 = (size_t)sim->ring_len * sim->npad * sim->A * sizeof(float);
-  const size_t s3 = (size_t)sim->E * sizeof(int2);
-  HIP_TRY(hipMemcpyAsync(sim->d_state, b + off, s1, hipMemcpyHostToDevice, st)); off += s1;
-  HIP_TRY(hipMemcpyAsync(sim->d_ring, b + off, s2, hipMemcpyHostToDevice, st)); off += s2;
-  HIP_TRY(hipMemcpyAsync(sim->d_ctr, b + off, s3, hipMemcpyHostToDevice, st));
+  size_t off = 32;
+  Section sec[4];
+  const int ns = sections(sim, sec);
+  for (int i = 0; i < ns; ++i) {
+    if (sec[i].bytes) HIP_TRY(hipMemcpyAsync(sec[i].dev, b + off, sec[i].bytes, hipMemcpyHostToDevice, st));
+    off += sec[i].bytes;
+  }
   HIP_TRY(hipStreamSynchronize(st));
   return GPD_OK;
 }

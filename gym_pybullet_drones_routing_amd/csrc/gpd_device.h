@@ -55,6 +55,19 @@ template <> struct PiC<double> { static constexpr double pi = 3.1415926535897932
 enum : int { MODEL_CF2X = 0, MODEL_CF2P = 1, MODEL_RACE = 2 };
 enum : int { F_GND = 1, F_DRAG = 2, F_DW = 4, F_GEOM = 8 };
 
+// DSLPIDControl coefficients (control/DSLPIDControl.py:37-60, settable like
+// BaseControl.setPIDCoefficients :138-177) and the controller's own constants.
+template <typename R>
+struct PidConsts {
+  R p_for[3], i_for[3], d_for[3];          // P/I/D_COEFF_FOR
+  R p_tor[3], i_tor[3], d_tor[3];          // P/I/D_COEFF_TOR
+  R pwm2rpm_scale, pwm2rpm_const, min_pwm, max_pwm;
+  R mixer[12];                             // MIXER_MATRIX [4][3]
+  R gravity, kf;                           // g*m and KF of the cf2x URDF (BaseControl.py:35-39)
+  R ctrl_dt;                               // CTRL_TIMESTEP = 1./CTRL_FREQ
+  double speed_limit;                      // VEL: 0.03*MAX_SPEED_KMH*(1000/3600)  BaseRLAviary.py:95
+};
+
 template <typename R>
 struct Consts {
   R dt;                    // PYB_TIMESTEP = 1./PYB_FREQ              BaseAviary.py:83
@@ -73,6 +86,7 @@ struct Consts {
                            // read it with scalar loads instead of a dependent per-lane load
   float hover_f32;         // float32(HOVER_RPM) (numpy 1.x casting, BaseRLAviary.py:192)
   int model, flags, nsub;
+  PidConsts<R> pid;        // PID / VEL / ONE_D_PID action types only
 };
 
 template <typename R>

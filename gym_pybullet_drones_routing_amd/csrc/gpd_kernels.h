@@ -24,6 +24,7 @@
 //   * the 12 state columns and the current action are written from registers at the end;
 //   * the tile is then streamed out with fully coalesced 16-byte (A=4) / 4-byte (A=1) stores.
 #pragma once
+#include "gpd_ctrl.h"
 #include "gpd_device.h"
 
 namespace gpd {
@@ -58,6 +59,7 @@ typedef __attribute__((address_space(1))) void* gbl_void_ptr;
 template <typename R>
 struct SimView {
   R* state;               // [20][npad]
+  R* ctrl;                // [9][npad] DSLPIDControl state (PID action types only, else null)
   float* ring;            // [ring_len][npad*A]
   int2* ctr;              // [E] {step_counter, ring head}
   const R* init;          // [D][10]
@@ -136,17 +138,21 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
 // Bytes of dynamic LDS the step kernel needs for its observation tile: the row's columns
 // (state, history, current action) plus the first 12 floats of the terminal row (pre-reset
 // state of envs that finish this step; the rest of a terminal row equals the reset row).
+// A == 4 keeps float4 columns (state 3, history+action L, terminal 3); A == 1 / 3 keep float
+// columns (state 12, history+action L*A, terminal 12).
 __host__ __device__ inline int step_tile_bytes(int A, int ring_len) {
-  return A == 4 ? (3 + ring_len + 3) * kPad * 16 : (12 + ring_len + 12) * kPad * 4;
+  return A == 4 ? (3 + ring_len + 3) * kPad * 16 : (12 + ring_len * A + 12) * kPad * 4;
 }
 
 // ---------------------------------------------------------------------------------------
 // gpd_step: one env.step() for every env (BaseAviary.py:259-383) in ONE launch.
+// ACT: action type (GPD_ACT_*); PID types run DSLPIDControl before the substeps.
 // FAST: physics_flags == 0 (plain DYN, the bench path) - the aero / PYB-wrench code is compiled out.
-template <typename R, int A, bool MULTI, bool FAST>
+template <typename R, int ACT, bool MULTI, bool FAST>
 __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io, const Consts<R>* __restrict__ cp) {
+  constexpr int A = act_width(ACT);
   extern __shared__ float4 tile4[];          // A == 4: [3+L][kPad] float4
-  float* tilef = reinterpret_cast<float*>(tile4);  // A == 1: [12+L][kPad] float
+  float* tilef = reinterpret_cast<float*>(tile4);  // A == 1, 3: [12+L*A][kPad] float
   __shared__ R sx[MULTI ? 2 * kWave : 1], sy[MULTI ? 2 * kWave : 1], sz[MULTI ? 2 * kWave : 1];
   __shared__ float srew[MULTI ? 2 * kWave : 1], sdist[MULTI ? 2 * kWave : 1];
   __shared__ int sflag[MULTI ? 2 * kWave : 1];
@@ -175,13 +181,29 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
     const float4 a4 = *reinterpret_cast<const float4*>(io.actions + nn * 4);
     a[0] = a4.x; a[1] = a4.y; a[2] = a4.z; a[3] = a4.w;
   } else {
-    a[0] = io.actions[nn];
+#pragma unroll
+    for (int j = 0; j < A; ++j) a[j] = io.actions[nn * A + j];
   }
 
-  // _preprocessAction: rpm = HOVER_RPM*(1+0.05*a)  (BaseRLAviary.py:191-192, :224-225)
   R rpm[4];
+  R cs[9];  // controller state (PID types)
+  if (!act_is_pid(ACT)) {
+    // _preprocessAction: rpm = HOVER_RPM*(1+0.05*a)  (BaseRLAviary.py:191-192, :224-225)
 #pragma unroll
-  for (int k = 0; k < 4; ++k) rpm[k] = (R)action_to_rpm(c.hover_f32, a[A == 4 ? k : 0]);
+    for (int k = 0; k < 4; ++k) rpm[k] = (R)action_to_rpm(c.hover_f32, a[A == 4 ? k : 0]);
+  } else {
+    // PID / VEL / ONE_D_PID (BaseRLAviary.py:193-235): DSLPIDControl on the state vector of
+    // the last readback (_getDroneStateVector :559-561)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) cs[k] = v.ctrl[k * v.npad + nn];
+    R qn[4], Rm[9], rpy[3];
+    readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
+    quat_to_euler(qn, rpy[0], rpy[1], rpy[2]);
+    const R pos[3] = {s.px, s.py, s.pz}, vel[3] = {s.vx, s.vy, s.vz};
+    R tpos[3], tvel[3], tyaw;
+    pid_targets<R, ACT>(c.pid, a, pos, rpy, tpos, tyaw, tvel);
+    dsl_pid(c.pid, pos, Rm, rpy, vel, tpos, tyaw, tvel, cs, rpm);
+  }
 
   const int nh = v.ring_len - 1;
   const long long slot_stride = v.npad * A;
@@ -194,10 +216,14 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
       int slot = head + 1 + k;
       slot -= slot >= v.ring_len ? v.ring_len : 0;
       const float* src = v.ring + (long long)slot * slot_stride + nn * A;
-      if (A == 4)
+      if (A == 4) {
         __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tile4 + (3 + k) * kPad), 16, 0, 0);
-      else
-        __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tilef + (12 + k) * kPad), 4, 0, 0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < A; ++j)
+          __builtin_amdgcn_global_load_lds((gbl_void_ptr)(src + j), (lds_void_ptr)(tilef + (12 + k * A + j) * kPad), 4,
+                                           0, 0);
+      }
     }
   };
   // substeps 1..nsub-1 skip the (write-only) world ang_v; the last one produces it
@@ -268,7 +294,9 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
   if (active) {
     float* ring_cur = v.ring + (long long)head * slot_stride + n * A;
     if (A == 4) *reinterpret_cast<float4*>(ring_cur) = make_float4(a[0], a[1], a[2], a[3]);
-    else ring_cur[0] = a[0];
+    else
+#pragma unroll
+      for (int j = 0; j < A; ++j) ring_cur[j] = a[j];
   }
 
   float row12[12] = {(float)s.px, (float)s.py, (float)s.pz, roll, pitch, yaw,
@@ -277,7 +305,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // history DMA has landed in the tile
   GPD_STAMP(4);
 
-  const int NC = A == 4 ? 3 + v.ring_len : 12 + v.ring_len;  // tile columns (float4 / float)
+  const int NC = A == 4 ? 3 + v.ring_len : 12 + v.ring_len * A;  // tile columns (float4 / float)
   if (do_reset) {
     // the terminal row's state part goes to the tile's extra columns (the history and action
     // columns are shared with the reset row); the env goes back to INIT_XYZS / INIT_RPYS
@@ -316,7 +344,8 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
   } else {
 #pragma unroll
     for (int k = 0; k < 12; ++k) tilef[k * kPad + tid] = row12[k];
-    tilef[(12 + nh) * kPad + tid] = a[0];
+#pragma unroll
+    for (int j = 0; j < A; ++j) tilef[(12 + nh * A + j) * kPad + tid] = a[j];
   }
   __syncthreads();
   GPD_STAMP(6);
@@ -390,6 +419,10 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
   GPD_STAMP(7);
   if (!active) return;
   store_drone(v, n, s, last);
+  if (act_is_pid(ACT)) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) v.ctrl[k * v.npad + n] = cs[k];
+  }
   if (d == 0) {
     io.reward[e] = reward;
     io.term[e] = term ? 1 : 0;
@@ -509,6 +542,22 @@ __global__ __launch_bounds__(256) void set_raw_kernel(SimView<R> v, const R* __r
   if (n >= v.N) return;
   const long long p = v.npad;
   for (int k = 0; k < 20; ++k) v.state[k * p + n] = in[n * 20 + k];
+}
+
+// [comps][npad] SoA <-> [N][comps] rows (controller state access)
+template <typename R>
+__global__ __launch_bounds__(256) void soa_to_rows_kernel(const R* __restrict__ soa, long long npad, int comps, int N,
+                                                          R* __restrict__ out) {
+  const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  for (int k = 0; k < comps; ++k) out[n * comps + k] = soa[k * npad + n];
+}
+template <typename R>
+__global__ __launch_bounds__(256) void rows_to_soa_kernel(const R* __restrict__ in, long long npad, int comps, int N,
+                                                          R* __restrict__ soa) {
+  const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  for (int k = 0; k < comps; ++k) soa[k * npad + n] = in[n * comps + k];
 }
 
 }  // namespace gpd

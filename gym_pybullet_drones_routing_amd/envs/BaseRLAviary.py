@@ -8,7 +8,7 @@ truncated, info)``, ``action_space`` / ``observation_space``, the 20-float
 one ``BatchedAviarySim`` with ``n_envs=1`` and no auto-reset; every step is one HIP launch
 followed by a device->host copy of the observation.
 
-Not on this path (raise): GUI, video recording, RGB observations, PID/VEL action types.
+Not on this path (raise): GUI, video recording, RGB observations.
 """
 import numpy as np
 import torch
@@ -65,6 +65,8 @@ class BaseRLAviary:
         self.DW_COEFF_1, self.DW_COEFF_2, self.DW_COEFF_3 = p.dw_coeff_1, p.dw_coeff_2, p.dw_coeff_3
         self.COLLISION_H, self.COLLISION_R, self.COLLISION_Z_OFFSET = p.collision_h, p.collision_r, p.collision_z_offset
         self.MAX_SPEED_KMH = p.max_speed_kmh
+        if self.ACT_TYPE == ActionType.VEL:                                   # BaseRLAviary.py:94-95
+            self.SPEED_LIMIT = 0.03 * self.MAX_SPEED_KMH * (1000 / 3600)
         if initial_xyzs is None:
             self.INIT_XYZS = np.array([[i * 4 * self.L, i * 4 * self.L, self.COLLISION_H / 2 - self.COLLISION_Z_OFFSET + .1]
                                        for i in range(self.NUM_DRONES)])
@@ -117,6 +119,10 @@ class BaseRLAviary:
         action = np.asarray(action)
         return np.where(action <= 0, (action + 1) * self.HOVER_RPM,
                         self.HOVER_RPM + (self.MAX_RPM - self.HOVER_RPM) * action)
+
+    def setPIDCoefficients(self, **coeffs):
+        """BaseControl.setPIDCoefficients on every drone's DSLPIDControl (PID action types)."""
+        self.sim.set_pid_coefficients(**coeffs)
 
     def getDroneIds(self):
         return np.arange(self.NUM_DRONES)

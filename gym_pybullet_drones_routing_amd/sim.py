@@ -15,6 +15,10 @@ from . import _lib
 from .assets import default_params, model_id, parse_urdf
 from .enums import ActionType, DroneModel, Physics
 
+_ACTS = {ActionType.RPM: _lib.GPD_ACT_RPM, ActionType.ONE_D_RPM: _lib.GPD_ACT_ONE_D_RPM,
+         ActionType.PID: _lib.GPD_ACT_PID, ActionType.VEL: _lib.GPD_ACT_VEL,
+         ActionType.ONE_D_PID: _lib.GPD_ACT_ONE_D_PID}
+PID_ACTS = (ActionType.PID, ActionType.VEL, ActionType.ONE_D_PID)
 _TASKS = {"none": _lib.GPD_TASK_NONE, "hover": _lib.GPD_TASK_HOVER, "multihover": _lib.GPD_TASK_MULTIHOVER}
 _AERO = {"gnd": _lib.GPD_F_GND, "drag": _lib.GPD_F_DRAG, "dw": _lib.GPD_F_DW, "geom": _lib.GPD_F_GEOM_WRENCH}
 _PHYSICS = {
@@ -72,8 +76,6 @@ class BatchedAviarySim:
             raise _lib.GpdLibraryError("BatchedAviarySim needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
         act = ActionType(act)
-        if act not in (ActionType.RPM, ActionType.ONE_D_RPM):
-            raise NotImplementedError(f"{act} needs the PID controller (SURVEY §8 f2), not on this path")
         if precision not in ("f32", "f64"):
             raise ValueError("precision must be 'f32' or 'f64'")
         self.drone_model = DroneModel(drone_model)
@@ -89,7 +91,7 @@ class BatchedAviarySim:
         cfg.drones_per_env = self.drones_per_env
         cfg.pyb_freq = int(pyb_freq)
         cfg.ctrl_freq = int(ctrl_freq)
-        cfg.act_type = _lib.GPD_ACT_RPM if act == ActionType.RPM else _lib.GPD_ACT_ONE_D_RPM
+        cfg.act_type = _ACTS[act]
         cfg.task = _TASKS[task]
         cfg.physics_flags = physics_flags(physics, aero)
         cfg.precision = _lib.GPD_F32 if precision == "f32" else _lib.GPD_F64
@@ -215,6 +217,34 @@ class BatchedAviarySim:
         assert r.numel() == self.n_drones * 20
         with torch.cuda.device(self.device):
             self._call("gpd_set_raw_state", _ptr(r), _stream(self.device))
+
+    # ------------------------------------------------------------------ DSLPIDControl (PID types)
+    def ctrl_state(self):
+        """Per-drone controller state [N, 9]: integral_pos_e, integral_rpy_e, last_rpy
+        (DSLPIDControl.py:65-78); only for the PID / VEL / ONE_D_PID action types."""
+        out = torch.empty((self.n_drones, _lib.CTRL_COMPS), dtype=self.real_dtype, device=self.device)
+        with torch.cuda.device(self.device):
+            self._call("gpd_get_ctrl_state", _ptr(out), _stream(self.device))
+        return out
+
+    def set_ctrl_state(self, cs):
+        t = torch.as_tensor(cs, dtype=self.real_dtype, device=self.device).contiguous()
+        assert t.numel() == self.n_drones * _lib.CTRL_COMPS
+        with torch.cuda.device(self.device):
+            self._call("gpd_set_ctrl_state", _ptr(t), _stream(self.device))
+
+    def set_pid_coefficients(self, p_coeff_pos=None, i_coeff_pos=None, d_coeff_pos=None,
+                             p_coeff_att=None, i_coeff_att=None, d_coeff_att=None):
+        """BaseControl.setPIDCoefficients (control/BaseControl.py:138-177) for every drone."""
+        q = getattr(self, "_pid", None) or _lib.default_pid_params()
+        for name, val in (("p_coeff_for", p_coeff_pos), ("i_coeff_for", i_coeff_pos), ("d_coeff_for", d_coeff_pos),
+                          ("p_coeff_tor", p_coeff_att), ("i_coeff_tor", i_coeff_att), ("d_coeff_tor", d_coeff_att)):
+            if val is not None:
+                v = np.asarray(val, dtype=np.float64).reshape(3)
+                getattr(q, name)[:] = v.tolist()
+        with torch.cuda.device(self.device):
+            _lib.check("gpd_set_pid_params", self._lib.gpd_set_pid_params(self._h, ctypes.byref(q)))
+        self._pid = q
 
     def step_counters(self):
         out = torch.empty((self.n_envs,), dtype=torch.int32, device=self.device)

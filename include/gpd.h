@@ -13,7 +13,8 @@
  *                        (+ _housekeeping :451-505, readback :509-519, _computeObs
  *                           envs/BaseRLAviary.py:284-319)
  *   gpd_step          <- BaseAviary.step()              envs/BaseAviary.py:259-383, i.e.
- *                        _preprocessAction (BaseRLAviary.py:160-239, RPM / ONE_D_RPM),
+ *                        _preprocessAction (BaseRLAviary.py:160-239; the PID types run
+ *                        DSLPIDControl, control/DSLPIDControl.py:82-259),
  *                        PYB_STEPS_PER_CTRL x (_updateAndStoreKinematicInformation :509-519
  *                        + _dynamics :815-874 + _integrateQ :876-889
  *                        [+ _groundEffect :715-750, _drag :754-781, _downwash :785-811]),
@@ -23,6 +24,9 @@
  *   gpd_integrate     <- the raw _dynamics + readback substep (:815-889, :509-519) driven by
  *                        explicit per-substep RPMs (parity / raw-integrator mode).
  *   gpd_get_state20   <- BaseAviary._getDroneStateVector()  envs/BaseAviary.py:541-561
+ *   gpd_set_pid_params <- BaseControl.setPIDCoefficients()   control/BaseControl.py:138-177
+ *   gpd_get/set_ctrl_state <- the per-drone DSLPIDControl attributes integral_pos_e,
+ *                        integral_rpy_e, last_rpy (control/DSLPIDControl.py:65-78)
  *
  * Conventions
  *   - All array arguments are DEVICE pointers (hipMalloc'd memory, e.g. a torch tensor's
@@ -46,23 +50,26 @@
 extern "C" {
 #endif
 
-#define GPD_ABI_VERSION 1
+#define GPD_ABI_VERSION 2
 
 /* return codes */
 #define GPD_OK 0
 #define GPD_EINVAL (-1)       /* invalid argument / configuration (BaseAviary.py:79-80 ValueError) */
 #define GPD_EHIP (-2)         /* HIP runtime error */
 #define GPD_ENOMEM (-3)       /* device allocation failed */
-#define GPD_EUNSUPPORTED (-4) /* valid in the reference, not on this path (e.g. PID actions) */
+#define GPD_EUNSUPPORTED (-4) /* valid in the reference, not on this path (e.g. RGB obs) */
 
 /* DroneModel (utils/enums.py:3-8) */
 #define GPD_MODEL_CF2X 0
 #define GPD_MODEL_CF2P 1
 #define GPD_MODEL_RACE 2
 
-/* ActionType subset on this path (utils/enums.py:35-41; BaseRLAviary.py:191-192, 224-225) */
-#define GPD_ACT_RPM 0
-#define GPD_ACT_ONE_D_RPM 1
+/* ActionType (utils/enums.py:35-41; BaseRLAviary._preprocessAction :160-239) */
+#define GPD_ACT_RPM 0         /* width 4: rpm = HOVER_RPM*(1+0.05a)                 :191-192 */
+#define GPD_ACT_ONE_D_RPM 1   /* width 1: same, repeated on the 4 motors            :224-225 */
+#define GPD_ACT_PID 2         /* width 3: DSLPIDControl to _calculateNextStep(pos, a, 1) :193-207 */
+#define GPD_ACT_VEL 3         /* width 4: DSLPIDControl to velocity SPEED_LIMIT*|a3|*a/|a| :208-223 */
+#define GPD_ACT_ONE_D_PID 4   /* width 1: DSLPIDControl to pos + (0,0,0.1a)         :226-235 */
 
 /* Task hooks (reward / terminated / truncated) */
 #define GPD_TASK_NONE 0       /* raw aviary: reward -1, never done (CtrlAviary-like) */
@@ -114,6 +121,17 @@ typedef struct gpd_constants {
   int trunc_step_counter;    /* smallest step_counter with step_counter/PYB_FREQ > EPISODE_LEN_SEC */
 } gpd_constants;
 
+/* DSLPIDControl coefficients and constants (control/DSLPIDControl.py:37-60; GRAVITY and KF
+ * from the cf2x URDF, BaseControl.py:35-39 - BaseRLAviary builds the CF2X controller for cf2x
+ * and cf2p drones alike, envs/BaseRLAviary.py:75-76). */
+typedef struct gpd_pid_params {
+  double p_coeff_for[3], i_coeff_for[3], d_coeff_for[3];
+  double p_coeff_tor[3], i_coeff_tor[3], d_coeff_tor[3];
+  double pwm2rpm_scale, pwm2rpm_const, min_pwm, max_pwm;
+  double mixer[4][3];
+  double gravity, kf;
+} gpd_pid_params;
+
 typedef struct gpd_sim gpd_sim;
 
 int gpd_abi_version(void);
@@ -121,6 +139,9 @@ const char* gpd_last_error(void);
 
 /* Fill `out` with the built-in parameters of a drone model (cf2x/cf2p/racer URDF values). */
 int gpd_default_params(int model, gpd_drone_params* out);
+
+/* The DSLPIDControl(DroneModel.CF2X) defaults. */
+int gpd_default_pid_params(gpd_pid_params* out);
 
 /* Create a batched aviary on the CURRENT HIP device; state is initialised as after reset()
  * and the action ring (15 = ctrl_freq//2 slots) is zero, as BaseRLAviary._actionSpace leaves it. */
@@ -154,11 +175,19 @@ int gpd_get_state20(gpd_sim* sim, void* out, void* stream);
  * seed arbitrary initial conditions. */
 int gpd_get_raw_state(gpd_sim* sim, void* out, void* stream);
 int gpd_set_raw_state(gpd_sim* sim, const void* in, void* stream);
+/* PID action types: replace the controller coefficients of every drone (setPIDCoefficients).
+ * Synchronous (uploads the constant block). */
+int gpd_set_pid_params(gpd_sim* sim, const gpd_pid_params* params);
+/* PID action types: per-drone controller state [N][9] real = integral_pos_e(3)
+ * integral_rpy_e(3) last_rpy(3).  Zero at create; NOT cleared by gpd_reset (the reference
+ * never resets its controllers after construction). */
+int gpd_get_ctrl_state(gpd_sim* sim, void* out, void* stream);
+int gpd_set_ctrl_state(gpd_sim* sim, const void* in, void* stream);
 /* step counters [E] int32 */
 int gpd_get_step_counters(gpd_sim* sim, int32_t* out, void* stream);
 int gpd_set_step_counters(gpd_sim* sim, const int32_t* in, void* stream);
 
-/* Whole-sim checkpoint (state, action ring, ring head, step counters) to/from host memory.
+/* Whole-sim checkpoint (state, controller state, action ring, ring head, step counters) to/from host memory.
  * gpd_state_bytes gives the blob size.  These synchronise `stream`. */
 size_t gpd_state_bytes(const gpd_sim* sim);
 int gpd_save_state(gpd_sim* sim, void* blob_host, void* stream);

@@ -52,8 +52,10 @@ import numpy as np
 
 from .bullet_math import euler_from_quat, quat_from_euler, quat_roundtrip, quat_to_mat
 from .params import derived
+from .ref_pid import RefDSLPID, pid_action_rpm
 
-ACT_WIDTH = {"rpm": 4, "one_d_rpm": 1}
+ACT_WIDTH = {"rpm": 4, "one_d_rpm": 1, "pid": 3, "vel": 4, "one_d_pid": 1}   # BaseRLAviary.py:141-147
+PID_ACTS = ("pid", "vel", "one_d_pid")
 
 
 def rpm_from_action(hover_rpm, a):
@@ -94,6 +96,12 @@ class RefAviary:
         self.WRENCH = wrench
         self.ACT = act
         self.A = ACT_WIDTH[act]
+        if act in PID_ACTS:                     # BaseRLAviary.py:73-78, 93-95
+            if model not in ("cf2x", "cf2p"):
+                raise NotImplementedError("no controller is available for the specified drone_model")
+            self.ctrl = [RefDSLPID() for _ in range(num_drones)]
+            self.CTRL_TIMESTEP = 1. / ctrl_freq
+            self.SPEED_LIMIT = 0.03 * p["max_speed_kmh"] * (1000 / 3600)
         self.TASK = task
         self.EPISODE_LEN_SEC = episode_len_sec
         # BaseAviary.py:194-207
@@ -256,8 +264,11 @@ class RefAviary:
             target = action[k, :]
             if self.ACT == "rpm":
                 rpm[k, :] = rpm_from_action(self.HOVER_RPM, target)
-            else:
+            elif self.ACT == "one_d_rpm":
                 rpm[k, :] = np.repeat(rpm_from_action(self.HOVER_RPM, target), 4)
+            else:
+                rpm[k, :] = pid_action_rpm(self.ACT, self.ctrl[k], self._getDroneStateVector(k), target,
+                                           self.CTRL_TIMESTEP, self.SPEED_LIMIT)
         return rpm
 
     def _computeObs(self):
@@ -341,6 +352,15 @@ class RefAviary:
         return np.array(out) if record else None
 
     # ------------------------------------------------------------------ test seeding
+    def ctrl_state(self):
+        """[N, 9] controller state (integral_pos_e, integral_rpy_e, last_rpy) per drone."""
+        return np.array([c.get_state() for c in self.ctrl])
+
+    def set_ctrl_state(self, v):
+        v = np.asarray(v, dtype=np.float64).reshape(self.NUM_DRONES, 9)
+        for c, row in zip(self.ctrl, v):
+            c.set_state(row)
+
     def set_raw_state(self, raw):
         """Seed the physics-client state from a raw [N, 20] array laid out as gpd_get_raw_state:
         pos(3) quat_as_stored(4) vel(3) rpy_rates(3) ang_v(3) last_clipped_action(4)."""

@@ -34,10 +34,14 @@ def run_integrate(rpms, raw0=None, **kw):
     return env.integrate(rpms)
 
 
-def run_vec(actions, n_envs, drones_per_env=1, act="rpm", task="hover", **kw):
+def run_vec(actions, n_envs, drones_per_env=1, act="rpm", task="hover", envs=None, **kw):
     """actions [T, E, D, A] float32 -> obs [T, E, D, W], reward [T, E], term/trunc [T, E],
-    terminal obs dict {(t, e): [D, W]}."""
-    envs = [RefAviary(num_drones=drones_per_env, act=act, task=task, **kw) for _ in range(n_envs)]
+    terminal obs dict {(t, e): [D, W]}.  Pass a list as ``envs`` to get the RefAviary objects
+    back (or to continue from existing ones)."""
+    if envs is None:
+        envs = []
+    if not envs:
+        envs.extend(RefAviary(num_drones=drones_per_env, act=act, task=task, **kw) for _ in range(n_envs))
     T = actions.shape[0]
     obs_l, rew, te, tr, term_obs = [], np.zeros((T, n_envs)), np.zeros((T, n_envs), bool), np.zeros((T, n_envs), bool), {}
     for t in range(T):

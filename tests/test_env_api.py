@@ -61,8 +61,10 @@ def test_unsupported_options_raise():
     with pytest.raises(ValueError):
         HoverAviary(pyb_freq=240, ctrl_freq=7)
     if torch.cuda.is_available():
-        with pytest.raises(NotImplementedError):
-            HoverAviary(act=ActionType.PID)
+        from gym_pybullet_drones_routing_amd import _lib
+        from gym_pybullet_drones_routing_amd.enums import DroneModel
+        with pytest.raises(_lib.GpdError, match="no controller"):   # BaseRLAviary.py:75-78
+            HoverAviary(act=ActionType.PID, drone_model=DroneModel.RACE)
 
 
 # ------------------------------------------------------------------------------------ GPU
