@@ -1,0 +1,203 @@
+"""examples/learn.py on the MI355X path: PPO on thousands of batched HoverAviary /
+MultiHoverAviary envs, everything resident in HBM.
+
+The reference (``gym_pybullet_drones/examples/learn.py:52-103``) trains stable-baselines3 PPO
+('MlpPolicy') on ``make_vec_env(HoverAviary, env_kwargs=dict(obs=KIN, act=ONE_D_RPM), n_envs=1)``
+and stops at an evaluation return of 474.15 (single agent) / 949.5 (two agents).  SB3 is not
+installed in this image, so this script carries a compact PPO with SB3's defaults (separate
+64-64 tanh actor and critic, state-independent log-std, GAE(0.99, 0.95), clip 0.2, 10 epochs,
+advantage normalisation, TimeLimit bootstrapping from ``terminal_observation``) over the same
+env surface: ``make_vec_env(..., output="torch")`` returns observations, rewards and done
+masks as device tensors, so the whole loop (policy, env step, GAE, update) stays on the GPU.
+
+    python examples/learn.py                     # HoverAviary, 4096 envs, ONE_D_RPM
+    python examples/learn.py --multiagent true   # MultiHoverAviary, 2 drones
+
+Evaluation follows the reference's EvalCallback(deterministic=True): the mean action of the
+policy on a fresh single env, the return of one full episode.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gym_pybullet_drones_routing_amd.enums import ActionType, ObservationType, Physics  # noqa: E402
+from gym_pybullet_drones_routing_amd.envs import HoverAviary, MultiHoverAviary, make_vec_env  # noqa: E402
+from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim  # noqa: E402
+
+DEFAULT_OBS = ObservationType('kin')
+DEFAULT_ACT = ActionType('one_d_rpm')
+DEFAULT_AGENTS = 2
+
+
+def mlp(n_in, n_out, out_gain):
+    layers = [nn.Linear(n_in, 64), nn.Tanh(), nn.Linear(64, 64), nn.Tanh(), nn.Linear(64, n_out)]
+    for i, l in enumerate(m for m in layers if isinstance(m, nn.Linear)):
+        nn.init.orthogonal_(l.weight, gain=out_gain if i == 2 else math.sqrt(2))
+        nn.init.zeros_(l.bias)
+    return nn.Sequential(*layers)
+
+
+class ActorCritic(nn.Module):
+    """SB3 MlpPolicy for a Box action space: separate pi / vf networks [64, 64] tanh."""
+
+    def __init__(self, n_obs, n_act):
+        super().__init__()
+        self.pi = mlp(n_obs, n_act, 0.01)
+        self.vf = mlp(n_obs, 1, 1.0)
+        self.log_std = nn.Parameter(torch.zeros(n_act))
+
+    def dist(self, obs):
+        return torch.distributions.Normal(self.pi(obs), self.log_std.exp())
+
+    def value(self, obs):
+        return self.vf(obs).squeeze(-1)
+
+
+def evaluate(policy, multiagent, device, act):
+    """EvalCallback(deterministic=True, n_eval_episodes=1): one episode of a fresh env."""
+    D = DEFAULT_AGENTS if multiagent else 1
+    sim = BatchedAviarySim(n_envs=1, drones_per_env=D, task="multihover" if multiagent else "hover",
+                           act=act, physics=Physics.DYN, autoreset=False, device=device)
+    obs = sim.reset().clone()
+    ret, steps = 0.0, 0
+    with torch.no_grad():
+        while True:
+            a = policy.pi(obs.reshape(1, -1)).clamp(-1, 1).reshape(1, D, -1).contiguous()
+            o, r, te, tr = sim.step(a, terminal_obs=False)
+            ret += float(r[0])
+            steps += 1
+            if bool(te[0]) or bool(tr[0]):
+                break
+            obs = o.clone()
+    sim.close()
+    return ret, steps
+
+
+def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), lr=3e-4, epochs=10,
+          minibatch=16384, gamma=0.99, gae_lambda=0.95, clip=0.2, vf_coef=0.5, max_grad_norm=0.5,
+          eval_every=2, seed=0, device="cuda:0", act=DEFAULT_ACT, target_reward=None, max_seconds=None,
+          log=print):
+    torch.manual_seed(seed)
+    env_cls = MultiHoverAviary if multiagent else HoverAviary
+    kw = dict(obs=DEFAULT_OBS, act=act)
+    if multiagent:
+        kw["num_drones"] = DEFAULT_AGENTS
+    env = make_vec_env(env_cls, env_kwargs=kw, n_envs=n_envs, seed=seed, output="torch", device=device)
+    if target_reward is None:   # learn.py:80-83
+        if act == ActionType.ONE_D_RPM:
+            target_reward = 474.15 if not multiagent else 949.5
+        else:
+            target_reward = 467. if not multiagent else 920.
+    log(f"[INFO] Action space: {env.action_space}")
+    log(f"[INFO] Observation space: {env.observation_space}")
+    D, A = env.num_drones, env.sim.act_width
+    n_obs, n_act = D * env.sim.obs_width, D * A
+    policy = ActorCritic(n_obs, n_act).to(device)
+    opt = torch.optim.Adam(policy.parameters(), lr=lr, eps=1e-5)
+    E = n_envs
+    buf_obs = torch.zeros((n_steps, E, n_obs), device=device)
+    buf_act = torch.zeros((n_steps, E, n_act), device=device)
+    buf_logp = torch.zeros((n_steps, E), device=device)
+    buf_val = torch.zeros((n_steps, E), device=device)
+    buf_rew = torch.zeros((n_steps, E), device=device)
+    buf_done = torch.zeros((n_steps, E), device=device)
+    obs = env.reset().reshape(E, -1)
+    history = []
+    t0 = time.time()
+    timesteps, it = 0, 0
+    best = -1e9
+    while timesteps < total_timesteps:
+        t_roll = time.time()
+        with torch.no_grad():
+            for t in range(n_steps):
+                d = policy.dist(obs)
+                a = d.sample()
+                v = policy.value(obs)
+                o2, r, done, info = env.step(a.clamp(-1, 1))            # SB3 clips to the Box
+                o2 = o2.reshape(E, -1)
+                trunc = info["TimeLimit.truncated"]
+                if bool(trunc.any()):                                 # bootstrap time limits
+                    tv = policy.value(info["terminal_observation"].reshape(E, -1))
+                    r = r + gamma * tv * trunc.float()
+                buf_obs[t], buf_act[t], buf_logp[t], buf_val[t] = obs, a, d.log_prob(a).sum(-1), v
+                buf_rew[t], buf_done[t] = r, done.float()
+                obs = o2
+            last_v = policy.value(obs)
+            adv = torch.zeros_like(buf_rew)
+            g = torch.zeros(E, device=device)
+            for t in reversed(range(n_steps)):
+                nv = last_v if t == n_steps - 1 else buf_val[t + 1]
+                nonterm = 1.0 - buf_done[t]
+                delta = buf_rew[t] + gamma * nv * nonterm - buf_val[t]
+                g = delta + gamma * gae_lambda * nonterm * g
+                adv[t] = g
+            ret = adv + buf_val
+        t_upd = time.time()
+        N = n_steps * E
+        b_obs, b_act, b_logp = buf_obs.reshape(N, -1), buf_act.reshape(N, -1), buf_logp.reshape(N)
+        b_adv, b_ret, b_val = adv.reshape(N), ret.reshape(N), buf_val.reshape(N)
+        for _ in range(epochs):
+            perm = torch.randperm(N, device=device)
+            for s in range(0, N, minibatch):
+                idx = perm[s:s + minibatch]
+                d = policy.dist(b_obs[idx])
+                logp = d.log_prob(b_act[idx]).sum(-1)
+                ratio = (logp - b_logp[idx]).exp()
+                ma = b_adv[idx]
+                ma = (ma - ma.mean()) / (ma.std() + 1e-8)
+                pg = -torch.min(ratio * ma, ratio.clamp(1 - clip, 1 + clip) * ma).mean()
+                vl = ((policy.value(b_obs[idx]) - b_ret[idx]) ** 2).mean()
+                loss = pg + vf_coef * vl
+                opt.zero_grad(set_to_none=True)
+                loss.backward()
+                nn.utils.clip_grad_norm_(policy.parameters(), max_grad_norm)
+                opt.step()
+        timesteps += N
+        it += 1
+        rec = {"iter": it, "timesteps": timesteps, "mean_step_reward": float(buf_rew.mean()),
+               "rollout_s": round(t_upd - t_roll, 3), "update_s": round(time.time() - t_upd, 3),
+               "wall_s": round(time.time() - t0, 1)}
+        if it % eval_every == 0:
+            er, el = evaluate(policy, multiagent, device, act)
+            rec.update(eval_return=er, eval_len=el)
+            best = max(best, er)
+        history.append(rec)
+        log(json.dumps(rec))
+        if rec.get("eval_return", -1e9) >= target_reward:
+            log(f"[INFO] reward threshold {target_reward} reached after {timesteps} timesteps")
+            break
+        if max_seconds and time.time() - t0 > max_seconds:
+            break
+    env.close()
+    return policy, history, best, target_reward
+
+
+def main():
+    p = argparse.ArgumentParser(description="PPO on batched HoverAviary / MultiHoverAviary (MI355X)")
+    p.add_argument("--multiagent", default="false")
+    p.add_argument("--n_envs", type=int, default=4096)
+    p.add_argument("--total_timesteps", type=float, default=2e8)
+    p.add_argument("--max_seconds", type=float, default=None)
+    p.add_argument("--output", default=None, help="JSON file for the training history")
+    a = p.parse_args()
+    multi = str(a.multiagent).lower() in ("1", "true", "yes")
+    policy, hist, best, target = train(multiagent=multi, n_envs=a.n_envs, total_timesteps=int(a.total_timesteps),
+                                       max_seconds=a.max_seconds)
+    out = {"multiagent": multi, "n_envs": a.n_envs, "target_reward": target, "best_eval_return": best,
+           "reached": best >= target, "history": hist}
+    print(json.dumps({k: v for k, v in out.items() if k != "history"}))
+    if a.output:
+        with open(a.output, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -316,13 +316,14 @@ __device__ __forceinline__ float action_to_rpm(float hover_f32, float a) {
   return hover_f32 * u;
 }
 
-// Thrust and body torques (BaseAviary.py:838-851, + _groundEffect :732-750).  Evaluated with FP
-// contraction OFF, like numpy: with contraction hipcc fuses r^2*kf into the following add, so
-// four equal RPMs (every ONE_D_RPM action, the hover equilibrium) would leave a residual
-// roll/pitch torque instead of the reference's exact zero.
+// Thrust and body torques of the propellers (BaseAviary.py:838-851).  They depend on the RPMs
+// only, so the step kernel evaluates them once per control step, outside the substep loop.
+// Evaluated with FP contraction OFF, like numpy: with contraction hipcc fuses r^2*kf into the
+// following add, so four equal RPMs (every ONE_D_RPM action, the hover equilibrium) would leave
+// a residual roll/pitch torque instead of the reference's exact zero.
+// W = {fz, tx, ty, tz} in the body frame.
 template <typename R, bool FAST>
-__device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bool gnd_upright, const R rpm[4],
-                                            const Consts<R>& c, R& fz_out, R& tx_out, R& ty_out, R& tz_out) {
+__device__ __forceinline__ void rpm_wrench(const R rpm[4], const Consts<R>& c, R W[4]) {
 #pragma clang fp contract(off)
   R f[4], zt[4];
 #pragma unroll
@@ -335,22 +336,32 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
 #pragma unroll
     for (int k = 0; k < 4; ++k) zt[k] = -zt[k];        // :843-844
   }
-  R fz = ((f[0] + f[1]) + f[2]) + f[3];                // np.sum(forces) :839
-  const R tz = ((-zt[0] + zt[1]) - zt[2]) + zt[3];     // :845
-  R tx, ty;
+  W[0] = ((f[0] + f[1]) + f[2]) + f[3];                // np.sum(forces) :839
+  W[3] = ((-zt[0] + zt[1]) - zt[2]) + zt[3];           // :845
   if (!FAST && (c.flags & F_GEOM)) {                   // _physics: forces at prop links :698-705
-    tx = R(0); ty = R(0);
+    R tx = R(0), ty = R(0);
 #pragma unroll
     for (int k = 0; k < 4; ++k) { tx = tx + c.ry[k] * f[k]; ty = ty - c.rx[k] * f[k]; }
+    W[1] = tx; W[2] = ty;
   } else if (c.model == MODEL_CF2P) {                  // :849-851
-    tx = (f[1] - f[3]) * c.L;
-    ty = (-f[0] + f[2]) * c.L;
+    W[1] = (f[1] - f[3]) * c.L;
+    W[2] = (-f[0] + f[2]) * c.L;
   } else {                                             // CF2X / RACE :846-848 (roll-sign quirk kept)
-    tx = (((f[0] + f[1]) - f[2]) - f[3]) * c.Ls2;
-    ty = (((-f[0] + f[1]) + f[2]) - f[3]) * c.Ls2;
+    W[1] = (((f[0] + f[1]) - f[2]) - f[3]) * c.Ls2;
+    W[2] = (((-f[0] + f[1]) + f[2]) - f[3]) * c.Ls2;
   }
+}
+
+// Body wrench of one substep: the propeller wrench W plus, with F_GND, the ground effect
+// (_groundEffect :732-750) at the current pose.
+template <typename R, bool FAST>
+__device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bool gnd_upright, const R rpm[4],
+                                            const R W[4], const Consts<R>& c, R& fz_out, R& tx_out, R& ty_out,
+                                            R& tz_out) {
+#pragma clang fp contract(off)
+  R fz = W[0], tx = W[1], ty = W[2];
   if (!FAST && (c.flags & F_GND) && gnd_upright) {
-    // _groundEffect :732-750 — prop COM heights via forward kinematics, clipped, +z link force
+    // prop COM heights via forward kinematics, clipped, +z link force at each prop
     R g[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -369,7 +380,7 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
   fz_out = fz;
   tx_out = tx;
   ty_out = ty;
-  tz_out = tz;
+  tz_out = W[3];
 }
 
 // ---------------------------------------------------------------- one DYN substep
@@ -385,10 +396,10 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
 // last substep of a control step is ever observed, so earlier substeps skip it).
 template <typename R, bool FAST, bool ANGV = true>
 __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R Rm[9], bool gnd_upright,
-                                            const R rpm[4], const R last[4], R dwsum,
+                                            const R rpm[4], const R W[4], const R last[4], R dwsum,
                                             const Consts<R>& c) {
   R fz, tx, ty, tz;
-  body_wrench<R, FAST>(s, Rm, gnd_upright, rpm, c, fz, tx, ty, tz);
+  body_wrench<R, FAST>(s, Rm, gnd_upright, rpm, W, c, fz, tx, ty, tz);
   if (!FAST && (c.flags & F_DW)) fz = fz + dwsum;      // _downwash :801-811 (body z)
   // R·(0,0,fz) - (0,0,GRAVITY) [+ drag]                 :839-841
   R Fx = Rm[2] * fz, Fy = Rm[5] * fz, Fz = Rm[8] * fz;
@@ -418,8 +429,10 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R 
   // _integrateQ(quat, rpy_rates, dt)                  :876-889
   const R p = s.wx, q = s.wy, r = s.wz;
   const R n2 = p * p + q * q + r * r;
-  const R rn = n2 > R(0) ? g_rsqrt(n2) : R(0);        // 1/|omega|
-  const R nrm = n2 * rn;                               // |omega|
+  // 1/|omega| and |omega| = n2/|omega|; for omega = 0 both are NaN (rsq(0) = inf), which
+  // fails the isclose test below exactly like |omega| = 0 does
+  const R rn = g_rsqrt(n2);
+  const R nrm = n2 * rn;
   if (nrm > R(1e-8)) {                                 // np.isclose(norm, 0): |norm| <= 1e-8
     const R th = nrm * c.dt * R(0.5);
     R co, si;

@@ -119,8 +119,8 @@ __device__ __forceinline__ void store_drone(const SimView<R>& v, long long n, co
 // One physics substep of every drone of the block, including the readback that precedes it
 // (BaseAviary.py:343-372 loop body).  MULTI: envs have D > 1 drones and may need downwash.
 template <typename R, bool MULTI, bool FAST, bool ANGV = true>
-__device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const R last[4], const Consts<R>& c,
-                                              R* sx, R* sy, R* sz, int tid, int base, int D) {
+__device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const R W[4], const R last[4],
+                                              const Consts<R>& c, R* sx, R* sy, R* sz, int tid, int base, int D) {
   R qn[4], Rm[9];
   readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);  // :346-347 -> :517, :836
   bool up = true;
@@ -132,7 +132,7 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
     dw = downwash_sum(s.px, s.py, s.pz, sx, sy, sz, base, D, c);
     __syncthreads();
   }
-  dyn_substep<R, FAST, ANGV>(s, qn, Rm, up, rpm, last, dw, c);
+  dyn_substep<R, FAST, ANGV>(s, qn, Rm, up, rpm, W, last, dw, c);
 }
 
 // Bytes of dynamic LDS the step kernel needs for its observation tile: the row's columns
@@ -226,9 +226,12 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
       }
     }
   };
+  // propeller wrench: the same RPMs drive every substep of the control step (:349-367)
+  R W[4];
+  rpm_wrench<R, FAST>(rpm, c, W);
   // substeps 1..nsub-1 skip the (write-only) world ang_v; the last one produces it
   for (int it = 0; it < c.nsub - 1; ++it) {
-    substep_block<R, MULTI, FAST, false>(s, rpm, last, c, sx, sy, sz, tid, base, D);
+    substep_block<R, MULTI, FAST, false>(s, rpm, W, last, c, sx, sy, sz, tid, base, D);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
     if (it == 0) {
@@ -236,7 +239,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
       history_dma();
     }
   }
-  substep_block<R, MULTI, FAST, true>(s, rpm, last, c, sx, sy, sz, tid, base, D);
+  substep_block<R, MULTI, FAST, true>(s, rpm, W, last, c, sx, sy, sz, tid, base, D);
 #pragma unroll
   for (int k = 0; k < 4; ++k) last[k] = rpm[k];
   if (c.nsub == 1) history_dma();
@@ -454,7 +457,9 @@ __global__ __launch_bounds__(kWave) void integrate_kernel(SimView<R> v, const Co
     R rpm[4];
     const R* src = rpm_in + ((long long)t * N + nn) * 4;
     rpm[0] = src[0]; rpm[1] = src[1]; rpm[2] = src[2]; rpm[3] = src[3];
-    substep_block<R, MULTI, false>(s, rpm, last, c, sx, sy, sz, tid, base, D);
+    R W[4];
+    rpm_wrench<R, false>(rpm, c, W);
+    substep_block<R, MULTI, false>(s, rpm, W, last, c, sx, sy, sz, tid, base, D);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];
     if (traj && active) {
