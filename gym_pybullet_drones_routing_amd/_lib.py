@@ -118,10 +118,12 @@ def load():
         "gpd_set_ctrl_state": (ci, [vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
+        if not hasattr(lib, name) and os.environ.get("GPD_ALLOW_ABI_MISMATCH"):
+            continue   # diagnostics against an older build (A/B timing only)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.gpd_abi_version() != GPD_ABI_VERSION:
+    if lib.gpd_abi_version() != GPD_ABI_VERSION and not os.environ.get("GPD_ALLOW_ABI_MISMATCH"):
         raise GpdLibraryError(f"{LIB_PATH} has ABI {lib.gpd_abi_version()}, this binding expects {GPD_ABI_VERSION}: rebuild it")
     _lib = lib
     return lib

@@ -53,6 +53,21 @@ __device__ unsigned long long g_stamps[65536 * kStampPhases];
 #define GPD_STAMP(k) do {} while (0)
 #endif
 
+// Write-through (sc1) stores through a buffer resource.  Every launch ends with a release that
+// writes the XCD L2's dirty lines back; rows stored write-through are already on their way to
+// memory when the wave stores them, so less of that write-back is left for the kernel's end.
+typedef int gpd_v4i __attribute__((ext_vector_type(4)));
+typedef unsigned gpd_v2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, int off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gpd_v4i, v), r, off, 0, 16);
+}
+__device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, int off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 16);
+}
+__device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, int off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(gpd_v2u, v), r, off, 0, 16);
+}
+
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 typedef __attribute__((address_space(1))) void* gbl_void_ptr;
 
@@ -67,6 +82,7 @@ struct SimView {
   long long npad;         // component stride of `state` (elements)
   int N, D, A, W, tpb, ring_len;
   int task, autoreset, trunc_sc;
+  int wt;                 // write-through stores: bit 0 obs/terminal rows, bit 1 state (see store_wt)
   R bound_xy;             // 1.5 (Hover) or 2.0 (MultiHover)
 };
 
@@ -102,6 +118,18 @@ __device__ __forceinline__ void load_drone_full(const SimView<R>& v, long long n
   load_drone(v, n, s, last, true);
   const long long p = v.npad;
   s.ax = v.state[13 * p + n]; s.ay = v.state[14 * p + n]; s.az = v.state[15 * p + n];
+}
+
+template <typename R>
+__device__ __forceinline__ void store_drone_wt(const SimView<R>& v, long long n, const Drone<R>& s, const R last[4]) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(v.state, 0, (int)(kStateComps * v.npad * (long long)sizeof(R)), 0x00020000);
+  const int p = (int)(v.npad * sizeof(R));
+  int o = (int)(n * sizeof(R));
+  const R vals[20] = {s.px, s.py, s.pz, s.qx, s.qy, s.qz, s.qw, s.vx, s.vy, s.vz,
+                      s.wx, s.wy, s.wz, s.ax, s.ay, s.az, last[0], last[1], last[2], last[3]};
+#pragma unroll
+  for (int k = 0; k < 20; ++k, o += p) store_wt(r, o, vals[k]);
 }
 
 template <typename R>
@@ -379,8 +407,14 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
           if (col >= NC) { col -= NC; ++row; }
         }
         float4* dst = reinterpret_cast<float4*>(io.obs) + n0 * NC;
+        if (v.wt & 1) {
+          const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, 0, total * 16, 0x00020000);
 #pragma unroll
-        for (int u = 0; u < U; ++u) dst[idx[u]] = val[u];
+          for (int u = 0; u < U; ++u) store_wt(r, (int)idx[u] * 16, val[u]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u) dst[idx[u]] = val[u];
+        }
         if (done_rows) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
@@ -405,8 +439,14 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
           if (col >= NC) { col -= NC; ++row; }
         }
         float* dst = io.obs + n0 * NC;
+        if (v.wt & 1) {
+          const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, 0, total * 4, 0x00020000);
 #pragma unroll
-        for (int u = 0; u < U; ++u) dst[idx[u]] = val[u];
+          for (int u = 0; u < U; ++u) store_wt(r, (int)idx[u] * 4, val[u]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u) dst[idx[u]] = val[u];
+        }
         if (done_rows) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
@@ -421,7 +461,8 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
   }
   GPD_STAMP(7);
   if (!active) return;
-  store_drone(v, n, s, last);
+  if (v.wt & 2) store_drone_wt(v, n, s, last);
+  else store_drone(v, n, s, last);
   if (act_is_pid(ACT)) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) v.ctrl[k * v.npad + n] = cs[k];
