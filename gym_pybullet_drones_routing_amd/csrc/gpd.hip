@@ -115,6 +115,7 @@ struct gpd_sim {
   void* d_consts = nullptr;       // Consts<real> in device memory
   int tile_bytes = 0;             // dynamic LDS of the step kernel
   int wt = 0;                     // SimView::wt (write-through store policy)
+  int nc_magic = 0;               // SimView::nc_magic
   double bound_xy;
   std::vector<double> init_tmpl;  // [D][10]
   std::vector<double> target;     // [D][3]
@@ -186,6 +187,7 @@ SimView<R> make_view(const gpd_sim* s) {
   v.autoreset = s->cfg.autoreset;
   v.trunc_sc = s->K.trunc_step_counter;
   v.wt = s->wt;
+  v.nc_magic = s->nc_magic;
   v.bound_xy = (R)s->bound_xy;
   return v;
 }
@@ -411,6 +413,16 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   }
   s->bound_xy = C.task == GPD_TASK_MULTIHOVER ? 2.0 : 1.5;
   s->tile_bytes = step_tile_bytes(s->A, s->ring_len);
+  {
+    // division-free row/column split of the copy-out (t / NC for t <= 64)
+    const int NC = s->A == 4 ? 3 + s->ring_len : 12 + s->ring_len * s->A;
+    s->nc_magic = (65536 + NC - 1) / NC;
+    for (int t = 0; t <= kWave; ++t)
+      if ((t * s->nc_magic) >> 16 != t / NC) {
+        delete s;
+        return fail(GPD_EUNSUPPORTED, "gpd_create: observation width not supported by the tile copy-out");
+      }
+  }
   if (s->tile_bytes > 160 * 1024) {
     delete s;
     return fail(GPD_EUNSUPPORTED, "gpd_create: ctrl_freq too high (observation tile exceeds 160 KiB of LDS)");

@@ -39,7 +39,7 @@ enum : int { TASK_NONE = 0, TASK_HOVER = 1, TASK_MULTIHOVER = 2 };
 // shader clock at phase boundaries of step_kernel into g_stamps[block][phase].  The shipped
 // library executes no stamp.
 #ifdef GPD_STAMPS
-constexpr int kStampPhases = 8;
+constexpr int kStampPhases = 10;
 __device__ unsigned long long g_stamps[65536 * kStampPhases];
 #define GPD_STAMP(k)                                                                      \
   do {                                                                                    \
@@ -83,6 +83,7 @@ struct SimView {
   int N, D, A, W, tpb, ring_len;
   int task, autoreset, trunc_sc;
   int wt;                 // write-through stores: bit 0 obs/terminal rows, bit 1 state (see store_wt)
+  int nc_magic;           // floor(t / NC) == (t * nc_magic) >> 16 for 0 <= t < 64 (host-checked)
   R bound_xy;             // 1.5 (Hover) or 2.0 (MultiHover)
 };
 
@@ -321,7 +322,13 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
   const bool done = term || trunc;
   const bool do_reset = done && v.autoreset;
 
-  // current action into the ring (deque.append); the DMA above never reads slot `head`
+  float row12[12] = {(float)s.px, (float)s.py, (float)s.pz, roll, pitch, yaw,
+                     (float)s.vx, (float)s.vy, (float)s.vz, (float)s.ax, (float)s.ay, (float)s.az};
+  GPD_STAMP(3);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // history DMA has landed in the tile
+  GPD_STAMP(4);
+  // current action into the ring (deque.append); issued after the wait above so that the wait
+  // does not also cover this store's write acknowledgement.  The DMA never reads slot `head`.
   if (active) {
     float* ring_cur = v.ring + (long long)head * slot_stride + n * A;
     if (A == 4) *reinterpret_cast<float4*>(ring_cur) = make_float4(a[0], a[1], a[2], a[3]);
@@ -330,11 +337,6 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
       for (int j = 0; j < A; ++j) ring_cur[j] = a[j];
   }
 
-  float row12[12] = {(float)s.px, (float)s.py, (float)s.pz, roll, pitch, yaw,
-                     (float)s.vx, (float)s.vy, (float)s.vz, (float)s.ax, (float)s.ay, (float)s.az};
-  GPD_STAMP(3);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // history DMA has landed in the tile
-  GPD_STAMP(4);
 
   const int NC = A == 4 ? 3 + v.ring_len : 12 + v.ring_len * A;  // tile columns (float4 / float)
   if (do_reset) {
@@ -386,35 +388,38 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
     // end re-stores the last element (same address, same value).  Rows of envs that finished
     // this step are also written to terminal_obs (state columns from the extra tile columns).
     const int total = nact * NC;
-    const int drow = kWave / NC, dcol = kWave - drow * NC;
-    int row = tid / NC, col = tid - (tid / NC) * NC;
+    const int drow = (kWave * v.nc_magic) >> 16, dcol = kWave - drow * NC;
+    int row = (tid * v.nc_magic) >> 16;
+    int col = tid - row * NC;
     constexpr int U = 6;
     const int last_row = nact - 1, last_col = NC - 1;
     const int ncs = A == 4 ? 3 : 12;  // state columns
     for (int g0 = tid; g0 - tid < total; g0 += U * kWave) {
       if (A == 4) {
         float4 val[U];
-        long long idx[U];
+        int idx[U];
         int rr[U], cc[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const bool ok = g0 + u * kWave < total;
           rr[u] = ok ? row : last_row;
           cc[u] = ok ? col : last_col;
-          val[u] = tile4[cc[u] * kPad + rr[u]];
-          idx[u] = ok ? (long long)(g0 + u * kWave) : (long long)(total - 1);
+          val[u] = tile4[__umul24(cc[u], kPad) + rr[u]];   // 24-bit multiply: full-rate VALU
+          idx[u] = ok ? g0 + u * kWave : total - 1;
           col += dcol; row += drow;
           if (col >= NC) { col -= NC; ++row; }
         }
+        GPD_STAMP(8);
         float4* dst = reinterpret_cast<float4*>(io.obs) + n0 * NC;
         if (v.wt & 1) {
           const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, 0, total * 16, 0x00020000);
 #pragma unroll
-          for (int u = 0; u < U; ++u) store_wt(r, (int)idx[u] * 16, val[u]);
+          for (int u = 0; u < U; ++u) store_wt(r, idx[u] * 16, val[u]);
         } else {
 #pragma unroll
           for (int u = 0; u < U; ++u) dst[idx[u]] = val[u];
         }
+        GPD_STAMP(9);
         if (done_rows) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
@@ -426,15 +431,15 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
         }
       } else {
         float val[U];
-        long long idx[U];
+        int idx[U];
         int rr[U], cc[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const bool ok = g0 + u * kWave < total;
           rr[u] = ok ? row : last_row;
           cc[u] = ok ? col : last_col;
-          val[u] = tilef[cc[u] * kPad + rr[u]];
-          idx[u] = ok ? (long long)(g0 + u * kWave) : (long long)(total - 1);
+          val[u] = tilef[__umul24(cc[u], kPad) + rr[u]];
+          idx[u] = ok ? g0 + u * kWave : total - 1;
           col += dcol; row += drow;
           if (col >= NC) { col -= NC; ++row; }
         }
@@ -442,7 +447,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
         if (v.wt & 1) {
           const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, 0, total * 4, 0x00020000);
 #pragma unroll
-          for (int u = 0; u < U; ++u) store_wt(r, (int)idx[u] * 4, val[u]);
+          for (int u = 0; u < U; ++u) store_wt(r, idx[u] * 4, val[u]);
         } else {
 #pragma unroll
           for (int u = 0; u < U; ++u) dst[idx[u]] = val[u];
