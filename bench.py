@@ -181,6 +181,40 @@ def time_steps(sim, pool, steps, warmup):
     return wall, 1000.0 * float(np.mean(kern_ms))
 
 
+def other_configs(device, precision, act):
+    """BASELINE.json configs 3 and 4 and the controller action types, each timed like the main
+    line (hipGraph replays of env.step for every env) - reported beside the metric, not as it."""
+    import math
+    from gym_pybullet_drones_routing_amd.enums import ActionType, Physics
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+    stag = [[0.15 * math.cos(2 * math.pi * i / 8), 0.15 * math.sin(2 * math.pi * i / 8), 0.5 + 0.1 * i] for i in range(8)]
+    cases = [
+        ("config3: 4096 HoverAviary envs, ground effect + drag on the DYN integrator",
+         dict(n_envs=4096, task="hover", act=ActionType(act), physics=Physics.DYN, aero=("gnd", "drag")), 4),
+        ("config4: 512 MultiHoverAviary x 8 drones, downwash (staggered init, SURVEY 8(d))",
+         dict(n_envs=512, drones_per_env=8, task="multihover", act=ActionType.RPM, physics=Physics.DYN, aero=("dw",),
+              initial_xyzs=stag), 4),
+        ("4096 HoverAviary envs, ActionType.ONE_D_PID (batched DSLPIDControl + DYN)",
+         dict(n_envs=4096, task="hover", act=ActionType.ONE_D_PID, physics=Physics.DYN), 1),
+        ("4096 HoverAviary envs, ActionType.PID (waypoint + DSLPIDControl, PYB force placement)",
+         dict(n_envs=4096, task="hover", act=ActionType.PID, physics=Physics.PYB), 3),
+    ]
+    out = []
+    for name, kw, A in cases:
+        sim = BatchedAviarySim(precision=precision, autoreset=True, device=device, **kw)
+        E, D = sim.n_envs, sim.drones_per_env
+        g = torch.Generator(device=device)
+        g.manual_seed(3)
+        pool = (torch.rand((16, E, D, A), generator=g, device=device) * 2 - 1).contiguous()
+        if A == 3:
+            pool *= 0.5
+        w, n, k = time_graph(sim, pool, 64, 16)
+        out.append({"config": name, "n_drones": E * D, "kernel_us": k, "ms_per_step": 1000 * w / n,
+                    "value": E * D * sim.pyb_steps_per_ctrl * n / w, "unit": "drone*dt/s"})
+        sim.close()
+    return out
+
+
 def make_pool(E, A, device, seed, pool=64):
     g = torch.Generator(device=device)
     g.manual_seed(seed)
@@ -255,7 +289,8 @@ def main():
         "ctrl_steps_per_s": world * E * args.steps / wall,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "traffic_unit": "bytes per launch",
-                     "kernel": "gpd::step_kernel<%s,%d,false>" % ("double" if rbytes == 8 else "float", A),
+                     "kernel": "gpd::step_kernel<%s, %d, false, true>" % ("double" if rbytes == 8 else "float",
+                                                                         0 if args.act == "rpm" else 1),
                      "alg_bytes_per_launch": alg},
     }
 
@@ -295,6 +330,12 @@ def main():
             del p2
             torch.cuda.empty_cache()
         result["sweep"] = sweep
+
+    if rank == 0 and world == 1 and not args.no_sweep:
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            result["other_configs"] = other_configs(device, args.precision, args.act)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.act)

@@ -289,3 +289,34 @@ def test_gpu_kat_hover_and_symmetric_thrust(prec):
     for col in (0, 1, 7, 8, 13, 14):   # x, y, roll, pitch, ang_v x, ang_v y
         assert np.abs(traj[..., col]).max() == 0.0, col
     sim.close()
+
+
+@pytest.mark.parametrize("case", ["c3_gnd_drag", "c4_downwash"])
+def test_step_parity_aero_configs(case):
+    """BASELINE configs 3 and 4 through step(): ground effect + drag on single-drone hover envs,
+    and 8-drone MultiHover envs with downwash from a staggered start."""
+    import math
+    from gym_pybullet_drones_routing_amd.enums import ActionType
+    rng = np.random.default_rng(21)
+    if case == "c3_gnd_drag":
+        E, D, T, task, aero, xyz = 16, 1, 60, "hover", ("gnd", "drag"), None
+    else:
+        E, D, T, task, aero = 4, 8, 40, "multihover", ("dw",)
+        xyz = [[0.15 * math.cos(2 * math.pi * i / 8), 0.15 * math.sin(2 * math.pi * i / 8), 0.5 + 0.1 * i]
+               for i in range(8)]
+    acts = np.clip(rng.normal(0, 0.2, (T, E, D, 4)), -1, 1).astype(np.float32)
+    envs = []
+    obs_r, rew_r, te_r, tr_r, _ = run_vec(acts, E, drones_per_env=D, task=task, aero=aero, initial_xyzs=xyz,
+                                          envs=envs)
+    sim = _sim(n_envs=E, drones_per_env=D, task=task, precision="f64", act=ActionType.RPM, aero=aero,
+               initial_xyzs=xyz)
+    for t in range(T):
+        o, r, te, tr = sim.step(torch.from_numpy(acts[t]).cuda())
+        np.testing.assert_array_equal(te.cpu().numpy().astype(bool), te_r[t])
+        np.testing.assert_array_equal(tr.cpu().numpy().astype(bool), tr_r[t])
+        np.testing.assert_allclose(o.cpu().numpy(), obs_r[t], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(r.cpu().numpy(), rew_r[t], rtol=1e-6, atol=1e-5)
+    ref = np.concatenate([e.state20() for e in envs])
+    err = state_rel_err(sim.state20().cpu().numpy(), ref)
+    assert err.max() <= TOL["f64"], err.max()
+    sim.close()
