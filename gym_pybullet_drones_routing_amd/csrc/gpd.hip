@@ -128,6 +128,8 @@ Consts<R> make_consts(const gpd_sim* s) {
   const gpd_drone_params& P = s->P;
   Consts<R> c;
   c.dt = (R)s->K.pyb_timestep;
+  c.hdt = (R)(0.5 * s->K.pyb_timestep);
+  c.hdt2 = (R)((0.5 * s->K.pyb_timestep) * (0.5 * s->K.pyb_timestep));
   c.m = (R)P.m;
   c.gravity = (R)s->K.gravity;
   c.kf = (R)P.kf;

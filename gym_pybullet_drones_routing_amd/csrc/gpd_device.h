@@ -71,6 +71,7 @@ struct PidConsts {
 template <typename R>
 struct Consts {
   R dt;                    // PYB_TIMESTEP = 1./PYB_FREQ              BaseAviary.py:83
+  R hdt, hdt2;             // dt/2 and (dt/2)^2 (_integrateQ half angle, :887)
   R m, gravity;            // M, GRAVITY = G*M                        :97, :117
   R kf, km, L, Ls2;        // KF, KM, L, L/np.sqrt(2)                 :847
   R jx, jy, jz;            // J diagonal                              :996
@@ -88,6 +89,28 @@ struct Consts {
   int model, flags, nsub;
   PidConsts<R> pid;        // PID / VEL / ONE_D_PID action types only
 };
+
+// The constants the substep loop reads every iteration, held in VGPRs: with the 64-bit
+// constants in SGPRs the loop runs out of scalar registers and hipcc re-loads them with
+// s_load + s_waitcnt inside the loop (a scalar-cache round trip per use).
+template <typename R>
+struct DynK {
+  R dt, inv_m, gravity, jx, jy, jz, ijx, ijy, ijz, hdt, hdt2;
+};
+template <typename R>
+__device__ __forceinline__ R vpin(R x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+template <typename R>
+__device__ __forceinline__ DynK<R> dyn_consts(const Consts<R>& c) {
+  DynK<R> k;
+  k.dt = vpin(c.dt); k.inv_m = vpin(c.inv_m); k.gravity = vpin(c.gravity);
+  k.jx = vpin(c.jx); k.jy = vpin(c.jy); k.jz = vpin(c.jz);
+  k.ijx = vpin(c.ijx); k.ijy = vpin(c.ijy); k.ijz = vpin(c.ijz);
+  k.hdt = vpin(c.hdt); k.hdt2 = vpin(c.hdt2);
+  return k;
+}
 
 template <typename R>
 struct Drone {
@@ -205,30 +228,19 @@ __device__ __forceinline__ void readback_fused(R x, R y, R z, R w, R qn[4], R m[
   qn[0] = x * inv; qn[1] = y * inv; qn[2] = z * inv; qn[3] = w * inv;
 }
 
-// sin/cos of the half rotation angle of _integrateQ (:887-888).  |theta| = |omega|*dt/2 is
-// small for all but violently tumbling drones, so a Taylor series (error < 1e-16 relative for
-// |theta| < 0.5 in double, < 1e-9 in float) replaces the library call there.
-__device__ __forceinline__ void small_sincos(double th, double& s, double& c) {
-  if (fabs(th) < 0.5) {
-    const double t2 = th * th;
-    s = th * (1.0 + t2 * (-1.0 / 6 + t2 * (1.0 / 120 + t2 * (-1.0 / 5040 + t2 * (1.0 / 362880 +
-             t2 * (-1.0 / 39916800 + t2 * (1.0 / 6227020800.0)))))));
-    c = 1.0 + t2 * (-0.5 + t2 * (1.0 / 24 + t2 * (-1.0 / 720 + t2 * (1.0 / 40320 + t2 * (-1.0 / 3628800 +
-             t2 * (1.0 / 479001600.0 + t2 * (-1.0 / 87178291200.0)))))));
-  } else {
-    s = sin(th);
-    c = cos(th);
-  }
+// cos(theta) and sin(theta)/theta of the half rotation angle of _integrateQ (:887-888) from
+// t2 = theta^2, |theta| < 0.5.  Both are even series in theta, so the step needs neither the
+// square root of |omega|^2 nor a division by |omega| (error < 1e-17 relative in double,
+// < 1e-9 in float).
+__device__ __forceinline__ void cos_sinc(double t2, double& c, double& sc) {
+  sc = 1.0 + t2 * (-1.0 / 6 + t2 * (1.0 / 120 + t2 * (-1.0 / 5040 + t2 * (1.0 / 362880 + t2 * (-1.0 / 39916800 +
+           t2 * (1.0 / 6227020800.0 + t2 * (-1.0 / 1307674368000.0)))))));
+  c = 1.0 + t2 * (-0.5 + t2 * (1.0 / 24 + t2 * (-1.0 / 720 + t2 * (1.0 / 40320 + t2 * (-1.0 / 3628800 +
+          t2 * (1.0 / 479001600.0 + t2 * (-1.0 / 87178291200.0)))))));
 }
-__device__ __forceinline__ void small_sincos(float th, float& s, float& c) {
-  if (fabsf(th) < 0.5f) {
-    const float t2 = th * th;
-    s = th * (1.0f + t2 * (-1.0f / 6 + t2 * (1.0f / 120 + t2 * (-1.0f / 5040 + t2 * (1.0f / 362880)))));
-    c = 1.0f + t2 * (-0.5f + t2 * (1.0f / 24 + t2 * (-1.0f / 720 + t2 * (1.0f / 40320 + t2 * (-1.0f / 3628800)))));
-  } else {
-    s = sinf(th);
-    c = cosf(th);
-  }
+__device__ __forceinline__ void cos_sinc(float t2, float& c, float& sc) {
+  sc = 1.0f + t2 * (-1.0f / 6 + t2 * (1.0f / 120 + t2 * (-1.0f / 5040 + t2 * (1.0f / 362880))));
+  c = 1.0f + t2 * (-0.5f + t2 * (1.0f / 24 + t2 * (-1.0f / 720 + t2 * (1.0f / 40320 + t2 * (-1.0f / 3628800)))));
 }
 
 // btQuaternion::getEulerZYX (pybullet getEulerFromQuaternion, BaseAviary.py:518).
@@ -397,7 +409,7 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
 template <typename R, bool FAST, bool ANGV = true>
 __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R Rm[9], bool gnd_upright,
                                             const R rpm[4], const R W[4], const R last[4], R dwsum,
-                                            const Consts<R>& c) {
+                                            const Consts<R>& c, const DynK<R>& k) {
   R fz, tx, ty, tz;
   body_wrench<R, FAST>(s, Rm, gnd_upright, rpm, W, c, fz, tx, ty, tz);
   if (!FAST && (c.flags & F_DW)) fz = fz + dwsum;      // _downwash :801-811 (body z)
@@ -409,36 +421,44 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R 
     Fy = Fy + (-c.drag_xy * S) * s.vy;
     Fz = Fz + (-c.drag_z * S) * s.vz;
   }
-  Fz = Fz - c.gravity;
+  Fz = Fz - k.gravity;
   // torques - ω × (Jω); ω̇ = J⁻¹ τ                     :852-854
-  const R jwx = c.jx * s.wx, jwy = c.jy * s.wy, jwz = c.jz * s.wz;
+  const R jwx = k.jx * s.wx, jwy = k.jy * s.wy, jwz = k.jz * s.wz;
   const R cx = s.wy * jwz - s.wz * jwy;
   const R cy = s.wz * jwx - s.wx * jwz;
   const R cz = s.wx * jwy - s.wy * jwx;
-  const R dwx = c.ijx * (tx - cx), dwy = c.ijy * (ty - cy), dwz = c.ijz * (tz - cz);
+  const R dwx = k.ijx * (tx - cx), dwy = k.ijy * (ty - cy), dwz = k.ijz * (tz - cz);
   // semi-implicit Euler                                :855-859
-  s.vx = s.vx + c.dt * (Fx * c.inv_m);
-  s.vy = s.vy + c.dt * (Fy * c.inv_m);
-  s.vz = s.vz + c.dt * (Fz * c.inv_m);
-  s.wx = s.wx + c.dt * dwx;
-  s.wy = s.wy + c.dt * dwy;
-  s.wz = s.wz + c.dt * dwz;
-  s.px = s.px + c.dt * s.vx;
-  s.py = s.py + c.dt * s.vy;
-  s.pz = s.pz + c.dt * s.vz;
+  s.vx = s.vx + k.dt * (Fx * k.inv_m);
+  s.vy = s.vy + k.dt * (Fy * k.inv_m);
+  s.vz = s.vz + k.dt * (Fz * k.inv_m);
+  s.wx = s.wx + k.dt * dwx;
+  s.wy = s.wy + k.dt * dwy;
+  s.wz = s.wz + k.dt * dwz;
+  s.px = s.px + k.dt * s.vx;
+  s.py = s.py + k.dt * s.vy;
+  s.pz = s.pz + k.dt * s.vz;
   // _integrateQ(quat, rpy_rates, dt)                  :876-889
   const R p = s.wx, q = s.wy, r = s.wz;
   const R n2 = p * p + q * q + r * r;
-  // 1/|omega| and |omega| = n2/|omega|; for omega = 0 both are NaN (rsq(0) = inf), which
-  // fails the isclose test below exactly like |omega| = 0 does
-  const R rn = g_rsqrt(n2);
-  const R nrm = n2 * rn;
-  if (nrm > R(1e-8)) {                                 // np.isclose(norm, 0): |norm| <= 1e-8
-    const R th = nrm * c.dt * R(0.5);
-    R co, si;
-    small_sincos(th, si, co);
-    const R k2 = R(2) * rn;                            // 2/|omega|
-    const R P = (k2 * (R(0.5) * p)) * si, Q = (k2 * (R(0.5) * q)) * si, Rr = (k2 * (R(0.5) * r)) * si;
+  // np.isclose(|omega|, 0) <=> |omega| <= 1e-8 <=> n2 <= 1e-16; the square root is taken only
+  // inside a rounding window around the threshold
+  const bool rot = n2 > R(1.000001e-16) || (n2 > R(0.999999e-16) && g_sqrt(n2) > R(1e-8));
+  if (rot) {
+    // q' = (I cos(theta) + (2/|omega|) Lambda sin(theta)) q, theta = |omega| dt/2: the off-diagonal
+    // weights (2/|omega|)(p/2) sin(theta) = p * (dt/2) * sin(theta)/theta
+    const R t2 = n2 * k.hdt2;                          // theta^2
+    R co, sh;                                          // cos(theta), sin(theta)/|omega|
+    if (t2 < R(0.25)) {
+      R sc;
+      cos_sinc(t2, co, sc);
+      sh = k.hdt * sc;
+    } else {
+      const R nrm = g_sqrt(n2), th = nrm * k.hdt;
+      co = g_cos(th);
+      sh = g_sin(th) / nrm;
+    }
+    const R P = p * sh, Q = q * sh, Rr = r * sh;
     const R x = qn[0], y = qn[1], z = qn[2], w = qn[3];
     s.qx = ((co * x + Rr * y) - Q * z) + P * w;
     s.qy = ((-Rr * x + co * y) + P * z) + Q * w;

@@ -149,7 +149,8 @@ __device__ __forceinline__ void store_drone(const SimView<R>& v, long long n, co
 // (BaseAviary.py:343-372 loop body).  MULTI: envs have D > 1 drones and may need downwash.
 template <typename R, bool MULTI, bool FAST, bool ANGV = true>
 __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const R W[4], const R last[4],
-                                              const Consts<R>& c, R* sx, R* sy, R* sz, int tid, int base, int D) {
+                                              const Consts<R>& c, const DynK<R>& k, R* sx, R* sy, R* sz, int tid,
+                                              int base, int D) {
   R qn[4], Rm[9];
   readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);  // :346-347 -> :517, :836
   bool up = true;
@@ -161,16 +162,14 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
     dw = downwash_sum(s.px, s.py, s.pz, sx, sy, sz, base, D, c);
     __syncthreads();
   }
-  dyn_substep<R, FAST, ANGV>(s, qn, Rm, up, rpm, W, last, dw, c);
+  dyn_substep<R, FAST, ANGV>(s, qn, Rm, up, rpm, W, last, dw, c, k);
 }
 
 // Bytes of dynamic LDS the step kernel needs for its observation tile: the row's columns
-// (state, history, current action) plus the first 12 floats of the terminal row (pre-reset
-// state of envs that finish this step; the rest of a terminal row equals the reset row).
-// A == 4 keeps float4 columns (state 3, history+action L, terminal 3); A == 1 / 3 keep float
-// columns (state 12, history+action L*A, terminal 12).
+// (state, history, current action).  A == 4 keeps float4 columns (state 3, history+action L);
+// A == 1 / 3 keep float columns (state 12, history+action L*A).
 __host__ __device__ inline int step_tile_bytes(int A, int ring_len) {
-  return A == 4 ? (3 + ring_len + 3) * kPad * 16 : (12 + ring_len * A + 12) * kPad * 4;
+  return A == 4 ? (3 + ring_len) * kPad * 16 : (12 + ring_len * A) * kPad * 4;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -258,9 +257,10 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
   // propeller wrench: the same RPMs drive every substep of the control step (:349-367)
   R W[4];
   rpm_wrench<R, FAST>(rpm, c, W);
+  const DynK<R> dk = dyn_consts(c);
   // substeps 1..nsub-1 skip the (write-only) world ang_v; the last one produces it
   for (int it = 0; it < c.nsub - 1; ++it) {
-    substep_block<R, MULTI, FAST, false>(s, rpm, W, last, c, sx, sy, sz, tid, base, D);
+    substep_block<R, MULTI, FAST, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
     if (it == 0) {
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
       history_dma();
     }
   }
-  substep_block<R, MULTI, FAST, true>(s, rpm, W, last, c, sx, sy, sz, tid, base, D);
+  substep_block<R, MULTI, FAST, true>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D);
 #pragma unroll
   for (int k = 0; k < 4; ++k) last[k] = rpm[k];
   if (c.nsub == 1) history_dma();
@@ -340,16 +340,21 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
 
   const int NC = A == 4 ? 3 + v.ring_len : 12 + v.ring_len * A;  // tile columns (float4 / float)
   if (do_reset) {
-    // the terminal row's state part goes to the tile's extra columns (the history and action
-    // columns are shared with the reset row); the env goes back to INIT_XYZS / INIT_RPYS
-    // (_housekeeping :458-477; SB3 DummyVecEnv keeps the last obs as terminal_observation)
-    if (A == 4) {
-      tile4[(NC + 0) * kPad + tid] = make_float4(row12[0], row12[1], row12[2], row12[3]);
-      tile4[(NC + 1) * kPad + tid] = make_float4(row12[4], row12[5], row12[6], row12[7]);
-      tile4[(NC + 2) * kPad + tid] = make_float4(row12[8], row12[9], row12[10], row12[11]);
-    } else {
+    // the terminal row's state part is stored straight from registers (finished envs are rare;
+    // its history and action columns equal the reset row's and go out with the tile copy-out);
+    // the env goes back to INIT_XYZS / INIT_RPYS (_housekeeping :458-477; SB3 DummyVecEnv keeps
+    // the last obs as terminal_observation)
+    if (active && io.terminal_obs != nullptr) {
+      float* trow = io.terminal_obs + n * v.W;
+      if (A == 4) {   // W = 72: 16-byte aligned rows
+        float4* t4 = reinterpret_cast<float4*>(trow);
+        t4[0] = make_float4(row12[0], row12[1], row12[2], row12[3]);
+        t4[1] = make_float4(row12[4], row12[5], row12[6], row12[7]);
+        t4[2] = make_float4(row12[8], row12[9], row12[10], row12[11]);
+      } else {
 #pragma unroll
-      for (int k = 0; k < 12; ++k) tilef[(NC + k) * kPad + tid] = row12[k];
+        for (int k = 0; k < 12; ++k) trow[k] = row12[k];
+      }
     }
     const R* ini = MULTI ? v.init + d * 10 : c.init0;
     s.px = ini[0]; s.py = ini[1]; s.pz = ini[2];
@@ -424,8 +429,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             if ((done_rows >> rr[u]) & 1ull) {
-              const float4 tv = cc[u] < ncs ? tile4[(NC + cc[u]) * kPad + rr[u]] : val[u];
-              reinterpret_cast<float4*>(io.terminal_obs)[n0 * NC + idx[u]] = tv;
+              if (cc[u] >= ncs) reinterpret_cast<float4*>(io.terminal_obs)[n0 * NC + idx[u]] = val[u];
             }
           }
         }
@@ -456,8 +460,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(SimView<R> v, StepIO<R> io,
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             if ((done_rows >> rr[u]) & 1ull) {
-              const float tv = cc[u] < ncs ? tilef[(NC + cc[u]) * kPad + rr[u]] : val[u];
-              io.terminal_obs[n0 * NC + idx[u]] = tv;
+              if (cc[u] >= ncs) io.terminal_obs[n0 * NC + idx[u]] = val[u];
             }
           }
         }
@@ -499,13 +502,14 @@ __global__ __launch_bounds__(kWave) void integrate_kernel(SimView<R> v, const Co
   R last[4];
   load_drone(v, nn, s, last, true);
   const long long N = v.N;
+  const DynK<R> dk = dyn_consts(c);
   for (int t = 0; t < n_sub; ++t) {
     R rpm[4];
     const R* src = rpm_in + ((long long)t * N + nn) * 4;
     rpm[0] = src[0]; rpm[1] = src[1]; rpm[2] = src[2]; rpm[3] = src[3];
     R W[4];
     rpm_wrench<R, false>(rpm, c, W);
-    substep_block<R, MULTI, false>(s, rpm, W, last, c, sx, sy, sz, tid, base, D);
+    substep_block<R, MULTI, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];
     if (traj && active) {
