@@ -145,6 +145,7 @@ Consts<R> make_consts(const gpd_sim* s) {
   c.drag_z = (R)P.drag_coeff_z;
   c.two_pi = (R)(2.0 * M_PI);
   c.dw1 = (R)P.dw_coeff_1; c.dw2 = (R)P.dw_coeff_2; c.dw3 = (R)P.dw_coeff_3;
+  c.dwk1 = (R)(P.dw_coeff_1 * ((P.prop_radius / 4) * (P.prop_radius / 4)));
   c.inv_m = (R)(1.0 / P.m);
   c.rpm2rad = (R)(2.0 * M_PI / 60.0);
   for (int k = 0; k < 4; ++k) {

@@ -79,6 +79,7 @@ struct Consts {
   R ge_coeff, prop_r, ge_clip;             // :108-109, :128
   R drag_xy, drag_z, two_pi;               // :1009, 2*np.pi (:773)
   R dw1, dw2, dw3;                         // :1010-1012
+  R dwk1;                                  // DW1 * (PROP_RADIUS/4)^2 (downwash alpha numerator)
   R rx[4], ry[4], rz[4];                   // prop link origins (cf2x.urdf:42,54,66,78)
   R inv_m;                 // 1/M      (F/M as a multiply; differs from the division by <= 1 ulp)
   R rpm2rad;               // 2*pi/60  (drag: sum(2*pi*rpm/60))
@@ -484,15 +485,15 @@ __device__ __forceinline__ R downwash_sum(R px, R py, R pz, const R* sx, const R
   for (int j = 0; j < D; ++j) {
     const R dz = sz[base + j] - pz;
     const R ddx = sx[base + j] - px, ddy = sy[base + j] - py;
-    const R dxy = g_sqrt(ddx * ddx + ddy * ddy);
-    const bool hit = (dz > R(0)) && (dxy < R(10));
+    const R dxy2 = ddx * ddx + ddy * ddy;                 // |dxy|^2: the force needs no square root
+    const bool hit = (dz > R(0)) && (dxy2 < R(100));      // delta_z > 0 and delta_xy < 10
     if (__ballot(hit) != 0ull) {
       if (hit) {
-        const R qq = c.prop_r / (R(4) * dz);
-        const R alpha = c.dw1 * (qq * qq);
+        // alpha = DW1 (PROP_RADIUS/(4 dz))^2, beta = DW2 dz + DW3, f = -alpha exp(-0.5 (dxy/beta)^2);
+        // beta = 0 keeps numpy's IEEE result: dxy^2/0 = inf -> exp(-inf) = 0 (0/0 = nan at dxy = 0)
+        const R alpha = c.dwk1 / (dz * dz);
         const R beta = c.dw2 * dz + c.dw3;
-        const R t = dxy / beta;
-        total = total + (-alpha * g_exp(R(-0.5) * (t * t)));
+        total = total + (-alpha * g_exp(R(-0.5) * (dxy2 / (beta * beta))));
       }
     }
   }

@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
 from oracle.bullet_math import quat_from_euler, quat_roundtrip  # noqa: E402
 from oracle.params import derived  # noqa: E402
-from oracle.ref_aviary import RefAviary, rpm_from_action  # noqa: E402
+from oracle.ref_aviary import ACT_WIDTH, RefAviary, rpm_from_action  # noqa: E402
 from tests.oracle_runs import run_vec  # noqa: E402
 
 HOVER = derived("cf2x")["hover_rpm"]
@@ -56,16 +56,22 @@ def integrate_fixture(name, n, T, every, aero=(), z=1.0, scale=1.0, seed=0, dron
                         traj=traj[every - 1::every])
 
 
-def step_fixture(name, n_envs, T, act, task, D=1, seed=0):
+def step_fixture(name, n_envs, T, act, task, D=1, seed=0, wrench="dyn", scale=1.0):
     rng = np.random.default_rng(seed)
-    A = 4 if act == "rpm" else 1
-    actions = rng.uniform(-1, 1, (T, n_envs, D, A)).astype(np.float32)
-    obs, rew, te, tr, tobs = run_vec(actions, n_envs, drones_per_env=D, act=act, task=task)
+    A = ACT_WIDTH[act]
+    actions = (rng.uniform(-1, 1, (T, n_envs, D, A)) * scale).astype(np.float32)
+    envs = []
+    obs, rew, te, tr, tobs = run_vec(actions, n_envs, drones_per_env=D, act=act, task=task, wrench=wrench, envs=envs)
+    extra = {}
+    if hasattr(envs[0], "ctrl"):
+        extra["ctrl_state"] = np.concatenate([e.ctrl_state() for e in envs])
+        extra["state20"] = np.concatenate([e.state20() for e in envs])
     keys = sorted(tobs)
     W = obs.shape[-1]
     np.savez_compressed(os.path.join(HERE, name), actions=actions, obs=obs, reward=rew, terminated=te,
                         truncated=tr, terminal_keys=np.array(keys, dtype=np.int64).reshape(-1, 2),
-                        terminal_obs=np.array([tobs[k] for k in keys], dtype=np.float32).reshape(len(keys), D, W))
+                        terminal_obs=np.array([tobs[k] for k in keys], dtype=np.float32).reshape(len(keys), D, W),
+                        wrench=wrench, **extra)
 
 
 def main():
@@ -74,6 +80,10 @@ def main():
     step_fixture("c1_hover_one_d_rpm.npz", 1, 150, "one_d_rpm", "hover")
     step_fixture("hover_rpm_8env.npz", 8, 60, "rpm", "hover", seed=3)
     step_fixture("multihover_2x2.npz", 2, 60, "rpm", "multihover", D=2, seed=4)
+    # DSLPIDControl action types; the VEL loop is chaotic, so its horizon is short
+    step_fixture("pid_waypoint_pyb.npz", 4, 60, "pid", "hover", seed=8, wrench="geom", scale=0.5)
+    step_fixture("one_d_pid_dyn.npz", 4, 60, "one_d_pid", "hover", seed=9)
+    step_fixture("vel_pyb.npz", 4, 16, "vel", "hover", seed=10, wrench="geom")
     # raw DYN integrator, 5 s (1200 substeps), every 10th substep kept
     integrate_fixture("integrate_dyn_5s.npz", n=8, T=1200, every=10, seed=5)
     integrate_fixture("integrate_gnd_drag.npz", n=8, T=600, every=10, aero=("gnd", "drag"), z=0.06, scale=0.5, seed=6)
