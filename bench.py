@@ -234,16 +234,24 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of hipGraph replays")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, the real multi-GPU path); gloo only to rehearse several ranks on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dev_index = local_rank
+    if args.dist_backend == "gloo":
+        dev_index = local_rank % torch.cuda.device_count()
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        torch.distributed.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
-    device = torch.device(f"cuda:{local_rank}")
+        torch.cuda.set_device(dev_index)
+        if args.dist_backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device(f"cuda:{dev_index}"))
+        else:
+            torch.distributed.init_process_group("gloo")
+    device = torch.device(f"cuda:{dev_index}")
     torch.cuda.set_device(device)
 
     from gym_pybullet_drones_routing_amd.enums import ActionType
@@ -312,7 +320,8 @@ def main():
             gather_batch(sim.reward, rew_all)
         torch.cuda.synchronize(device)
         gw = max_over_ranks(time.perf_counter() - t0, device)
-        result["gather"] = {"mode": "eager step + RCCL all_gather of obs and reward per step",
+        coll = "RCCL" if args.dist_backend == "nccl" else "gloo (rehearsal)"
+        result["gather"] = {"mode": f"eager step + {coll} all_gather of obs and reward per step",
                             "ms_per_step": 1000 * gw / G, "value": world * E * nsub * G / gw,
                             "bytes_per_step": int(obs_all.numel() * 4 + rew_all.numel() * 4)}
 

@@ -29,6 +29,8 @@ def max_over_ranks(value, device=None):
     """The max of a host float over all ranks (the bench's job time)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return float(value)
+    if dist.get_backend() == "gloo":
+        device = None            # gloo reduces host tensors
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -41,6 +43,12 @@ def gather_batch(local, out=None):
     world = dist.get_world_size()
     if out is None:
         out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    if dist.get_backend() == "gloo" and local.is_cuda:
+        # gloo (CPU tests, single-GPU rehearsals): gather through host memory
+        parts = [torch.empty_like(local, device="cpu") for _ in range(world)]
+        dist.all_gather(parts, local.detach().cpu().contiguous())
+        out.copy_(torch.cat(parts))
+        return out
     dist.all_gather_into_tensor(out, local.contiguous())
     return out
 
