@@ -1,0 +1,129 @@
+"""GPU-vs-oracle parity over the configuration space the reference's constructor accepts:
+drone models (cf2x / cf2p / racer, BaseAviary.py:843-851), frequencies (pyb_freq / ctrl_freq:
+substeps per step and action-buffer length, BaseAviary.py:76-84, BaseRLAviary.py:66),
+custom initial positions and attitudes (:194-207, :486-491), ragged env counts (partial last
+block), drones per env from 1 to 64, autoreset off, and masked resets (reset() of a subset).
+
+f64 path gates: observations to float32 rounding (rtol 1e-5), done flags exact, final state
+relative L2 <= 1e-10 (state_rel_err)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.ref_aviary import RefAviary
+from tests.oracle_runs import run_vec, state_rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _sim(**kw):
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+    return BatchedAviarySim(device="cuda:0", precision="f64", **kw)
+
+
+def _compare_run(acts, E, D=1, act="rpm", task="hover", sim_kw=None, ref_kw=None):
+    from gym_pybullet_drones_routing_amd.enums import ActionType
+    envs = []
+    obs_r, rew_r, te_r, tr_r, tobs_r = run_vec(acts, E, drones_per_env=D, act=act, task=task, envs=envs,
+                                               **(ref_kw or {}))
+    sim = _sim(n_envs=E, drones_per_env=D, task=task, act=ActionType(act), **(sim_kw or {}))
+    for t in range(acts.shape[0]):
+        o, r, te, tr = sim.step(torch.from_numpy(acts[t]).cuda())
+        np.testing.assert_array_equal(te.cpu().numpy().astype(bool), te_r[t], err_msg=f"terminated, step {t}")
+        np.testing.assert_array_equal(tr.cpu().numpy().astype(bool), tr_r[t], err_msg=f"truncated, step {t}")
+        np.testing.assert_allclose(o.cpu().numpy(), obs_r[t], rtol=1e-5, atol=1e-6, err_msg=f"obs, step {t}")
+        np.testing.assert_allclose(r.cpu().numpy(), rew_r[t], rtol=1e-6, atol=1e-5)
+        tobs = sim.terminal_obs.cpu().numpy()
+        for e in np.nonzero(te_r[t] | tr_r[t])[0]:
+            np.testing.assert_allclose(tobs[e], tobs_r[(t, e)], rtol=1e-5, atol=1e-6)
+    err = state_rel_err(sim.state20().cpu().numpy(), np.concatenate([e.state20() for e in envs]))
+    assert err.max() <= 1e-10, err.max()
+    sim.close()
+
+
+@pytest.mark.parametrize("model", ["cf2p", "racer"])
+def test_models_step_parity(model):
+    from gym_pybullet_drones_routing_amd.enums import DroneModel
+    rng = np.random.default_rng(31)
+    E, T = 8, 60
+    acts = np.clip(rng.normal(0, 0.15, (T, E, 1, 4)), -1, 1).astype(np.float32)
+    _compare_run(acts, E, sim_kw=dict(drone_model=DroneModel(model)), ref_kw=dict(model=model))
+
+
+@pytest.mark.parametrize("pyb,ctrl,act", [(240, 240, "rpm"), (240, 48, "one_d_rpm"), (480, 60, "rpm"),
+                                          (1000, 50, "rpm")])
+def test_frequencies_step_parity(pyb, ctrl, act):
+    rng = np.random.default_rng(32)
+    E, T = 6, 50
+    A = 4 if act == "rpm" else 1
+    acts = np.clip(rng.normal(0, 0.2, (T, E, 1, A)), -1, 1).astype(np.float32)
+    _compare_run(acts, E, act=act, sim_kw=dict(pyb_freq=pyb, ctrl_freq=ctrl),
+                 ref_kw=dict(pyb_freq=pyb, ctrl_freq=ctrl))
+
+
+def test_initial_pose_step_parity():
+    """Custom INIT_XYZS / INIT_RPYS: the reset template goes through the Bullet orientation
+    round trip (quat from Euler -> btTransform -> readback)."""
+    rng = np.random.default_rng(33)
+    E, T = 6, 40
+    xyz = [[0.2, -0.1, 0.5]]
+    rpy = [[0.1, -0.05, 0.7]]
+    acts = np.clip(rng.normal(0, 0.1, (T, E, 1, 4)), -1, 1).astype(np.float32)
+    _compare_run(acts, E, sim_kw=dict(initial_xyzs=xyz, initial_rpys=rpy),
+                 ref_kw=dict(initial_xyzs=xyz, initial_rpys=rpy))
+
+
+@pytest.mark.parametrize("E", [1, 3, 70])
+def test_ragged_env_counts(E):
+    """Env counts that leave the last 64-lane block partly empty."""
+    rng = np.random.default_rng(34 + E)
+    T = 30
+    acts = rng.uniform(-1, 1, (T, E, 1, 4)).astype(np.float32)
+    _compare_run(acts, E)
+
+
+@pytest.mark.parametrize("D,E,dw", [(5, 4, True), (64, 2, False)])
+def test_multihover_drone_counts(D, E, dw):
+    """Drones per env that do not divide the wave (5: 12 envs per 64-lane block) and a whole
+    wave per env (64); downwash from a staggered start for D = 5."""
+    rng = np.random.default_rng(35 + D)
+    T = 30
+    if dw:
+        xyz = [[0.1 * math.cos(2 * math.pi * i / D), 0.1 * math.sin(2 * math.pi * i / D), 0.4 + 0.1 * i]
+               for i in range(D)]
+        aero = ("dw",)
+    else:
+        xyz, aero = None, ()
+    acts = np.clip(rng.normal(0, 0.1, (T, E, D, 4)), -1, 1).astype(np.float32)
+    _compare_run(acts, E, D=D, task="multihover", sim_kw=dict(initial_xyzs=xyz, aero=aero),
+                 ref_kw=dict(initial_xyzs=xyz, aero=aero))
+
+
+def test_autoreset_off_and_masked_reset():
+    """autoreset=False: finished envs keep integrating (the caller decides when to reset);
+    reset(env_mask) re-initialises exactly the masked envs (BaseAviary.reset :220-255) and keeps
+    the action history (never cleared by the reference)."""
+    rng = np.random.default_rng(36)
+    E, T = 5, 40
+    acts = rng.uniform(-1, 1, (T, E, 1, 4)).astype(np.float32)
+    envs = [RefAviary(task="hover") for _ in range(E)]
+    sim = _sim(n_envs=E, task="hover", autoreset=False)
+    mask = np.array([1, 0, 1, 0, 0], np.uint8)
+    for t in range(T):
+        if t == 25:
+            obs_reset = sim.reset(torch.from_numpy(mask).cuda()).cpu().numpy()
+            for e in np.nonzero(mask)[0]:
+                o_ref, _ = envs[e].reset()
+                np.testing.assert_allclose(obs_reset[e], o_ref, rtol=1e-6, atol=1e-7)
+        o, r, te, tr = sim.step(torch.from_numpy(acts[t]).cuda())
+        o = o.cpu().numpy()
+        for e, env in enumerate(envs):
+            o_ref, r_ref, te_ref, tr_ref, _ = env.step(acts[t, e])
+            np.testing.assert_allclose(o[e], o_ref, rtol=1e-5, atol=1e-6)
+            assert bool(tr.cpu().numpy()[e]) == tr_ref and bool(te.cpu().numpy()[e]) == te_ref
+    err = state_rel_err(sim.state20().cpu().numpy(), np.concatenate([e.state20() for e in envs]))
+    assert err.max() <= 1e-10
+    np.testing.assert_array_equal(sim.step_counters().cpu().numpy(), [e.step_counter for e in envs])
+    sim.close()
