@@ -16,7 +16,13 @@ from ..sim import BatchedAviarySim
 from .spaces import action_space, observation_space
 
 
-class AviaryVecEnv:
+try:  # a real SB3 VecEnv where stable-baselines3 is installed, so PPO(policy, env) takes it as is
+    from stable_baselines3.common.vec_env import VecEnv as _VecEnvBase
+except Exception:  # SB3 absent (this image): same protocol, no base class
+    _VecEnvBase = object
+
+
+class AviaryVecEnv(_VecEnvBase):
     def __init__(self, num_envs, task="hover", num_drones=1, drone_model=DroneModel.CF2X, initial_xyzs=None,
                  initial_rpys=None, physics=Physics.DYN, aero=(), pyb_freq=240, ctrl_freq=30,
                  obs=ObservationType.KIN, act=ActionType.RPM, precision="f64", device=None, output="numpy",
@@ -39,6 +45,8 @@ class AviaryVecEnv:
         self.observation_space = observation_space(num_drones, self.sim.act_width, int(ctrl_freq // 2))
         self._actions = torch.zeros((num_envs, num_drones, self.sim.act_width), dtype=torch.float32,
                                     device=self.sim.device)
+        if _VecEnvBase is not object:
+            super().__init__(self.num_envs, self.observation_space, self.action_space)
         self.render_mode = None
 
     # ------------------------------------------------------------------ VecEnv protocol
