@@ -45,9 +45,9 @@ class AviaryVecEnv(_VecEnvBase):
         self.observation_space = observation_space(num_drones, self.sim.act_width, int(ctrl_freq // 2))
         self._actions = torch.zeros((num_envs, num_drones, self.sim.act_width), dtype=torch.float32,
                                     device=self.sim.device)
+        self.render_mode = None
         if _VecEnvBase is not object:
             super().__init__(self.num_envs, self.observation_space, self.action_space)
-        self.render_mode = None
 
     # ------------------------------------------------------------------ VecEnv protocol
     def reset(self):
