@@ -249,9 +249,9 @@ int launch_step(gpd_sim* s, const float* actions, float* obs, float* reward, uin
   const Consts<R>* c = (const Consts<R>*)s->d_consts;
   const unsigned grid = grid_for(s->N, s->tpb);
   const size_t lds = (size_t)s->tile_bytes;
-  typedef void (*StepFn)(SimView<R>, StepIO<R>, const Consts<R>*);
+  typedef void (*StepFn)(R*, const float*, int2*, const Consts<R>*, long long, int, int, SimView<R>, StepIO<R>);
   const StepFn f = (StepFn)step_kernel_fn<R>(s);
-  hipLaunchKernelGGL(f, dim3(grid), dim3(kWave), lds, st, v, io, c);
+  hipLaunchKernelGGL(f, dim3(grid), dim3(kWave), lds, st, v.state, io.actions, v.ctr, c, v.npad, v.N, v.tpb, v, io);
   HIP_TRY(hipGetLastError());
   return GPD_OK;
 }

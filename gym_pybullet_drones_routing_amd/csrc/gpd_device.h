@@ -97,6 +97,9 @@ struct Consts {
 template <typename R>
 struct DynK {
   R dt, inv_m, gravity, jx, jy, jz, ijx, ijy, ijz, hdt, hdt2;
+  R kf, km, L, Ls2;        // propeller wrench (rpm_wrench)
+  float hover_f32;         // action -> RPM
+  int model;
 };
 template <typename R>
 __device__ __forceinline__ R vpin(R x) {
@@ -106,10 +109,17 @@ __device__ __forceinline__ R vpin(R x) {
 template <typename R>
 __device__ __forceinline__ DynK<R> dyn_consts(const Consts<R>& c) {
   DynK<R> k;
-  k.dt = vpin(c.dt); k.inv_m = vpin(c.inv_m); k.gravity = vpin(c.gravity);
-  k.jx = vpin(c.jx); k.jy = vpin(c.jy); k.jz = vpin(c.jz);
-  k.ijx = vpin(c.ijx); k.ijy = vpin(c.ijy); k.ijz = vpin(c.ijz);
-  k.hdt = vpin(c.hdt); k.hdt2 = vpin(c.hdt2);
+  k.dt = c.dt; k.inv_m = c.inv_m; k.gravity = c.gravity;
+  k.jx = c.jx; k.jy = c.jy; k.jz = c.jz;
+  k.ijx = c.ijx; k.ijy = c.ijy; k.ijz = c.ijz;
+  k.hdt = c.hdt; k.hdt2 = c.hdt2;
+  k.kf = c.kf; k.km = c.km; k.L = c.L; k.Ls2 = c.Ls2; k.hover_f32 = c.hover_f32; k.model = c.model;
+  // one statement for all of them: hipcc issues the scalar loads of every constant-block line
+  // back to back and waits once (K$ misses in parallel), instead of a load + wait pair per use
+  // behind each model / flag branch
+  asm volatile("" : "+v"(k.dt), "+v"(k.inv_m), "+v"(k.gravity), "+v"(k.jx), "+v"(k.jy), "+v"(k.jz),
+               "+v"(k.ijx), "+v"(k.ijy), "+v"(k.ijz), "+v"(k.hdt), "+v"(k.hdt2), "+v"(k.kf), "+v"(k.km),
+               "+v"(k.L), "+v"(k.Ls2), "+v"(k.hover_f32), "+s"(k.model));
   return k;
 }
 
@@ -336,32 +346,32 @@ __device__ __forceinline__ float action_to_rpm(float hover_f32, float a) {
 // a residual roll/pitch torque instead of the reference's exact zero.
 // W = {fz, tx, ty, tz} in the body frame.
 template <typename R, bool FAST>
-__device__ __forceinline__ void rpm_wrench(const R rpm[4], const Consts<R>& c, R W[4]) {
+__device__ __forceinline__ void rpm_wrench(const R rpm[4], const DynK<R>& k, const Consts<R>& c, R W[4]) {
 #pragma clang fp contract(off)
   R f[4], zt[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const R r2 = rpm[k] * rpm[k];
-    f[k] = r2 * c.kf;                                  // :838
-    zt[k] = r2 * c.km;                                 // :842
+  for (int m = 0; m < 4; ++m) {
+    const R r2 = rpm[m] * rpm[m];
+    f[m] = r2 * k.kf;                                  // :838
+    zt[m] = r2 * k.km;                                 // :842
   }
-  if (c.model == MODEL_RACE) {
+  if (k.model == MODEL_RACE) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) zt[k] = -zt[k];        // :843-844
+    for (int m = 0; m < 4; ++m) zt[m] = -zt[m];        // :843-844
   }
   W[0] = ((f[0] + f[1]) + f[2]) + f[3];                // np.sum(forces) :839
   W[3] = ((-zt[0] + zt[1]) - zt[2]) + zt[3];           // :845
   if (!FAST && (c.flags & F_GEOM)) {                   // _physics: forces at prop links :698-705
     R tx = R(0), ty = R(0);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { tx = tx + c.ry[k] * f[k]; ty = ty - c.rx[k] * f[k]; }
+    for (int m = 0; m < 4; ++m) { tx = tx + c.ry[m] * f[m]; ty = ty - c.rx[m] * f[m]; }
     W[1] = tx; W[2] = ty;
-  } else if (c.model == MODEL_CF2P) {                  // :849-851
-    W[1] = (f[1] - f[3]) * c.L;
-    W[2] = (-f[0] + f[2]) * c.L;
+  } else if (k.model == MODEL_CF2P) {                  // :849-851
+    W[1] = (f[1] - f[3]) * k.L;
+    W[2] = (-f[0] + f[2]) * k.L;
   } else {                                             // CF2X / RACE :846-848 (roll-sign quirk kept)
-    W[1] = (((f[0] + f[1]) - f[2]) - f[3]) * c.Ls2;
-    W[2] = (((-f[0] + f[1]) + f[2]) - f[3]) * c.Ls2;
+    W[1] = (((f[0] + f[1]) - f[2]) - f[3]) * k.Ls2;
+    W[2] = (((-f[0] + f[1]) + f[2]) - f[3]) * k.Ls2;
   }
 }
 

@@ -22,10 +22,10 @@ for prec in ("f64", "f32"):
         for _ in range(4): g.replay()
         torch.cuda.synchronize()
         nb = min(65536, (E + 63) // 64)
-        buf = np.zeros((nb, 10), np.uint64)
+        buf = np.zeros((nb, 12), np.uint64)
         assert lib.gpd_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), nb) == 0
         t = buf.astype(np.int64)
-        order = [0, 1, 2, 3, 4, 5, 6, 8, 9, 7]   # 8/9 sit inside the copy-out (after LDS reads, after stores)
+        order = [0, 10, 1, 2, 3, 4, 5, 6, 8, 9, 7]   # 10: loads landed; 8/9 inside the copy-out (after LDS reads, after stores)
         d = [(a, b, int(np.median(t[:, b] - t[:, a]))) for a, b in zip(order[:-1], order[1:])]
         print(f"{prec} E={E}: per-block phase cycles (median) " + " ".join(f"{a}->{b}:{c}" for a, b, c in d) +
               f" | total median {int(np.median(t[:,7]-t[:,0]))}", flush=True)
