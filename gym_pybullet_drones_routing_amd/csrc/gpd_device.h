@@ -209,17 +209,14 @@ template <> struct UnitTol<float> { static constexpr float v = 1e-4f; };
 template <typename R>
 __device__ __forceinline__ void readback_fused(R x, R y, R z, R w, R qn[4], R m[9]) {
   const R d = x * x + y * y + z * z + w * w;
-  R inv, s;
-  if (g_abs(d - R(1)) < UnitTol<R>::v) {
-    // |q| = 1 +- eps (every quaternion _integrateQ produces from a unit one: its update matrix
-    // is orthogonal): one Newton step from 1 gives 1/sqrt(d) and 2/d with errors 3eps^2/8 and
-    // 2eps^2, below the last bit for |eps| < 1e-9 (double) / 1e-4 (float).
-    inv = R(1.5) - R(0.5) * d;
-    s = R(2) * (R(2) - d);
-  } else {
-    inv = g_rsqrt(d);             // 1/|q|
-    s = R(2) * (inv * inv);       // 2/|q|^2  (setRotation's s)
-  }
+  // |q| = 1 +- eps (every quaternion _integrateQ produces from a unit one: its update matrix
+  // is orthogonal): one Newton step from 1 gives 1/sqrt(d) and 2/d with errors 3eps^2/8 and
+  // 2eps^2, below the last bit for |eps| < 1e-9 (double) / 1e-4 (float).  Both forms are
+  // evaluated and selected, which keeps the substep one basic block (no exec-mask branch).
+  const bool unit = g_abs(d - R(1)) < UnitTol<R>::v;
+  const R invr = g_rsqrt(d);                            // 1/|q|
+  const R inv0 = unit ? R(1.5) - R(0.5) * d : invr;
+  const R s = unit ? R(2) * (R(2) - d) : R(2) * (invr * invr);   // 2/|q|^2 (setRotation's s)
   const R xs = x * s, ys = y * s, zs = z * s;
   const R wx = w * xs, wy = w * ys, wz = w * zs;
   const R xx = x * xs, xy = x * ys, xz = x * zs;
@@ -228,14 +225,12 @@ __device__ __forceinline__ void readback_fused(R x, R y, R z, R w, R qn[4], R m[
   m[3] = xy + wz;          m[4] = R(1) - (xx + zz);  m[5] = yz - wx;
   m[6] = xz - wy;          m[7] = yz + wx;           m[8] = R(1) - (xx + yy);
   const R trace = m[0] + m[4] + m[8];
-  R key;
-  if (trace > R(0)) {
-    key = w;
-  } else {
-    const int i = m[0] < m[4] ? (m[4] < m[8] ? 2 : 1) : (m[0] < m[8] ? 2 : 0);
-    key = i == 0 ? x : (i == 1 ? y : z);
-  }
-  inv = key < R(0) ? -inv : inv;
+  // sign rule as selects: the key component is w when trace > 0, else the component of the
+  // largest diagonal entry
+  const int i = m[0] < m[4] ? (m[4] < m[8] ? 2 : 1) : (m[0] < m[8] ? 2 : 0);
+  const R keyd = i == 0 ? x : (i == 1 ? y : z);
+  const R key = trace > R(0) ? w : keyd;
+  const R inv = key < R(0) ? -inv0 : inv0;
   qn[0] = x * inv; qn[1] = y * inv; qn[2] = z * inv; qn[3] = w * inv;
 }
 
@@ -452,32 +447,32 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R 
   // _integrateQ(quat, rpy_rates, dt)                  :876-889
   const R p = s.wx, q = s.wy, r = s.wz;
   const R n2 = p * p + q * q + r * r;
-  // np.isclose(|omega|, 0) <=> |omega| <= 1e-8 <=> n2 <= 1e-16; the square root is taken only
-  // inside a rounding window around the threshold
-  const bool rot = n2 > R(1.000001e-16) || (n2 > R(0.999999e-16) && g_sqrt(n2) > R(1e-8));
-  if (rot) {
-    // q' = (I cos(theta) + (2/|omega|) Lambda sin(theta)) q, theta = |omega| dt/2: the off-diagonal
-    // weights (2/|omega|)(p/2) sin(theta) = p * (dt/2) * sin(theta)/theta
-    const R t2 = n2 * k.hdt2;                          // theta^2
-    R co, sh;                                          // cos(theta), sin(theta)/|omega|
-    if (t2 < R(0.25)) {
-      R sc;
-      cos_sinc(t2, co, sc);
-      sh = k.hdt * sc;
-    } else {
+  // np.isclose(|omega|, 0) <=> |omega| <= 1e-8 <=> |omega|^2 <= 1e-16 (the two tests can only
+  // disagree when |omega| lies within an ulp of 1e-8; numpy's BLAS norm itself rounds there)
+  const bool rot = n2 > R(1e-16);
+  // q' = (I cos(theta) + (2/|omega|) Lambda sin(theta)) q, theta = |omega| dt/2: the off-diagonal
+  // weights (2/|omega|)(p/2) sin(theta) = p * (dt/2) * sin(theta)/theta.  Evaluated for every
+  // lane and selected (no branch); the library sin/cos fix-up for |theta| >= 0.5 (|omega| >=
+  // 240 rad/s at 240 Hz) is a wave-uniform branch that practically never runs.
+  const R t2 = n2 * k.hdt2;                            // theta^2
+  R co, sc;                                            // cos(theta), sin(theta)/theta
+  cos_sinc(t2, co, sc);
+  R sh = k.hdt * sc;                                   // sin(theta)/|omega|
+  const bool big = t2 >= R(0.25);
+  if (__ballot(big) != 0ull) {
+    if (big) {
       const R nrm = g_sqrt(n2), th = nrm * k.hdt;
       co = g_cos(th);
       sh = g_sin(th) / nrm;
     }
-    const R P = p * sh, Q = q * sh, Rr = r * sh;
-    const R x = qn[0], y = qn[1], z = qn[2], w = qn[3];
-    s.qx = ((co * x + Rr * y) - Q * z) + P * w;
-    s.qy = ((-Rr * x + co * y) + P * z) + Q * w;
-    s.qz = ((Q * x - P * y) + co * z) + Rr * w;
-    s.qw = ((-P * x - Q * y) - Rr * z) + co * w;
-  } else {
-    s.qx = qn[0]; s.qy = qn[1]; s.qz = qn[2]; s.qw = qn[3];
   }
+  const R P = p * sh, Q = q * sh, Rr = r * sh;
+  const R x = qn[0], y = qn[1], z = qn[2], w = qn[3];
+  const R nx = ((co * x + Rr * y) - Q * z) + P * w;
+  const R ny = ((-Rr * x + co * y) + P * z) + Q * w;
+  const R nz = ((Q * x - P * y) + co * z) + Rr * w;
+  const R nw = ((-P * x - Q * y) - Rr * z) + co * w;
+  s.qx = rot ? nx : x; s.qy = rot ? ny : y; s.qz = rot ? nz : z; s.qw = rot ? nw : w;
   // resetBaseVelocity(..., np.dot(rotation, rpy_rates))  :868-872
   if (!ANGV) return;
   s.ax = (Rm[0] * s.wx + Rm[1] * s.wy) + Rm[2] * s.wz;
