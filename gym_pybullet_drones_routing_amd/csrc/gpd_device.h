@@ -294,10 +294,11 @@ __device__ __forceinline__ AttitudeArgs<R> attitude_args(const R q[4]) {
 // |roll| > lim or |pitch| > lim, 0 < lim < pi/2 (HoverAviary.py:112, MultiHoverAviary.py:121)
 template <typename R>
 __device__ __forceinline__ bool tilted_beyond(const AttitudeArgs<R>& t, R sin_lim, R tan_lim) {
-  if (t.gimbal) return true;                      // |pitch| = pi/2
-  if (g_abs(t.sarg) > sin_lim) return true;       // |asin(sarg)| > lim
-  if (t.b > R(0)) return g_abs(t.a) > tan_lim * t.b;
-  return !(t.b == R(0) && t.a == R(0) && !signbit(t.b));  // |atan2| >= pi/2 except atan2(+-0, +0)
+  // gimbal: |pitch| = pi/2; |asin(sarg)| > lim; |atan2(a, b)| > lim (b > 0), >= pi/2 (b <= 0)
+  // except atan2(+-0, +0) = 0.  Written as one predicate (no branches).
+  const bool zero_roll = t.b == R(0) && t.a == R(0) && !signbit(t.b);
+  const bool roll_out = t.b > R(0) ? g_abs(t.a) > tan_lim * t.b : !zero_roll;
+  return t.gimbal || g_abs(t.sarg) > sin_lim || roll_out;
 }
 // |roll| < pi/2 and |pitch| < pi/2 (the _groundEffect condition, BaseAviary.py:742)
 template <typename R>
@@ -311,15 +312,18 @@ template <typename R>
 __device__ __forceinline__ void obs_euler_f32(const R q[4], const AttitudeArgs<R>& t, float& roll, float& pitch,
                                               float& yaw) {
   const R x = q[0], y = q[1], z = q[2], w = q[3];
-  if (t.sarg <= R(-0.99999)) {
-    pitch = -1.57079632679489661923f; roll = 0.0f; yaw = 2.0f * atan2f((float)x, (float)-y);
-  } else if (t.sarg >= R(0.99999)) {
-    pitch = 1.57079632679489661923f; roll = 0.0f; yaw = 2.0f * atan2f((float)-x, (float)y);
-  } else {
-    const R sa = t.sarg < R(-1) ? R(-1) : (t.sarg > R(1) ? R(1) : t.sarg);
-    pitch = asinf((float)sa);
-    roll = atan2f((float)t.a, (float)t.b);
-    yaw = atan2f((float)(R(2) * (x * y + w * z)), (float)(w * w + x * x - y * y - z * z));
+  // the regular branch for every lane, the gimbal branches (|sarg| >= 0.99999) as a
+  // wave-uniform fix-up
+  const R sa = t.sarg < R(-1) ? R(-1) : (t.sarg > R(1) ? R(1) : t.sarg);
+  pitch = asinf((float)sa);
+  roll = atan2f((float)t.a, (float)t.b);
+  yaw = atan2f((float)(R(2) * (x * y + w * z)), (float)(w * w + x * x - y * y - z * z));
+  if (__ballot(t.gimbal) != 0ull) {
+    if (t.sarg <= R(-0.99999)) {
+      pitch = -1.57079632679489661923f; roll = 0.0f; yaw = 2.0f * atan2f((float)x, (float)-y);
+    } else if (t.sarg >= R(0.99999)) {
+      pitch = 1.57079632679489661923f; roll = 0.0f; yaw = 2.0f * atan2f((float)-x, (float)y);
+    }
   }
 }
 

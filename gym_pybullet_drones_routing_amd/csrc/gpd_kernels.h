@@ -302,8 +302,10 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
   if (v.task != TASK_NONE) {
     const R* tg = MULTI ? v.target + d * 3 : c.target0;
     const R tx = tg[0] - s.px, ty = tg[1] - s.py, tz = tg[2] - s.pz;
-    const R dist = g_sqrt(tx * tx + ty * ty + tz * tz);
-    const R d2 = dist * dist;
+    // |e|^2: the reward max(0, 2 - |e|^4) and HoverAviary's |e| < 1e-4 need no square root;
+    // MultiHoverAviary sums the distances themselves
+    const R d2 = tx * tx + ty * ty + tz * tz;
+    const R dist = MULTI ? g_sqrt(d2) : R(0);
     R r = R(2) - d2 * d2;
     r = r > R(0) ? r : R(0);
     const bool oob = g_abs(s.px) > v.bound_xy || g_abs(s.py) > v.bound_xy || s.pz > R(2) ||
@@ -331,7 +333,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
       reward = srew[base];
     } else {
       reward = (float)r;
-      term = dist < R(1e-4);
+      term = d2 < R(1e-8);
       trunc = oob || sc >= v.trunc_sc;
     }
   }
