@@ -302,7 +302,9 @@ def main():
                      "alg_bytes_per_launch": alg},
     }
 
-    tr = pmc_traffic(E, args.precision)
+    grid_lanes = -(-sim.n_drones // sim.constants.drones_per_block) * 64   # launch geometry of the step kernel
+    result["roofline"]["grid_lanes"] = grid_lanes
+    tr = pmc_traffic(grid_lanes, args.precision)
     if tr is not None:
         result["roofline"]["traffic"] = tr[0]
         result["roofline"]["traffic_source"] = tr[1] + " (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate passes)"

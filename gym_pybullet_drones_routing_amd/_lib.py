@@ -75,7 +75,7 @@ class Constants(ctypes.Structure):
         "gravity", "hover_rpm", "max_rpm", "max_thrust", "max_xy_torque", "max_z_torque",
         "gnd_eff_h_clip", "pyb_timestep", "ctrl_timestep")] + [(n, ctypes.c_int) for n in (
             "pyb_steps_per_ctrl", "action_buffer_size", "obs_width", "act_width", "n_drones",
-            "trunc_step_counter")]
+            "trunc_step_counter", "drones_per_block")]
 
 
 _lib = None

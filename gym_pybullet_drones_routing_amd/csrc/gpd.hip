@@ -451,6 +451,7 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   K.obs_width = s->W;
   K.act_width = s->A;
   K.n_drones = s->N;
+  K.drones_per_block = s->tpb;
   {  // truncated iff step_counter / PYB_FREQ > EPISODE_LEN_SEC  (HoverAviary.py:114)
     long long sc = (long long)std::floor(C.episode_len_sec * C.pyb_freq);
     if (sc < 0) sc = 0;

@@ -119,6 +119,7 @@ typedef struct gpd_constants {
   double pyb_timestep, ctrl_timestep;
   int pyb_steps_per_ctrl, action_buffer_size, obs_width, act_width, n_drones;
   int trunc_step_counter;    /* smallest step_counter with step_counter/PYB_FREQ > EPISODE_LEN_SEC */
+  int drones_per_block;      /* drones per 64-lane block of the step kernel (launch geometry) */
 } gpd_constants;
 
 /* DSLPIDControl coefficients and constants (control/DSLPIDControl.py:37-60; GRAVITY and KF

@@ -61,5 +61,5 @@ def test_struct_sizes_match_header():
     # int + 19 doubles (8-aligned after the int) + 12 doubles
     assert ctypes.sizeof(_lib.DroneParams) == 8 + 19 * 8 + 12 * 8
     assert ctypes.sizeof(_lib.Config) == 9 * 4 + 4 + 8 + 8 + 8
-    assert ctypes.sizeof(_lib.Constants) == 9 * 8 + 6 * 4 + 0
+    assert ctypes.sizeof(_lib.Constants) == 9 * 8 + 7 * 4 + 4   # 7 ints + tail padding to 8
     assert ctypes.sizeof(_lib.PidParams) == (6 * 3 + 4 + 12 + 2) * 8
