@@ -107,7 +107,7 @@ struct gpd_sim {
   int E, D, N, A, W, nsub, ring_len, prec, tpb;
   long long npad;
   void* d_state = nullptr;
-  void* d_ctrl = nullptr;         // [9][npad] DSLPIDControl state (PID action types)
+  void* d_ctrl = nullptr;         // tiled [npad/64][9][64] DSLPIDControl state (PID action types)
   float* d_ring = nullptr;
   int2* d_ctr = nullptr;          // [E] {step_counter, ring head}
   void* d_init = nullptr;

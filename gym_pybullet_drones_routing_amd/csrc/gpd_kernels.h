@@ -1,8 +1,10 @@
 // gpd_kernels.h — the launch-level kernels of the batched DYN path (gfx950).
 //
 // HBM layout (owned by the sim):
-//   state  real [20][npad]   SoA: pos(3) quat_raw(4) vel(3) rpy_rates(3) ang_v(3) last_rpm(4)
-//   ring   float[L][npad*A]  action history ring (BaseRLAviary.action_buffer),
+//   state  real [npad/64][20][64]  tiled SoA: pos(3) quat_raw(4) vel(3) rpy_rates(3) ang_v(3)
+//                            last_rpm(4); each 64-drone tile keeps its 20 components contiguous
+//   ring   float[npad/64][L][64*A]  action history ring (BaseRLAviary.action_buffer), tiled the
+//                            same way,
 //                            L = ACTION_BUFFER_SIZE = ctrl_freq//2
 //   ctr    int2[E]           per-env {step_counter, ring head}: the head is the ring slot that
 //                            receives the env's next action.  All envs advance it in lockstep,
@@ -73,13 +75,13 @@ typedef __attribute__((address_space(1))) void* gbl_void_ptr;
 
 template <typename R>
 struct SimView {
-  R* state;               // [20][npad]
-  R* ctrl;                // [9][npad] DSLPIDControl state (PID action types only, else null)
-  float* ring;            // [ring_len][npad*A]
+  R* state;               // [npad/64][20][64]
+  R* ctrl;                // [npad/64][9][64] DSLPIDControl state (PID action types only, else null)
+  float* ring;            // [npad/64][ring_len][64*A]
   int2* ctr;              // [E] {step_counter, ring head}
   const R* init;          // [D][10]
   const R* target;        // [D][3]
-  long long npad;         // component stride of `state` (elements)
+  long long npad;         // drones rounded up to whole 64-drone tiles
   int N, D, A, W, tpb, ring_len;
   int task, autoreset, trunc_sc;
   int wt;                 // write-through stores: bit 0 obs/terminal rows, bit 1 state (see store_wt)
@@ -97,18 +99,29 @@ struct StepIO {
   float* terminal_obs;    // [N][W] or null
 };
 
+// Tiled SoA: component k of drone n lives at tile(n) * C*64 + k*64 + lane(n).  Every wave
+// load / store of one component is still 64 consecutive elements, while each 64-drone tile's
+// state (and history) is one contiguous stretch of HBM: a block streams a few large runs
+// instead of one 512-B run from each of 20 (+14) widely separated arrays.
+__host__ __device__ __forceinline__ long long tidx(long long n, int k, int C) {
+  return (n >> 6) * (64LL * C) + k * 64 + (n & 63);
+}
+// ring slot `slot` of drone n (units of float, A floats per drone)
+__host__ __device__ __forceinline__ long long ridx(long long n, int slot, int L, int A) {
+  return ((n >> 6) * L + slot) * (64LL * A) + (n & 63) * A;
+}
+
 // Only what the dynamics reads: ang_v is write-only, last_clipped_action is read only by drag.
 template <typename R>
 __device__ __forceinline__ void load_drone(const SimView<R>& v, long long n, Drone<R>& s, R last[4], bool need_last) {
-  const R* st = v.state;
-  const long long p = v.npad;
-  s.px = st[0 * p + n]; s.py = st[1 * p + n]; s.pz = st[2 * p + n];
-  s.qx = st[3 * p + n]; s.qy = st[4 * p + n]; s.qz = st[5 * p + n]; s.qw = st[6 * p + n];
-  s.vx = st[7 * p + n]; s.vy = st[8 * p + n]; s.vz = st[9 * p + n];
-  s.wx = st[10 * p + n]; s.wy = st[11 * p + n]; s.wz = st[12 * p + n];
+  const R* st = v.state + tidx(n, 0, kStateComps);
+  s.px = st[0 * 64]; s.py = st[1 * 64]; s.pz = st[2 * 64];
+  s.qx = st[3 * 64]; s.qy = st[4 * 64]; s.qz = st[5 * 64]; s.qw = st[6 * 64];
+  s.vx = st[7 * 64]; s.vy = st[8 * 64]; s.vz = st[9 * 64];
+  s.wx = st[10 * 64]; s.wy = st[11 * 64]; s.wz = st[12 * 64];
   s.ax = s.ay = s.az = R(0);
   if (need_last) {
-    last[0] = st[16 * p + n]; last[1] = st[17 * p + n]; last[2] = st[18 * p + n]; last[3] = st[19 * p + n];
+    last[0] = st[16 * 64]; last[1] = st[17 * 64]; last[2] = st[18 * 64]; last[3] = st[19 * 64];
   } else {
     last[0] = last[1] = last[2] = last[3] = R(0);
   }
@@ -117,32 +130,30 @@ __device__ __forceinline__ void load_drone(const SimView<R>& v, long long n, Dro
 template <typename R>
 __device__ __forceinline__ void load_drone_full(const SimView<R>& v, long long n, Drone<R>& s, R last[4]) {
   load_drone(v, n, s, last, true);
-  const long long p = v.npad;
-  s.ax = v.state[13 * p + n]; s.ay = v.state[14 * p + n]; s.az = v.state[15 * p + n];
+  const R* st = v.state + tidx(n, 0, kStateComps);
+  s.ax = st[13 * 64]; s.ay = st[14 * 64]; s.az = st[15 * 64];
 }
 
 template <typename R>
 __device__ __forceinline__ void store_drone_wt(const SimView<R>& v, long long n, const Drone<R>& s, const R last[4]) {
   const __amdgpu_buffer_rsrc_t r =
       __builtin_amdgcn_make_buffer_rsrc(v.state, 0, (int)(kStateComps * v.npad * (long long)sizeof(R)), 0x00020000);
-  const int p = (int)(v.npad * sizeof(R));
-  int o = (int)(n * sizeof(R));
+  int o = (int)(tidx(n, 0, kStateComps) * sizeof(R));
   const R vals[20] = {s.px, s.py, s.pz, s.qx, s.qy, s.qz, s.qw, s.vx, s.vy, s.vz,
                       s.wx, s.wy, s.wz, s.ax, s.ay, s.az, last[0], last[1], last[2], last[3]};
 #pragma unroll
-  for (int k = 0; k < 20; ++k, o += p) store_wt(r, o, vals[k]);
+  for (int k = 0; k < 20; ++k, o += 64 * (int)sizeof(R)) store_wt(r, o, vals[k]);
 }
 
 template <typename R>
 __device__ __forceinline__ void store_drone(const SimView<R>& v, long long n, const Drone<R>& s, const R last[4]) {
-  R* st = v.state;
-  const long long p = v.npad;
-  st[0 * p + n] = s.px; st[1 * p + n] = s.py; st[2 * p + n] = s.pz;
-  st[3 * p + n] = s.qx; st[4 * p + n] = s.qy; st[5 * p + n] = s.qz; st[6 * p + n] = s.qw;
-  st[7 * p + n] = s.vx; st[8 * p + n] = s.vy; st[9 * p + n] = s.vz;
-  st[10 * p + n] = s.wx; st[11 * p + n] = s.wy; st[12 * p + n] = s.wz;
-  st[13 * p + n] = s.ax; st[14 * p + n] = s.ay; st[15 * p + n] = s.az;
-  st[16 * p + n] = last[0]; st[17 * p + n] = last[1]; st[18 * p + n] = last[2]; st[19 * p + n] = last[3];
+  R* st = v.state + tidx(n, 0, kStateComps);
+  st[0 * 64] = s.px; st[1 * 64] = s.py; st[2 * 64] = s.pz;
+  st[3 * 64] = s.qx; st[4 * 64] = s.qy; st[5 * 64] = s.qz; st[6 * 64] = s.qw;
+  st[7 * 64] = s.vx; st[8 * 64] = s.vy; st[9 * 64] = s.vz;
+  st[10 * 64] = s.wx; st[11 * 64] = s.wy; st[12 * 64] = s.wz;
+  st[13 * 64] = s.ax; st[14 * 64] = s.ay; st[15 * 64] = s.az;
+  st[16 * 64] = last[0]; st[17 * 64] = last[1]; st[18 * 64] = last[2]; st[19 * 64] = last[3];
 }
 
 // One physics substep of every drone of the block, including the readback that precedes it
@@ -240,7 +251,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
     // PID / VEL / ONE_D_PID (BaseRLAviary.py:193-235): DSLPIDControl on the state vector of
     // the last readback (_getDroneStateVector :559-561)
 #pragma unroll
-    for (int k = 0; k < 9; ++k) cs[k] = v.ctrl[k * v.npad + nn];
+    for (int k = 0; k < 9; ++k) cs[k] = v.ctrl[tidx(nn, k, 9)];
     R qn[4], Rm[9], rpy[3];
     readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
     quat_to_euler(qn, rpy[0], rpy[1], rpy[2]);
@@ -251,7 +262,6 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
   }
 
   const int nh = v.ring_len - 1;
-  const long long slot_stride = v.npad * A;
   // history ring -> obs tile: the L-1 oldest actions (LDS-DMA).  Issued after the first
   // substep: hipcc waits vmcnt(0) at the next use of an ordinary load while an LDS-DMA is in
   // flight, so issuing it before the state/action loads were consumed would put the DMA round
@@ -260,7 +270,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
     for (int k = 0; k < nh; ++k) {
       int slot = head + 1 + k;
       slot -= slot >= v.ring_len ? v.ring_len : 0;
-      const float* src = v.ring + (long long)slot * slot_stride + nn * A;
+      const float* src = v.ring + ridx(nn, slot, v.ring_len, A);
       if (A == 4) {
         __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tile4 + (3 + k) * kPad), 16, 0, 0);
       } else {
@@ -348,7 +358,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
   // current action into the ring (deque.append); issued after the wait above so that the wait
   // does not also cover this store's write acknowledgement.  The DMA never reads slot `head`.
   if (active) {
-    float* ring_cur = v.ring + (long long)head * slot_stride + n * A;
+    float* ring_cur = v.ring + ridx(n, head, v.ring_len, A);
     if (A == 4) *reinterpret_cast<float4*>(ring_cur) = make_float4(a[0], a[1], a[2], a[3]);
     else
 #pragma unroll
@@ -491,7 +501,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
   else store_drone(v, n, s, last);
   if (act_is_pid(ACT)) {
 #pragma unroll
-    for (int k = 0; k < 9; ++k) v.ctrl[k * v.npad + n] = cs[k];
+    for (int k = 0; k < 9; ++k) v.ctrl[tidx(n, k, 9)] = cs[k];
   }
   if (d == 0) {
     io.reward[e] = reward;
@@ -574,11 +584,10 @@ __global__ __launch_bounds__(256) void reset_kernel(SimView<R> v, const uint8_t*
     orow[3] = (float)ini[7]; orow[4] = (float)ini[8]; orow[5] = (float)ini[9];
     for (int k = 6; k < 12; ++k) orow[k] = 0.0f;
     const int A = v.A;
-    const long long slot_stride = v.npad * A;
     for (int k = 0; k < v.ring_len; ++k) {   // oldest first: the slot about to be overwritten
       int slot = head + k;
       slot -= slot >= v.ring_len ? v.ring_len : 0;
-      const float* src = v.ring + (long long)slot * slot_stride + n * A;
+      const float* src = v.ring + ridx(n, slot, v.ring_len, A);
       for (int j = 0; j < A; ++j) orow[12 + k * A + j] = src[j];
     }
   }
@@ -591,8 +600,7 @@ __global__ __launch_bounds__(256) void state20_kernel(SimView<R> v, R* __restric
   if (n >= v.N) return;
   R* o = out + n * 20;
   if (raw) {
-    const long long p = v.npad;
-    for (int k = 0; k < 20; ++k) o[k] = v.state[k * p + n];
+    for (int k = 0; k < 20; ++k) o[k] = v.state[tidx(n, k, kStateComps)];
     return;
   }
   Drone<R> s;
@@ -613,24 +621,25 @@ template <typename R>
 __global__ __launch_bounds__(256) void set_raw_kernel(SimView<R> v, const R* __restrict__ in) {
   const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= v.N) return;
-  const long long p = v.npad;
-  for (int k = 0; k < 20; ++k) v.state[k * p + n] = in[n * 20 + k];
+  for (int k = 0; k < 20; ++k) v.state[tidx(n, k, kStateComps)] = in[n * 20 + k];
 }
 
-// [comps][npad] SoA <-> [N][comps] rows (controller state access)
+// tiled SoA <-> [N][comps] rows (controller state access)
 template <typename R>
 __global__ __launch_bounds__(256) void soa_to_rows_kernel(const R* __restrict__ soa, long long npad, int comps, int N,
                                                           R* __restrict__ out) {
+  (void)npad;
   const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
-  for (int k = 0; k < comps; ++k) out[n * comps + k] = soa[k * npad + n];
+  for (int k = 0; k < comps; ++k) out[n * comps + k] = soa[tidx(n, k, comps)];
 }
 template <typename R>
 __global__ __launch_bounds__(256) void rows_to_soa_kernel(const R* __restrict__ in, long long npad, int comps, int N,
                                                           R* __restrict__ soa) {
+  (void)npad;
   const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
-  for (int k = 0; k < comps; ++k) soa[k * npad + n] = in[n * comps + k];
+  for (int k = 0; k < comps; ++k) soa[tidx(n, k, comps)] = in[n * comps + k];
 }
 
 }  // namespace gpd
