@@ -63,3 +63,15 @@ def test_struct_sizes_match_header():
     assert ctypes.sizeof(_lib.Config) == 9 * 4 + 4 + 8 + 8 + 8
     assert ctypes.sizeof(_lib.Constants) == 9 * 8 + 7 * 4 + 4   # 7 ints + tail padding to 8
     assert ctypes.sizeof(_lib.PidParams) == (6 * 3 + 4 + 12 + 2) * 8
+
+
+def test_abi_version_consistent():
+    """include/gpd.h, the ctypes binding and the built library agree on GPD_ABI_VERSION (and
+    __graft_entry__.build() checks against the binding, not a literal)."""
+    from gym_pybullet_drones_routing_amd import _lib
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "gpd.h")).read()
+    m = re.search(r"#define GPD_ABI_VERSION (\d+)", hdr)
+    assert m and int(m.group(1)) == _lib.GPD_ABI_VERSION
+    assert _lib.load().gpd_abi_version() == _lib.GPD_ABI_VERSION
+    entry = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "__graft_entry__.py")).read()
+    assert "gpd_abi_version() == _lib.GPD_ABI_VERSION" in entry
