@@ -215,6 +215,37 @@ def other_configs(device, precision, act):
     return out
 
 
+def raw_integrator(device, precision, n_drones=1 << 20, n_sub=32):
+    """SURVEY §8(d) raw-integrator mode: gpd_integrate with the RPMs streamed per substep
+    ([n_sub][N][4] real), state in registers for all n_sub substeps, no trajectory; algorithmic
+    bytes = n_sub*N*4r (RPMs) + N*17r (state + last RPM read) + N*20r (state written)."""
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+    sim = BatchedAviarySim(n_envs=n_drones, task="none", precision=precision, autoreset=False, device=device)
+    r = 8 if precision == "f64" else 4
+    dt = torch.float64 if precision == "f64" else torch.float32
+    rpm = (14468.43 * (1 + 0.05 * (torch.rand((n_sub, n_drones, 4), device=device) * 2 - 1))).to(dt).contiguous()
+    for _ in range(2):
+        sim.integrate(rpm)
+    stream = torch.cuda.current_stream(device)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    torch.cuda.synchronize(device)
+    ev0.record(stream)
+    for _ in range(reps):
+        sim.integrate(rpm)
+    ev1.record(stream)
+    torch.cuda.synchronize(device)
+    us = 1000.0 * ev0.elapsed_time(ev1) / reps
+    alg = n_sub * n_drones * 4 * r + n_drones * 17 * r + n_drones * 20 * r
+    sim.close()
+    del rpm
+    torch.cuda.empty_cache()
+    return {"mode": f"gpd_integrate, {n_sub} substeps per launch, RPMs streamed from HBM, no trajectory",
+            "n_drones": n_drones, "kernel_us": us, "value": n_drones * n_sub / (us * 1e-6), "unit": "drone*dt/s",
+            "achieved_GBps": alg / (us * 1e-6) / 1e9, "frac": alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS,
+            "alg_bytes_per_drone_dt": (alg / (n_drones * n_sub))}
+
+
 def make_pool(E, A, device, seed, pool=64):
     g = torch.Generator(device=device)
     g.manual_seed(seed)
@@ -347,6 +378,7 @@ def main():
         with warnings.catch_warnings():
             warnings.simplefilter("ignore")
             result["other_configs"] = other_configs(device, args.precision, args.act)
+        result["raw_integrator"] = raw_integrator(device, args.precision)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.act)

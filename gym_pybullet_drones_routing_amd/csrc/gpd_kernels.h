@@ -531,10 +531,19 @@ __global__ __launch_bounds__(kWave) void integrate_kernel(SimView<R> v, const Co
   load_drone(v, nn, s, last, true);
   const long long N = v.N;
   const DynK<R> dk = dyn_consts(c);
+  // RPMs of substep t+1 are loaded while substep t integrates (one load round trip per launch
+  // instead of one per substep)
+  R nxt[4];
+  {
+    const R* src = rpm_in + nn * 4;
+    nxt[0] = src[0]; nxt[1] = src[1]; nxt[2] = src[2]; nxt[3] = src[3];
+  }
   for (int t = 0; t < n_sub; ++t) {
-    R rpm[4];
-    const R* src = rpm_in + ((long long)t * N + nn) * 4;
-    rpm[0] = src[0]; rpm[1] = src[1]; rpm[2] = src[2]; rpm[3] = src[3];
+    R rpm[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
+    if (t + 1 < n_sub) {
+      const R* src = rpm_in + ((long long)(t + 1) * N + nn) * 4;
+      nxt[0] = src[0]; nxt[1] = src[1]; nxt[2] = src[2]; nxt[3] = src[3];
+    }
     R W[4];
     rpm_wrench<R, false>(rpm, dk, c, W);
     substep_block<R, MULTI, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D);
