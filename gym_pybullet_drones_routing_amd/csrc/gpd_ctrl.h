@@ -13,7 +13,7 @@
 // before using it.  That round trip is the identity on rotation matrices (also at gimbal lock,
 // where scipy zeroes the third angle and folds it into the first), and the angles themselves
 // are only returned to the caller as a yaw error that BaseRLAviary discards, so the matrix is
-// used directly; tests/test_gpu_pid.py bounds the difference against scipy's round trip.
+// used directly; tests/test_oracle_pid.py bounds the difference against scipy's round trip.
 #pragma once
 #include "gpd_device.h"
 
@@ -36,7 +36,8 @@ __device__ __forceinline__ R np_clip(R x, R lo, R hi) {
 // DSLPIDControl.computeControl for one drone.  cs = {integral_pos_e[3], integral_rpy_e[3],
 // last_rpy[3]} (updated in place), Rm = getMatrixFromQuaternion(cur_quat) row-major,
 // rpy = getEulerFromQuaternion(cur_quat).  Evaluated with FP contraction off, like numpy.
-template <typename R>
+// YAW0: the target yaw is the default 0 (PID, ONE_D_PID), so target_x_c = (1, 0, 0) exactly.
+template <typename R, bool YAW0 = false>
 __device__ __forceinline__ void dsl_pid(const PidConsts<R>& k, const R pos[3], const R Rm[9], const R rpy[3],
                                         const R vel[3], const R tpos[3], R tyaw, const R tvel[3], R cs[9],
                                         R rpm[4]) {
@@ -58,7 +59,7 @@ __device__ __forceinline__ void dsl_pid(const PidConsts<R>& k, const R pos[3], c
   const R thrust = (g_sqrt(scalar_thrust / (R(4) * k.kf)) - k.pwm2rpm_const) / k.pwm2rpm_scale;
   const R ntt = g_sqrt((tt[0] * tt[0] + tt[1] * tt[1]) + tt[2] * tt[2]);
   const R z0 = tt[0] / ntt, z1 = tt[1] / ntt, z2 = tt[2] / ntt;   // target_z_ax
-  const R xc0 = g_cos(tyaw), xc1 = g_sin(tyaw);                    // target_x_c (z = 0)
+  const R xc0 = YAW0 ? R(1) : g_cos(tyaw), xc1 = YAW0 ? R(0) : g_sin(tyaw);   // target_x_c (z = 0)
   const R c0 = z1 * R(0) - z2 * xc1, c1 = z2 * xc0 - z0 * R(0), c2 = z0 * xc1 - z1 * xc0;
   const R nc = g_sqrt((c0 * c0 + c1 * c1) + c2 * c2);
   const R y0 = c0 / nc, y1 = c1 / nc, y2 = c2 / nc;               // target_y_ax

@@ -258,7 +258,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
     const R pos[3] = {s.px, s.py, s.pz}, vel[3] = {s.vx, s.vy, s.vz};
     R tpos[3], tvel[3], tyaw;
     pid_targets<R, ACT>(c.pid, a, pos, rpy, tpos, tyaw, tvel);
-    dsl_pid(c.pid, pos, Rm, rpy, vel, tpos, tyaw, tvel, cs, rpm);
+    dsl_pid<R, ACT != ACT_VEL>(c.pid, pos, Rm, rpy, vel, tpos, tyaw, tvel, cs, rpm);
   }
 
   const int nh = v.ring_len - 1;
