@@ -116,6 +116,7 @@ struct gpd_sim {
   int tile_bytes = 0;             // dynamic LDS of the step kernel
   int wt = 0;                     // SimView::wt (write-through store policy)
   int nc_magic = 0;               // SimView::nc_magic
+  DwPairs dw_pairs{0, 0};         // SimView::dw_pairs
   double bound_xy;
   std::vector<double> init_tmpl;  // [D][10]
   std::vector<double> target;     // [D][3]
@@ -191,6 +192,7 @@ SimView<R> make_view(const gpd_sim* s) {
   v.trunc_sc = s->K.trunc_step_counter;
   v.wt = s->wt;
   v.nc_magic = s->nc_magic;
+  v.dw_pairs = s->dw_pairs;
   v.bound_xy = (R)s->bound_xy;
   return v;
 }
@@ -404,6 +406,16 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     s->tpb = want;
   }
   s->npad = ((long long)s->N + 63) / 64 * 64;
+  {
+    // downwash pairs over idle lanes: only for thin blocks whose pairs fit the LDS buffer
+    const int D = s->D, n = s->tpb * D;
+    if (D > 1 && (C.physics_flags & GPD_F_DW) && s->tpb < kWave && n <= kPairMax) {
+      const int m = ((1 << 20) + D - 1) / D;
+      bool ok = true;
+      for (int p = 0; p < n && ok; ++p) ok = ((p * m) >> 20) == p / D;
+      if (ok) s->dw_pairs = DwPairs{n, m};
+    }
+  }
   {
     // write-through (sc1) stores for the obs rows (bit 0) and the state (bit 1), default both:
     // measured on one MI355X, 4096 envs 8.60 -> 8.37 us/step and 65536 envs 15.3 -> 13.7 us,

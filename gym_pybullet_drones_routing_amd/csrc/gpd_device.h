@@ -487,25 +487,35 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R 
 // Summed downwash on drone (px,py,pz) from the env's D drones whose positions sit in LDS
 // (BaseAviary._downwash :798-811).  A wave-wide ballot skips the α/β/exp block whenever no
 // lane of the wave has an active pair (Δz > 0 ∧ Δxy < 10) for neighbour j.
+// The downwash force on drone (px,py,pz) from drone (qx,qy,qz) (:798-811), 0 when the pair is
+// culled (delta_z <= 0 or delta_xy >= 10).  alpha = DW1 (PROP_RADIUS/(4 dz))^2,
+// beta = DW2 dz + DW3, f = -alpha exp(-0.5 (dxy/beta)^2); |dxy|^2 needs no square root, and
+// beta = 0 keeps numpy's IEEE result (dxy^2/0 = inf -> exp(-inf) = 0; 0/0 = nan at dxy = 0).
+// The ballot skips the exp block for a whole wave when no lane has an active pair.
+template <typename R>
+__device__ __forceinline__ R dw_pair(R px, R py, R pz, R qx, R qy, R qz, const Consts<R>& c) {
+  const R dz = qz - pz;
+  const R ddx = qx - px, ddy = qy - py;
+  const R dxy2 = ddx * ddx + ddy * ddy;
+  const bool hit = (dz > R(0)) && (dxy2 < R(100));       // delta_z > 0 and delta_xy < 10
+  R f = R(0);
+  if (__ballot(hit) != 0ull) {
+    if (hit) {
+      const R alpha = c.dwk1 / (dz * dz);
+      const R beta = c.dw2 * dz + c.dw3;
+      f = -alpha * g_exp(R(-0.5) * (dxy2 / (beta * beta)));
+    }
+  }
+  return f;
+}
+
+// Summed downwash on one drone from its env's D drones (positions in LDS), neighbours in the
+// reference's order j = 0..D-1 (culled pairs add +0, which changes no sum).
 template <typename R>
 __device__ __forceinline__ R downwash_sum(R px, R py, R pz, const R* sx, const R* sy, const R* sz,
                                           int base, int D, const Consts<R>& c) {
   R total = R(0);
-  for (int j = 0; j < D; ++j) {
-    const R dz = sz[base + j] - pz;
-    const R ddx = sx[base + j] - px, ddy = sy[base + j] - py;
-    const R dxy2 = ddx * ddx + ddy * ddy;                 // |dxy|^2: the force needs no square root
-    const bool hit = (dz > R(0)) && (dxy2 < R(100));      // delta_z > 0 and delta_xy < 10
-    if (__ballot(hit) != 0ull) {
-      if (hit) {
-        // alpha = DW1 (PROP_RADIUS/(4 dz))^2, beta = DW2 dz + DW3, f = -alpha exp(-0.5 (dxy/beta)^2);
-        // beta = 0 keeps numpy's IEEE result: dxy^2/0 = inf -> exp(-inf) = 0 (0/0 = nan at dxy = 0)
-        const R alpha = c.dwk1 / (dz * dz);
-        const R beta = c.dw2 * dz + c.dw3;
-        total = total + (-alpha * g_exp(R(-0.5) * (dxy2 / (beta * beta))));
-      }
-    }
-  }
+  for (int j = 0; j < D; ++j) total = total + dw_pair(px, py, pz, sx[base + j], sy[base + j], sz[base + j], c);
   return total;
 }
 

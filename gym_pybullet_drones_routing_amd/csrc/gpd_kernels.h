@@ -73,6 +73,15 @@ __device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, int off, doub
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 typedef __attribute__((address_space(1))) void* gbl_void_ptr;
 
+// Downwash work split for blocks with idle lanes: with n > 0, the block's n = tpb*D drone
+// pairs are spread over all 64 lanes (pair k: drone k/D of the block, neighbour k%D of its
+// env), each force goes to LDS, and the drone's lane sums its D forces in the reference's
+// order.  k/D = (k*dmagic) >> 20 (host-checked for k < n).
+struct DwPairs {
+  int n, dmagic;
+};
+constexpr int kPairMax = 256;
+
 template <typename R>
 struct SimView {
   R* state;               // [npad/64][20][64]
@@ -86,6 +95,7 @@ struct SimView {
   int task, autoreset, trunc_sc;
   int wt;                 // write-through stores: bit 0 obs/terminal rows, bit 1 state (see store_wt)
   int nc_magic;           // floor(t / NC) == (t * nc_magic) >> 16 for 0 <= t < 64 (host-checked)
+  DwPairs dw_pairs;       // downwash pair split (n = 0: one lane per drone loops over its env)
   R bound_xy;             // 1.5 (Hover) or 2.0 (MultiHover)
 };
 
@@ -161,7 +171,7 @@ __device__ __forceinline__ void store_drone(const SimView<R>& v, long long n, co
 template <typename R, bool MULTI, bool FAST, bool ANGV = true>
 __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const R W[4], const R last[4],
                                               const Consts<R>& c, const DynK<R>& k, R* sx, R* sy, R* sz, int tid,
-                                              int base, int D) {
+                                              int base, int D, DwPairs pairs = DwPairs{0, 0}, R* spair = nullptr) {
   R qn[4], Rm[9];
   readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);  // :346-347 -> :517, :836
   bool up = true;
@@ -170,7 +180,19 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
   if (MULTI && !FAST && (c.flags & F_DW)) {
     sx[tid] = s.px; sy[tid] = s.py; sz[tid] = s.pz;
     __syncthreads();
-    dw = downwash_sum(s.px, s.py, s.pz, sx, sy, sz, base, D, c);
+    if (pairs.n > 0) {
+      for (int p = tid; p < pairs.n; p += kWave) {
+        const int i = (p * pairs.dmagic) >> 20;          // drone of the block
+        const int j = p - i * D;                          // neighbour within its env
+        const int ib = ((i * pairs.dmagic) >> 20) * D;   // the env's first drone in the block
+        spair[p] = dw_pair(sx[i], sy[i], sz[i], sx[ib + j], sy[ib + j], sz[ib + j], c);
+      }
+      __syncthreads();
+      if (tid * D < pairs.n)
+        for (int j = 0; j < D; ++j) dw = dw + spair[tid * D + j];
+    } else {
+      dw = downwash_sum(s.px, s.py, s.pz, sx, sy, sz, base, D, c);
+    }
     __syncthreads();
   }
   dyn_substep<R, FAST, ANGV>(s, qn, Rm, up, rpm, W, last, dw, c, k);
@@ -202,6 +224,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
   __shared__ R sx[MULTI ? 2 * kWave : 1], sy[MULTI ? 2 * kWave : 1], sz[MULTI ? 2 * kWave : 1];
   __shared__ float srew[MULTI ? 2 * kWave : 1], sdist[MULTI ? 2 * kWave : 1];
   __shared__ int sflag[MULTI ? 2 * kWave : 1];
+  __shared__ R spair[MULTI ? kPairMax : 1];
   GPD_STAMP(0);
   const Consts<R>& c = *cp;
   const int tid = threadIdx.x;
@@ -286,7 +309,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
   rpm_wrench<R, FAST>(rpm, dk, c, W);
   // substeps 1..nsub-1 skip the (write-only) world ang_v; the last one produces it
   for (int it = 0; it < c.nsub - 1; ++it) {
-    substep_block<R, MULTI, FAST, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D);
+    substep_block<R, MULTI, FAST, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
     if (it == 0) {
@@ -294,7 +317,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
       history_dma();
     }
   }
-  substep_block<R, MULTI, FAST, true>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D);
+  substep_block<R, MULTI, FAST, true>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
 #pragma unroll
   for (int k = 0; k < 4; ++k) last[k] = rpm[k];
   if (c.nsub == 1) history_dma();
