@@ -99,7 +99,7 @@ struct DynK {
   R dt, inv_m, gravity, jx, jy, jz, ijx, ijy, ijz, hdt, hdt2;
   R kf, km, L, Ls2;        // propeller wrench (rpm_wrench)
   float hover_f32;         // action -> RPM
-  int model;
+  int model, flags;
 };
 template <typename R>
 __device__ __forceinline__ R vpin(R x) {
@@ -114,12 +114,13 @@ __device__ __forceinline__ DynK<R> dyn_consts(const Consts<R>& c) {
   k.ijx = c.ijx; k.ijy = c.ijy; k.ijz = c.ijz;
   k.hdt = c.hdt; k.hdt2 = c.hdt2;
   k.kf = c.kf; k.km = c.km; k.L = c.L; k.Ls2 = c.Ls2; k.hover_f32 = c.hover_f32; k.model = c.model;
+  k.flags = c.flags;
   // one statement for all of them: hipcc issues the scalar loads of every constant-block line
   // back to back and waits once (K$ misses in parallel), instead of a load + wait pair per use
   // behind each model / flag branch
   asm volatile("" : "+v"(k.dt), "+v"(k.inv_m), "+v"(k.gravity), "+v"(k.jx), "+v"(k.jy), "+v"(k.jz),
                "+v"(k.ijx), "+v"(k.ijy), "+v"(k.ijz), "+v"(k.hdt), "+v"(k.hdt2), "+v"(k.kf), "+v"(k.km),
-               "+v"(k.L), "+v"(k.Ls2), "+v"(k.hover_f32), "+s"(k.model));
+               "+v"(k.L), "+v"(k.Ls2), "+v"(k.hover_f32), "+s"(k.model), "+s"(k.flags));
   return k;
 }
 
@@ -303,8 +304,7 @@ __device__ __forceinline__ bool tilted_beyond(const AttitudeArgs<R>& t, R sin_li
 // |roll| < pi/2 and |pitch| < pi/2 (the _groundEffect condition, BaseAviary.py:742)
 template <typename R>
 __device__ __forceinline__ bool upright(const AttitudeArgs<R>& t) {
-  if (t.gimbal) return false;
-  return t.b > R(0) || (t.b == R(0) && t.a == R(0) && !signbit(t.b));
+  return !t.gimbal && (t.b > R(0) || (t.b == R(0) && t.a == R(0) && !signbit(t.b)));
 }
 // float32 Euler angles for the float32 observation (the reference casts its float64 angles to
 // float32, BaseRLAviary.py:315); evaluated in float32 from the double-precision arguments.
@@ -360,7 +360,7 @@ __device__ __forceinline__ void rpm_wrench(const R rpm[4], const DynK<R>& k, con
   }
   W[0] = ((f[0] + f[1]) + f[2]) + f[3];                // np.sum(forces) :839
   W[3] = ((-zt[0] + zt[1]) - zt[2]) + zt[3];           // :845
-  if (!FAST && (c.flags & F_GEOM)) {                   // _physics: forces at prop links :698-705
+  if (!FAST && (k.flags & F_GEOM)) {                   // _physics: forces at prop links :698-705
     R tx = R(0), ty = R(0);
 #pragma unroll
     for (int m = 0; m < 4; ++m) { tx = tx + c.ry[m] * f[m]; ty = ty - c.rx[m] * f[m]; }
@@ -378,12 +378,13 @@ __device__ __forceinline__ void rpm_wrench(const R rpm[4], const DynK<R>& k, con
 // (_groundEffect :732-750) at the current pose.
 template <typename R, bool FAST>
 __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bool gnd_upright, const R rpm[4],
-                                            const R W[4], const Consts<R>& c, R& fz_out, R& tx_out, R& ty_out,
-                                            R& tz_out) {
+                                            const R W[4], const Consts<R>& c, const DynK<R>& kk, R& fz_out, R& tx_out,
+                                            R& ty_out, R& tz_out) {
 #pragma clang fp contract(off)
   R fz = W[0], tx = W[1], ty = W[2];
-  if (!FAST && (c.flags & F_GND) && gnd_upright) {
-    // prop COM heights via forward kinematics, clipped, +z link force at each prop
+  if (!FAST && (kk.flags & F_GND)) {
+    // prop COM heights via forward kinematics, clipped, +z link force at each prop; applied only
+    // while upright (a select, not a branch)
     R g[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -392,12 +393,13 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
       const R qq = c.prop_r / (R(4) * h);
       g[k] = ((rpm[k] * rpm[k]) * c.kf * c.ge_coeff) * (qq * qq);
     }
-    fz = fz + (((g[0] + g[1]) + g[2]) + g[3]);
+    const R gz = ((g[0] + g[1]) + g[2]) + g[3];
     R gx = R(0), gy = R(0);
 #pragma unroll
     for (int k = 0; k < 4; ++k) { gx = gx + c.ry[k] * g[k]; gy = gy - c.rx[k] * g[k]; }
-    tx = tx + gx;
-    ty = ty + gy;
+    fz = gnd_upright ? fz + gz : fz;
+    tx = gnd_upright ? tx + gx : tx;
+    ty = gnd_upright ? ty + gy : ty;
   }
   fz_out = fz;
   tx_out = tx;
@@ -421,11 +423,11 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R 
                                             const R rpm[4], const R W[4], const R last[4], R dwsum,
                                             const Consts<R>& c, const DynK<R>& k) {
   R fz, tx, ty, tz;
-  body_wrench<R, FAST>(s, Rm, gnd_upright, rpm, W, c, fz, tx, ty, tz);
-  if (!FAST && (c.flags & F_DW)) fz = fz + dwsum;      // _downwash :801-811 (body z)
+  body_wrench<R, FAST>(s, Rm, gnd_upright, rpm, W, c, k, fz, tx, ty, tz);
+  if (!FAST && (k.flags & F_DW)) fz = fz + dwsum;      // _downwash :801-811 (body z)
   // R·(0,0,fz) - (0,0,GRAVITY) [+ drag]                 :839-841
   R Fx = Rm[2] * fz, Fy = Rm[5] * fz, Fz = Rm[8] * fz;
-  if (!FAST && (c.flags & F_DRAG)) {                   // _drag :773-774 with last_clipped_action
+  if (!FAST && (k.flags & F_DRAG)) {                   // _drag :773-774 with last_clipped_action
     const R S = ((last[0] * c.rpm2rad + last[1] * c.rpm2rad) + last[2] * c.rpm2rad) + last[3] * c.rpm2rad;
     Fx = Fx + (-c.drag_xy * S) * s.vx;
     Fy = Fy + (-c.drag_xy * S) * s.vy;

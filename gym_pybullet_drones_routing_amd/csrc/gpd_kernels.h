@@ -175,9 +175,9 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
   R qn[4], Rm[9];
   readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);  // :346-347 -> :517, :836
   bool up = true;
-  if (!FAST && (c.flags & F_GND)) up = upright(attitude_args(qn));  // |self.rpy[0,1]| < pi/2, :742
+  if (!FAST && (k.flags & F_GND)) up = upright(attitude_args(qn));  // |self.rpy[0,1]| < pi/2, :742
   R dw = R(0);
-  if (MULTI && !FAST && (c.flags & F_DW)) {
+  if (MULTI && !FAST && (k.flags & F_DW)) {
     sx[tid] = s.px; sy[tid] = s.py; sz[tid] = s.pz;
     __syncthreads();
     if (pairs.n > 0) {
