@@ -4,8 +4,7 @@
 //   state  real [npad/64][20][64]  tiled SoA: pos(3) quat_raw(4) vel(3) rpy_rates(3) ang_v(3)
 //                            last_rpm(4); each 64-drone tile keeps its 20 components contiguous
 //   ring   float[npad/64][L][64*A]  action history ring (BaseRLAviary.action_buffer), tiled the
-//                            same way,
-//                            L = ACTION_BUFFER_SIZE = ctrl_freq//2
+//                            same way, L = ACTION_BUFFER_SIZE = ctrl_freq//2
 //   ctr    int2[E]           per-env {step_counter, ring head}: the head is the ring slot that
 //                            receives the env's next action.  All envs advance it in lockstep,
 //                            but keeping it per env (instead of a host-side launch argument)
@@ -13,8 +12,9 @@
 //   init   real [D][10]      per-drone reset template: pos(3) quat_raw(4) rpy(3)
 //   target real [D][3]       task target positions
 //   consts Consts<real>      model constants, read through a uniform pointer
-// One lane = one drone; one 64-lane block (one wave) holds floor(64/D) whole envs so that the
-// per-env exchange (downwash positions, reward/done reduction) stays inside a block.
+// One lane = one drone; one 64-lane block (one wave) holds whole envs (up to floor(64/D); fewer
+// "thin" blocks when there are too few drones to give every CU a wave) so that the per-env
+// exchange (downwash positions, reward/done reduction) stays inside a block.
 //
 // Observation rows are [E][D][W] row-major (W = 12 + L*A, the Gym layout).  A lane's row is W
 // floats, so writing rows straight from registers would scatter 16-byte pieces over 64
@@ -22,9 +22,10 @@
 // LDS tile stored column-major (tile[col][lane], one pad element per column so that the
 // transposed reads are bank-conflict free):
 //   * the L-1 history columns are DMA'd from the ring straight into the tile with
-//     global_load_lds at kernel start, so their HBM latency hides under the physics;
+//     global_load_lds after the first substep, so their HBM latency hides under the physics;
 //   * the 12 state columns and the current action are written from registers at the end;
-//   * the tile is then streamed out with fully coalesced 16-byte (A=4) / 4-byte (A=1) stores.
+//   * the tile is then streamed out with coalesced write-through 16-byte (A=4) / 4-byte
+//     (A=1, 3) stores.
 #pragma once
 #include "gpd_ctrl.h"
 #include "gpd_device.h"
