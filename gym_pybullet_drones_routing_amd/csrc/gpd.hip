@@ -668,6 +668,14 @@ int gpd_set_step_counters(gpd_sim* sim, const int32_t* in, void* stream) {
 namespace {
 // checkpoint sections: state, controller state (PID types), action ring, counters
 struct Section { void* dev; size_t bytes; };
+// blob header: everything that fixes the section sizes and meaning
+constexpr size_t kBlobHeader = 64;
+void blob_header(const gpd_sim* sim, int64_t h[kBlobHeader / 8]) {
+  const int64_t v[kBlobHeader / 8] = {(int64_t)GPD_ABI_VERSION, (int64_t)sim->N, (int64_t)sim->E, (int64_t)sim->D,
+                                      (int64_t)sim->cfg.act_type, (int64_t)sim->prec, (int64_t)sim->ring_len,
+                                      (int64_t)sim->npad};
+  for (size_t i = 0; i < kBlobHeader / 8; ++i) h[i] = v[i];
+}
 int sections(gpd_sim* sim, Section out[4]) {
   out[0] = {sim->d_state, (size_t)kStateComps * sim->npad * real_size(sim)};
   out[1] = {sim->d_ctrl, sim->d_ctrl ? (size_t)kCtrlComps * sim->npad * real_size(sim) : 0};
@@ -681,7 +689,7 @@ size_t gpd_state_bytes(const gpd_sim* sim) {
   if (!sim) return 0;
   Section sec[4];
   const int ns = sections(const_cast<gpd_sim*>(sim), sec);
-  size_t total = 32;
+  size_t total = kBlobHeader;
   for (int i = 0; i < ns; ++i) total += sec[i].bytes;
   return total;
 }
@@ -690,9 +698,10 @@ int gpd_save_state(gpd_sim* sim, void* blob_host, void* stream) {
   if (!sim || !blob_host) return fail(GPD_EINVAL, "gpd_save_state: NULL argument");
   hipStream_t st = (hipStream_t)stream;
   char* b = (char*)blob_host;
-  const int64_t hdr[4] = {(int64_t)GPD_ABI_VERSION, (int64_t)sim->N, (int64_t)sim->cfg.act_type, (int64_t)sim->prec};
-  std::memcpy(b, hdr, 32);
-  size_t off = 32;
+  int64_t hdr[kBlobHeader / 8];
+  blob_header(sim, hdr);
+  std::memcpy(b, hdr, kBlobHeader);
+  size_t off = kBlobHeader;
   Section sec[4];
   const int ns = sections(sim, sec);
   for (int i = 0; i < ns; ++i) {
@@ -707,11 +716,12 @@ int gpd_load_state(gpd_sim* sim, const void* blob_host, void* stream) {
   if (!sim || !blob_host) return fail(GPD_EINVAL, "gpd_load_state: NULL argument");
   hipStream_t st = (hipStream_t)stream;
   const char* b = (const char*)blob_host;
-  int64_t hdr[4];
-  std::memcpy(hdr, b, 32);
-  if (hdr[0] != GPD_ABI_VERSION || hdr[1] != sim->N || hdr[2] != sim->cfg.act_type || hdr[3] != sim->prec)
+  int64_t hdr[kBlobHeader / 8], mine[kBlobHeader / 8];
+  std::memcpy(hdr, b, kBlobHeader);
+  blob_header(sim, mine);
+  if (std::memcmp(hdr, mine, kBlobHeader) != 0)
     return fail(GPD_EINVAL, "gpd_load_state: blob does not match this sim");
-  size_t off = 32;
+  size_t off = kBlobHeader;
   Section sec[4];
   const int ns = sections(sim, sec);
   for (int i = 0; i < ns; ++i) {

@@ -189,7 +189,9 @@ int gpd_get_step_counters(gpd_sim* sim, int32_t* out, void* stream);
 int gpd_set_step_counters(gpd_sim* sim, const int32_t* in, void* stream);
 
 /* Whole-sim checkpoint (state, controller state, action ring, ring head, step counters) to/from host memory.
- * gpd_state_bytes gives the blob size.  These synchronise `stream`. */
+ * gpd_state_bytes gives the blob size (the caller's buffer must have exactly that size); the
+ * blob's 64-byte header (ABI version, N, E, D, action type, precision, ring length, padding)
+ * must match the loading sim, else GPD_EINVAL.  These synchronise `stream`. */
 size_t gpd_state_bytes(const gpd_sim* sim);
 int gpd_save_state(gpd_sim* sim, void* blob_host, void* stream);
 int gpd_load_state(gpd_sim* sim, const void* blob_host, void* stream);

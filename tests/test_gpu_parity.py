@@ -320,3 +320,33 @@ def test_step_parity_aero_configs(case):
     err = state_rel_err(sim.state20().cpu().numpy(), ref)
     assert err.max() <= TOL["f64"], err.max()
     sim.close()
+
+
+def test_abi_error_paths():
+    """Bad arguments come back as GPD_EINVAL with a message, never as a fault."""
+    import ctypes
+    from gym_pybullet_drones_routing_amd import _lib
+    lib = _lib.load()
+    sim = _sim(n_envs=4, task="hover", precision="f64")
+    h = sim._h
+    obs = torch.zeros((4, 1, 72), device="cuda:0")
+    rew = torch.zeros(4, device="cuda:0")
+    te = torch.zeros(4, dtype=torch.uint8, device="cuda:0")
+    tr = torch.zeros(4, dtype=torch.uint8, device="cuda:0")
+    acts = torch.zeros((4 * 4 + 1,), device="cuda:0")
+    vp = ctypes.c_void_p
+    rc = lib.gpd_step(h, None, vp(obs.data_ptr()), vp(rew.data_ptr()), vp(te.data_ptr()), vp(tr.data_ptr()), None, None)
+    assert rc == _lib.GPD_EINVAL and b"NULL" in lib.gpd_last_error()
+    rc = lib.gpd_step(h, vp(acts.data_ptr() + 4), vp(obs.data_ptr()), vp(rew.data_ptr()), vp(te.data_ptr()),
+                      vp(tr.data_ptr()), None, None)
+    assert rc == _lib.GPD_EINVAL and b"aligned" in lib.gpd_last_error()
+    assert lib.gpd_integrate(h, vp(acts.data_ptr()), -1, None, None) == _lib.GPD_EINVAL
+    assert lib.gpd_get_ctrl_state(h, vp(obs.data_ptr()), None) == _lib.GPD_EINVAL   # RPM sim has no controller
+    other = _sim(n_envs=5, task="hover", precision="f64")
+    ob = ctypes.create_string_buffer(lib.gpd_state_bytes(other._h))
+    assert lib.gpd_save_state(other._h, ctypes.cast(ob, vp), None) == _lib.GPD_OK
+    assert lib.gpd_load_state(h, ctypes.cast(ob, vp), None) == _lib.GPD_EINVAL      # blob of another sim
+    with pytest.raises(ValueError):
+        sim.step(torch.zeros((4, 1, 3), device="cuda:0"))                           # wrong action width
+    sim.close()
+    other.close()
