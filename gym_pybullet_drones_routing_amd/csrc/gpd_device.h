@@ -226,11 +226,16 @@ __device__ __forceinline__ void readback_fused(R x, R y, R z, R w, R qn[4], R m[
   m[3] = xy + wz;          m[4] = R(1) - (xx + zz);  m[5] = yz - wx;
   m[6] = xz - wy;          m[7] = yz + wx;           m[8] = R(1) - (xx + yy);
   const R trace = m[0] + m[4] + m[8];
-  // sign rule as selects: the key component is w when trace > 0, else the component of the
-  // largest diagonal entry
-  const int i = m[0] < m[4] ? (m[4] < m[8] ? 2 : 1) : (m[0] < m[8] ? 2 : 0);
-  const R keyd = i == 0 ? x : (i == 1 ? y : z);
-  const R key = trace > R(0) ? w : keyd;
+  // sign rule: the key component is w when trace > 0 (tilt < 120 deg, every lane in practice),
+  // else the component of the largest diagonal entry - resolved in a wave-uniform branch that
+  // only runs when some lane of the wave is tilted that far
+  R key = w;
+  const bool tilted = !(trace > R(0));
+  if (__ballot(tilted) != 0ull) {
+    const int i = m[0] < m[4] ? (m[4] < m[8] ? 2 : 1) : (m[0] < m[8] ? 2 : 0);
+    const R keyd = i == 0 ? x : (i == 1 ? y : z);
+    key = tilted ? keyd : w;
+  }
   const R inv = key < R(0) ? -inv0 : inv0;
   qn[0] = x * inv; qn[1] = y * inv; qn[2] = z * inv; qn[3] = w * inv;
 }
