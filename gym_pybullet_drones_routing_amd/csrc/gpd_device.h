@@ -14,6 +14,13 @@
 namespace gpd {
 
 // ---------------------------------------------------------------- precision-overloaded math
+// A wave-uniform branch that practically never runs: laid out after the hot path, so its code
+// is not fetched into the instruction cache on the launches that skip it.
+#ifdef GPD_NOEXPECT
+#define GPD_RARE(x) (x)
+#else
+#define GPD_RARE(x) __builtin_expect((x), 0)
+#endif
 __device__ __forceinline__ float g_sqrt(float x) { return sqrtf(x); }
 __device__ __forceinline__ double g_sqrt(double x) { return sqrt(x); }
 __device__ __forceinline__ float g_sin(float x) { return sinf(x); }
@@ -207,8 +214,14 @@ template <typename R> struct UnitTol;
 template <> struct UnitTol<double> { static constexpr double v = 1e-9; };
 template <> struct UnitTol<float> { static constexpr float v = 1e-4f; };
 
+// 1/|q| with Bullet's sign (inv) and the rotation matrix.  Bullet's basis->quaternion
+// conversion returns q/|q| with the sign chosen so that w > 0 when trace(R) > 0 (rotation angle
+// < 120 deg), else so that the component of the largest diagonal entry is positive.  The angle
+// includes yaw, which HoverAviary leaves free: a tenth of the drones of a random-action batch
+// sit past 120 deg, so the key is selected branch-free (a branch would cost every wave that
+// holds one of them).
 template <typename R>
-__device__ __forceinline__ void readback_fused(R x, R y, R z, R w, R qn[4], R m[9]) {
+__device__ __forceinline__ void readback_core(R x, R y, R z, R w, R& inv, R m[9]) {
   const R d = x * x + y * y + z * z + w * w;
   // |q| = 1 +- eps (every quaternion _integrateQ produces from a unit one: its update matrix
   // is orthogonal): one Newton step from 1 gives 1/sqrt(d) and 2/d with errors 3eps^2/8 and
@@ -226,17 +239,15 @@ __device__ __forceinline__ void readback_fused(R x, R y, R z, R w, R qn[4], R m[
   m[3] = xy + wz;          m[4] = R(1) - (xx + zz);  m[5] = yz - wx;
   m[6] = xz - wy;          m[7] = yz + wx;           m[8] = R(1) - (xx + yy);
   const R trace = m[0] + m[4] + m[8];
-  // sign rule: the key component is w when trace > 0 (tilt < 120 deg, every lane in practice),
-  // else the component of the largest diagonal entry - resolved in a wave-uniform branch that
-  // only runs when some lane of the wave is tilted that far
-  R key = w;
-  const bool tilted = !(trace > R(0));
-  if (__ballot(tilted) != 0ull) {
-    const int i = m[0] < m[4] ? (m[4] < m[8] ? 2 : 1) : (m[0] < m[8] ? 2 : 0);
-    const R keyd = i == 0 ? x : (i == 1 ? y : z);
-    key = tilted ? keyd : w;
-  }
-  const R inv = key < R(0) ? -inv0 : inv0;
+  const R kd = m[0] < m[4] ? (m[4] < m[8] ? z : y) : (m[0] < m[8] ? z : x);
+  const R key = trace > R(0) ? w : kd;
+  inv = key < R(0) ? -inv0 : inv0;
+}
+
+template <typename R>
+__device__ __forceinline__ void readback_fused(R x, R y, R z, R w, R qn[4], R m[9]) {
+  R inv;
+  readback_core(x, y, z, w, inv, m);
   qn[0] = x * inv; qn[1] = y * inv; qn[2] = z * inv; qn[3] = w * inv;
 }
 
@@ -245,10 +256,16 @@ __device__ __forceinline__ void readback_fused(R x, R y, R z, R w, R qn[4], R m[
 // square root of |omega|^2 nor a division by |omega| (error < 1e-17 relative in double,
 // < 1e-9 in float).
 __device__ __forceinline__ void cos_sinc(double t2, double& c, double& sc) {
-  sc = 1.0 + t2 * (-1.0 / 6 + t2 * (1.0 / 120 + t2 * (-1.0 / 5040 + t2 * (1.0 / 362880 + t2 * (-1.0 / 39916800 +
-           t2 * (1.0 / 6227020800.0 + t2 * (-1.0 / 1307674368000.0)))))));
-  c = 1.0 + t2 * (-0.5 + t2 * (1.0 / 24 + t2 * (-1.0 / 720 + t2 * (1.0 / 40320 + t2 * (-1.0 / 3628800 +
-          t2 * (1.0 / 479001600.0 + t2 * (-1.0 / 87178291200.0)))))));
+  // Estrin's scheme (dependency depth 4 instead of Horner's 8; same truncation, ~1 ulp rounding)
+  const double t4 = t2 * t2, t8 = t4 * t4;
+  const double s01 = 1.0 + t2 * (-1.0 / 6), s23 = 1.0 / 120 + t2 * (-1.0 / 5040);
+  const double s45 = 1.0 / 362880 + t2 * (-1.0 / 39916800);
+  const double s67 = 1.0 / 6227020800.0 + t2 * (-1.0 / 1307674368000.0);
+  sc = (s01 + t4 * s23) + t8 * (s45 + t4 * s67);
+  const double c01 = 1.0 + t2 * (-0.5), c23 = 1.0 / 24 + t2 * (-1.0 / 720);
+  const double c45 = 1.0 / 40320 + t2 * (-1.0 / 3628800);
+  const double c67 = 1.0 / 479001600.0 + t2 * (-1.0 / 87178291200.0);
+  c = (c01 + t4 * c23) + t8 * (c45 + t4 * c67);
 }
 __device__ __forceinline__ void cos_sinc(float t2, float& c, float& sc) {
   sc = 1.0f + t2 * (-1.0f / 6 + t2 * (1.0f / 120 + t2 * (-1.0f / 5040 + t2 * (1.0f / 362880))));
@@ -323,7 +340,7 @@ __device__ __forceinline__ void obs_euler_f32(const R q[4], const AttitudeArgs<R
   pitch = asinf((float)sa);
   roll = atan2f((float)t.a, (float)t.b);
   yaw = atan2f((float)(R(2) * (x * y + w * z)), (float)(w * w + x * x - y * y - z * z));
-  if (__ballot(t.gimbal) != 0ull) {
+  if (GPD_RARE(__ballot(t.gimbal) != 0ull)) {
     if (t.sarg <= R(-0.99999)) {
       pitch = -1.57079632679489661923f; roll = 0.0f; yaw = 2.0f * atan2f((float)x, (float)-y);
     } else if (t.sarg >= R(0.99999)) {
@@ -413,23 +430,64 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
 }
 
 // ---------------------------------------------------------------- one DYN substep
+// The readback that precedes the substep (BaseAviary.py:346-347 -> :517, :836) followed by
 // BaseAviary._dynamics (:815-874) + _integrateQ (:876-889), evaluated on the readback
 // snapshot (pos/vel from the client copy, qn = re-normalised orientation, rpy = its Euler
-// angles, of which the ground effect only needs |roll|,|pitch| < pi/2 -> `gnd_upright`),
-// optionally with the aero force terms of _groundEffect/_drag/_downwash added as a
-// body wrench (see DESIGN.md §2 "new combination").
-//   rpm  : this ctrl step's clipped action (current substep)
+// angles, of which the ground effect only needs |roll|,|pitch| < pi/2 -> upright), optionally
+// with the aero force terms of _groundEffect/_drag/_downwash added as a body wrench (see
+// DESIGN.md §2 "new combination").
+//   rpm  : this ctrl step's clipped action (current substep); W its propeller wrench
 //   last : self.last_clipped_action (previous ctrl step's rpm on the first substep)
 //   dwsum: summed downwash force along body z (already reduced over the env's drones)
 // ANGV: also update the world-frame ang_v (write-only for the dynamics: only the value after the
 // last substep of a control step is ever observed, so earlier substeps skip it).
+// Schedule: the common path is ONE basic block.  With FAST (no aero terms) the torques do not
+// depend on the attitude, so the rotation chain (omega, theta^2, the cos/sinc series) is
+// written before the readback and the two dependency chains interleave.  Lanes with
+// |theta| >= 0.5 (|omega| >= 240 rad/s at 240 Hz: library sin/cos) are redone in a
+// wave-uniform branch at the end.
 template <typename R, bool FAST, bool ANGV = true>
-__device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R Rm[9], bool gnd_upright,
-                                            const R rpm[4], const R W[4], const R last[4], R dwsum,
+__device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R W[4], const R last[4], R dwsum,
                                             const Consts<R>& c, const DynK<R>& k) {
+  const R q0[4] = {s.qx, s.qy, s.qz, s.qw};
+  R inv, Rm[9];
+  bool up = true;
+  auto readback = [&]() {
+    readback_core(q0[0], q0[1], q0[2], q0[3], inv, Rm);
+    if (!FAST && (k.flags & F_GND)) {   // |self.rpy[0,1]| < pi/2, :742
+      const R qn[4] = {q0[0] * inv, q0[1] * inv, q0[2] * inv, q0[3] * inv};
+      up = upright(attitude_args(qn));
+    }
+  };
+  if (!FAST) readback();
   R fz, tx, ty, tz;
-  body_wrench<R, FAST>(s, Rm, gnd_upright, rpm, W, c, k, fz, tx, ty, tz);
+  body_wrench<R, FAST>(s, Rm, up, rpm, W, c, k, fz, tx, ty, tz);
   if (!FAST && (k.flags & F_DW)) fz = fz + dwsum;      // _downwash :801-811 (body z)
+  // torques - ω × (Jω); ω̇ = J⁻¹ τ                     :852-854
+  const R jwx = k.jx * s.wx, jwy = k.jy * s.wy, jwz = k.jz * s.wz;
+  const R cx = s.wy * jwz - s.wz * jwy;
+  const R cy = s.wz * jwx - s.wx * jwz;
+  const R cz = s.wx * jwy - s.wy * jwx;
+  const R dwx = k.ijx * (tx - cx), dwy = k.ijy * (ty - cy), dwz = k.ijz * (tz - cz);
+  s.wx = s.wx + k.dt * dwx;                            // :856
+  s.wy = s.wy + k.dt * dwy;
+  s.wz = s.wz + k.dt * dwz;
+  // _integrateQ(quat, rpy_rates, dt)                  :876-889
+  const R p = s.wx, q = s.wy, r = s.wz;
+  const R n2 = p * p + q * q + r * r;
+  // np.isclose(|omega|, 0) <=> |omega| <= 1e-8 <=> |omega|^2 <= 1e-16 (the two tests can only
+  // disagree when |omega| lies within an ulp of 1e-8; numpy's BLAS norm itself rounds there)
+  const bool rot = n2 > R(1e-16);
+  // q' = (I cos(theta) + (2/|omega|) Lambda sin(theta)) q, theta = |omega| dt/2: the off-diagonal
+  // weights (2/|omega|)(p/2) sin(theta) = p * (dt/2) * sin(theta)/theta.  Evaluated for every
+  // lane and selected (no branch); the library sin/cos for |theta| >= 0.5 (|omega| >= 240 rad/s
+  // at 240 Hz) is part of the rare-lane fix-up.
+  const R t2 = n2 * k.hdt2;                            // theta^2
+  R co, sc;                                            // cos(theta), sin(theta)/theta
+  cos_sinc(t2, co, sc);
+  const R sh = k.hdt * sc;                             // sin(theta)/|omega|
+  const bool big = t2 >= R(0.25);
+  if (FAST) readback();
   // R·(0,0,fz) - (0,0,GRAVITY) [+ drag]                 :839-841
   R Fx = Rm[2] * fz, Fy = Rm[5] * fz, Fz = Rm[8] * fz;
   if (!FAST && (k.flags & F_DRAG)) {                   // _drag :773-774 with last_clipped_action
@@ -439,56 +497,37 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R qn[4], const R 
     Fz = Fz + (-c.drag_z * S) * s.vz;
   }
   Fz = Fz - k.gravity;
-  // torques - ω × (Jω); ω̇ = J⁻¹ τ                     :852-854
-  const R jwx = k.jx * s.wx, jwy = k.jy * s.wy, jwz = k.jz * s.wz;
-  const R cx = s.wy * jwz - s.wz * jwy;
-  const R cy = s.wz * jwx - s.wx * jwz;
-  const R cz = s.wx * jwy - s.wy * jwx;
-  const R dwx = k.ijx * (tx - cx), dwy = k.ijy * (ty - cy), dwz = k.ijz * (tz - cz);
   // semi-implicit Euler                                :855-859
   s.vx = s.vx + k.dt * (Fx * k.inv_m);
   s.vy = s.vy + k.dt * (Fy * k.inv_m);
   s.vz = s.vz + k.dt * (Fz * k.inv_m);
-  s.wx = s.wx + k.dt * dwx;
-  s.wy = s.wy + k.dt * dwy;
-  s.wz = s.wz + k.dt * dwz;
   s.px = s.px + k.dt * s.vx;
   s.py = s.py + k.dt * s.vy;
   s.pz = s.pz + k.dt * s.vz;
-  // _integrateQ(quat, rpy_rates, dt)                  :876-889
-  const R p = s.wx, q = s.wy, r = s.wz;
-  const R n2 = p * p + q * q + r * r;
-  // np.isclose(|omega|, 0) <=> |omega| <= 1e-8 <=> |omega|^2 <= 1e-16 (the two tests can only
-  // disagree when |omega| lies within an ulp of 1e-8; numpy's BLAS norm itself rounds there)
-  const bool rot = n2 > R(1e-16);
-  // q' = (I cos(theta) + (2/|omega|) Lambda sin(theta)) q, theta = |omega| dt/2: the off-diagonal
-  // weights (2/|omega|)(p/2) sin(theta) = p * (dt/2) * sin(theta)/theta.  Evaluated for every
-  // lane and selected (no branch); the library sin/cos fix-up for |theta| >= 0.5 (|omega| >=
-  // 240 rad/s at 240 Hz) is a wave-uniform branch that practically never runs.
-  const R t2 = n2 * k.hdt2;                            // theta^2
-  R co, sc;                                            // cos(theta), sin(theta)/theta
-  cos_sinc(t2, co, sc);
-  R sh = k.hdt * sc;                                   // sin(theta)/|omega|
-  const bool big = t2 >= R(0.25);
-  if (__ballot(big) != 0ull) {
+  auto update = [&](R co_, R sh_, R inv_) {
+    const R P = p * sh_, Q = q * sh_, Rr = r * sh_;
+    const R x = q0[0] * inv_, y = q0[1] * inv_, z = q0[2] * inv_, w = q0[3] * inv_;
+    const R nx = ((co_ * x + Rr * y) - Q * z) + P * w;
+    const R ny = ((-Rr * x + co_ * y) + P * z) + Q * w;
+    const R nz = ((Q * x - P * y) + co_ * z) + Rr * w;
+    const R nw = ((-P * x - Q * y) - Rr * z) + co_ * w;
+    s.qx = rot ? nx : x; s.qy = rot ? ny : y; s.qz = rot ? nz : z; s.qw = rot ? nw : w;
+  };
+  update(co, sh, inv);
+  // resetBaseVelocity(..., np.dot(rotation, rpy_rates))  :868-872
+  if (ANGV) {
+    s.ax = (Rm[0] * s.wx + Rm[1] * s.wy) + Rm[2] * s.wz;
+    s.ay = (Rm[3] * s.wx + Rm[4] * s.wy) + Rm[5] * s.wz;
+    s.az = (Rm[6] * s.wx + Rm[7] * s.wy) + Rm[8] * s.wz;
+  }
+  // keep the translation in the main block (it fills the latency of the rotation chain)
+  asm volatile("" ::"v"(s.px), "v"(s.py), "v"(s.pz));
+  if (GPD_RARE(__ballot(big) != 0ull)) {
     if (big) {
       const R nrm = g_sqrt(n2), th = nrm * k.hdt;
-      co = g_cos(th);
-      sh = g_sin(th) / nrm;
+      update(g_cos(th), g_sin(th) / nrm, inv);
     }
   }
-  const R P = p * sh, Q = q * sh, Rr = r * sh;
-  const R x = qn[0], y = qn[1], z = qn[2], w = qn[3];
-  const R nx = ((co * x + Rr * y) - Q * z) + P * w;
-  const R ny = ((-Rr * x + co * y) + P * z) + Q * w;
-  const R nz = ((Q * x - P * y) + co * z) + Rr * w;
-  const R nw = ((-P * x - Q * y) - Rr * z) + co * w;
-  s.qx = rot ? nx : x; s.qy = rot ? ny : y; s.qz = rot ? nz : z; s.qw = rot ? nw : w;
-  // resetBaseVelocity(..., np.dot(rotation, rpy_rates))  :868-872
-  if (!ANGV) return;
-  s.ax = (Rm[0] * s.wx + Rm[1] * s.wy) + Rm[2] * s.wz;
-  s.ay = (Rm[3] * s.wx + Rm[4] * s.wy) + Rm[5] * s.wz;
-  s.az = (Rm[6] * s.wx + Rm[7] * s.wy) + Rm[8] * s.wz;
 }
 
 // Summed downwash on drone (px,py,pz) from the env's D drones whose positions sit in LDS

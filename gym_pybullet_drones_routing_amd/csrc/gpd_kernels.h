@@ -42,7 +42,7 @@ enum : int { TASK_NONE = 0, TASK_HOVER = 1, TASK_MULTIHOVER = 2 };
 // shader clock at phase boundaries of step_kernel into g_stamps[block][phase].  The shipped
 // library executes no stamp.
 #ifdef GPD_STAMPS
-constexpr int kStampPhases = 12;
+constexpr int kStampPhases = 14;   // 0..10 shader clocks; 11 / 12: s_memrealtime (100 MHz) at entry / end
 __device__ unsigned long long g_stamps[65536 * kStampPhases];
 #define GPD_STAMP(k)                                                                      \
   do {                                                                                    \
@@ -52,8 +52,17 @@ __device__ unsigned long long g_stamps[65536 * kStampPhases];
     if (threadIdx.x == 0 && blockIdx.x < 65536) g_stamps[blockIdx.x * kStampPhases + (k)] = t_; \
     __builtin_amdgcn_sched_barrier(0);                                                    \
   } while (0)
+#define GPD_RSTAMP(k)                                                                     \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    unsigned long long t_;                                                                \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) g_stamps[blockIdx.x * kStampPhases + (k)] = t_; \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+  } while (0)
 #else
 #define GPD_STAMP(k) do {} while (0)
+#define GPD_RSTAMP(k) do {} while (0)
 #endif
 
 // Write-through (sc1) stores through a buffer resource.  Every launch ends with a release that
@@ -173,10 +182,6 @@ template <typename R, bool MULTI, bool FAST, bool ANGV = true>
 __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const R W[4], const R last[4],
                                               const Consts<R>& c, const DynK<R>& k, R* sx, R* sy, R* sz, int tid,
                                               int base, int D, DwPairs pairs = DwPairs{0, 0}, R* spair = nullptr) {
-  R qn[4], Rm[9];
-  readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);  // :346-347 -> :517, :836
-  bool up = true;
-  if (!FAST && (k.flags & F_GND)) up = upright(attitude_args(qn));  // |self.rpy[0,1]| < pi/2, :742
   R dw = R(0);
   if (MULTI && !FAST && (k.flags & F_DW)) {
     sx[tid] = s.px; sy[tid] = s.py; sz[tid] = s.pz;
@@ -196,7 +201,7 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
     }
     __syncthreads();
   }
-  dyn_substep<R, FAST, ANGV>(s, qn, Rm, up, rpm, W, last, dw, c, k);
+  dyn_substep<R, FAST, ANGV>(s, rpm, W, last, dw, c, k);
 }
 
 // Bytes of dynamic LDS the step kernel needs for its observation tile: the row's columns
@@ -226,6 +231,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
   __shared__ float srew[MULTI ? 2 * kWave : 1], sdist[MULTI ? 2 * kWave : 1];
   __shared__ int sflag[MULTI ? 2 * kWave : 1];
   __shared__ R spair[MULTI ? kPairMax : 1];
+  GPD_RSTAMP(11);
   GPD_STAMP(0);
   const Consts<R>& c = *cp;
   const int tid = threadIdx.x;
@@ -309,14 +315,15 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
   R W[4];
   rpm_wrench<R, FAST>(rpm, dk, c, W);
   // substeps 1..nsub-1 skip the (write-only) world ang_v; the last one produces it
-  for (int it = 0; it < c.nsub - 1; ++it) {
+  // (the first substep is peeled so the loop body stays one basic block)
+  if (c.nsub > 1) {
     substep_block<R, MULTI, FAST, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
-    if (it == 0) {
-      GPD_STAMP(1);
-      history_dma();
-    }
+    GPD_STAMP(1);
+    history_dma();
+    for (int it = 1; it < c.nsub - 1; ++it)
+      substep_block<R, MULTI, FAST, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
   }
   substep_block<R, MULTI, FAST, true>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
 #pragma unroll
@@ -520,6 +527,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
     }
   }
   GPD_STAMP(7);
+  GPD_RSTAMP(12);
   if (!active) return;
   if (v.wt & 2) store_drone_wt(v, n, s, last);
   else store_drone(v, n, s, last);

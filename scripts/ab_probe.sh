@@ -4,7 +4,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out/ab
 P=gym_pybullet_drones_routing_amd
 i=0
-for cfg in "old 0" "new 0" "new 3" "old 0" "new 0" "new 3"; do
+for cfg in ${AB_CFGS:-"old 3" "new 3" "old 3" "new 3"}; do
   set -- $cfg
   lib=$P/libgpd.so; [ $1 = old ] && lib=$P/libgpd_old.so
   i=$((i+1))

@@ -6,27 +6,40 @@ Phases (lane 0 of every block, s_memtime shader clocks):
  barrier -> 7 tile copy-out issued."""
 import ctypes, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["GPD_LIB"] = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                     "gym_pybullet_drones_routing_amd", "libgpd_stamps.so")
+os.environ["GPD_LIB"] = os.environ.get("GPD_STAMPS_LIB") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gym_pybullet_drones_routing_amd", "libgpd_stamps.so")
 import numpy as np, torch
 from gym_pybullet_drones_routing_amd import _lib
 from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
 lib = _lib.load()
 lib.gpd_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-for prec in ("f64", "f32"):
-    for E in (4096, 1 << 20):
+for prec in os.environ.get("STAMP_PRECS", "f64 f32").split():
+    for E in [int(x) for x in os.environ.get("STAMP_ENVS", "4096 1048576").split()]:
         sim = BatchedAviarySim(n_envs=E, task="hover", precision=prec, device="cuda:0")
         scale = float(os.environ.get("ACT_SCALE", "1.0"))
         acts = [((torch.rand((E, 1, 4), device="cuda:0") * 2 - 1) * scale).contiguous() for _ in range(16)]
         g = sim.capture_graph(acts)
         for _ in range(4): g.replay()
         torch.cuda.synchronize()
-        nb = min(65536, (E + 63) // 64)
-        buf = np.zeros((nb, 12), np.uint64)
+        nb = min(65536, -(-sim.n_drones // sim.constants.drones_per_block))
+        buf = np.zeros((nb, 14), np.uint64)
         assert lib.gpd_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), nb) == 0
         t = buf.astype(np.int64)
         order = [0, 10, 1, 2, 3, 4, 5, 6, 8, 9, 7]   # 10: loads landed; 8/9 inside the copy-out (after LDS reads, after stores)
         d = [(a, b, int(np.median(t[:, b] - t[:, a]))) for a, b in zip(order[:-1], order[1:])]
+        tot = t[:, 7] - t[:, 0]
         print(f"{prec} E={E}: per-block phase cycles (median) " + " ".join(f"{a}->{b}:{c}" for a, b, c in d) +
-              f" | total median {int(np.median(t[:,7]-t[:,0]))}", flush=True)
+              f" | total median {int(np.median(tot))} p90 {int(np.percentile(tot, 90))} max {int(tot.max())}", flush=True)
+        slow = int(np.argmax(tot))
+        print(f"    slowest block {slow}: " + " ".join(f"{a}->{b}:{int(t[slow, b] - t[slow, a])}"
+                                                    for a, b in zip(order[:-1], order[1:])), flush=True)
+        hist = np.percentile(tot, [10, 25, 50, 75, 90, 95, 99]).astype(int)
+        print(f"    block total percentiles 10/25/50/75/90/95/99: {list(hist)}; blocks > median+1000: "
+              f"{int((tot > np.median(tot) + 1000).sum())} of {len(tot)}", flush=True)
+        # s_memrealtime (100 MHz, shared by the device): block start spread and first-start -> last-end span
+        rs, re_ = t[:, 11], t[:, 12]
+        if rs.min() > 0:
+            print(f"    realtime: start spread {(rs.max() - rs.min()) * 10} ns, block duration median "
+                  f"{int(np.median(re_ - rs)) * 10} ns max {int((re_ - rs).max()) * 10} ns, span {(re_.max() - rs.min()) * 10} ns",
+                  flush=True)
         sim.close()
