@@ -37,9 +37,11 @@ def build(force=False, verbose=False, stamps=False):
     if not force and not stamps and not needs_build():
         return LIB_PATH
     tmp = out.with_suffix(".so.tmp")
-    # kernarg preloading: the step kernel's leading scalar arguments arrive in SGPRs
+    # kernarg preloading: the step kernel's leading scalar arguments arrive in SGPRs.
+    # max-ilp scheduling: a step launch runs ONE wave per CU (thin blocks), so the default
+    # occupancy-driven scheduler buys nothing and ILP within the wave is what hides latency.
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-mcode-object-version=5", "-O3", "-std=c++17",
-           "-mllvm", "-amdgpu-kernarg-preload-count=12",
+           "-mllvm", "-amdgpu-kernarg-preload-count=12", "-mllvm", "-amdgpu-sched-strategy=max-ilp",
            "-fPIC", "-shared", "-Wall", "-Wno-unused-result", f"-I{INCLUDE}", "-o", str(tmp),
            str(CSRC / "gpd.hip")] + (["-DGPD_STAMPS"] if stamps else [])
     res = subprocess.run(cmd, capture_output=True, text=True)

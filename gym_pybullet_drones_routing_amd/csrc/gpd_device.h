@@ -244,6 +244,42 @@ __device__ __forceinline__ void readback_core(R x, R y, R z, R w, R& inv, R m[9]
   inv = key < R(0) ? -inv0 : inv0;
 }
 
+// Sign transfer through the high 32-bit word (the sign bit): mag carries sign(key).
+__device__ __forceinline__ int hi_word(double x) { return __double2hiint(x); }
+__device__ __forceinline__ int hi_word(float x) { return __float_as_int(x); }
+__device__ __forceinline__ double with_sign_word(double mag, int kw) {
+  return __hiloint2double((__double2hiint(mag) & 0x7fffffff) | (kw & int(0x80000000)), __double2loint(mag));
+}
+__device__ __forceinline__ float with_sign_word(float mag, int kw) {
+  return __int_as_float((__float_as_int(mag) & 0x7fffffff) | (kw & int(0x80000000)));
+}
+
+// The substep's readback for a quaternion with |q|^2 = d within UnitTol of 1 (dyn_substep
+// re-normalises any other lane first): inv = +-1/|q| with Bullet's sign rule and the rotation
+// matrix entries the substep uses - the third column (thrust direction) and, with FULL, all nine
+// (world-frame ang_v).  The sign key is chosen on the high words only (one select per candidate);
+// the key is never +-0 for a unit quaternion (trace > 0 gives w^2 > 1/4, else the component of
+// the largest diagonal entry has square >= 1/12), so its sign bit is the "< 0" test.
+template <typename R, bool FULL>
+__device__ __forceinline__ void readback_unit(R x, R y, R z, R w, R d, R& inv, R m[9]) {
+  const R inv0 = R(1.5) - R(0.5) * d;                   // 1/|q| (one Newton step from 1)
+  const R s = R(2) * (R(2) - d);                         // 2/|q|^2
+  const R xs = x * s, ys = y * s, zs = z * s;
+  const R wx = w * xs, wy = w * ys, wz = w * zs;
+  const R xx = x * xs, xy = x * ys, xz = x * zs;
+  const R yy = y * ys, yz = y * zs, zz = z * zs;
+  m[0] = R(1) - (yy + zz); m[2] = xz + wy;
+  m[4] = R(1) - (xx + zz); m[5] = yz - wx;
+  m[8] = R(1) - (xx + yy);
+  if (FULL) {
+    m[1] = xy - wz; m[3] = xy + wz; m[6] = xz - wy; m[7] = yz + wx;
+  }
+  const R trace = m[0] + m[4] + m[8];
+  int kw = m[0] < m[4] ? (m[4] < m[8] ? hi_word(z) : hi_word(y)) : (m[0] < m[8] ? hi_word(z) : hi_word(x));
+  kw = trace > R(0) ? hi_word(w) : kw;
+  inv = with_sign_word(inv0, kw);
+}
+
 template <typename R>
 __device__ __forceinline__ void readback_fused(R x, R y, R z, R w, R qn[4], R m[9]) {
   R inv;
@@ -449,11 +485,26 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
 template <typename R, bool FAST, bool ANGV = true>
 __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R W[4], const R last[4], R dwsum,
                                             const Consts<R>& c, const DynK<R>& k) {
-  const R q0[4] = {s.qx, s.qy, s.qz, s.qw};
+  R q0[4] = {s.qx, s.qy, s.qz, s.qw};
+  R d = q0[0] * q0[0] + q0[1] * q0[1] + q0[2] * q0[2] + q0[3] * q0[3];
+  // |q| = 1 +- eps for every quaternion _integrateQ produces from a unit one (its update matrix
+  // is orthogonal); a lane that is not (a state set from outside, a NaN) is re-normalised here
+  // in a wave-uniform branch that the substeps of a normal batch never take
+  {
+    const bool unit = g_abs(d - R(1)) < UnitTol<R>::v;
+    if (GPD_RARE(__ballot(!unit) != 0ull)) {
+      if (!unit) {
+        const R r = g_rsqrt(d);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q0[i] = q0[i] * r;
+        d = q0[0] * q0[0] + q0[1] * q0[1] + q0[2] * q0[2] + q0[3] * q0[3];
+      }
+    }
+  }
   R inv, Rm[9];
   bool up = true;
   auto readback = [&]() {
-    readback_core(q0[0], q0[1], q0[2], q0[3], inv, Rm);
+    readback_unit<R, ANGV || !FAST>(q0[0], q0[1], q0[2], q0[3], d, inv, Rm);
     if (!FAST && (k.flags & F_GND)) {   // |self.rpy[0,1]| < pi/2, :742
       const R qn[4] = {q0[0] * inv, q0[1] * inv, q0[2] * inv, q0[3] * inv};
       up = upright(attitude_args(qn));
@@ -504,16 +555,20 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R
   s.px = s.px + k.dt * s.vx;
   s.py = s.py + k.dt * s.vy;
   s.pz = s.pz + k.dt * s.vz;
-  auto update = [&](R co_, R sh_, R inv_) {
-    const R P = p * sh_, Q = q * sh_, Rr = r * sh_;
-    const R x = q0[0] * inv_, y = q0[1] * inv_, z = q0[2] * inv_, w = q0[3] * inv_;
-    const R nx = ((co_ * x + Rr * y) - Q * z) + P * w;
-    const R ny = ((-Rr * x + co_ * y) + P * z) + Q * w;
-    const R nz = ((Q * x - P * y) + co_ * z) + Rr * w;
-    const R nw = ((-P * x - Q * y) - Rr * z) + co_ * w;
-    s.qx = rot ? nx : x; s.qy = rot ? ny : y; s.qz = rot ? nz : z; s.qw = rot ? nw : w;
+  // q' = M(omega) (inv q0) = M'(omega) q0 with the readback's 1/|q| folded into M's entries;
+  // below the isclose threshold P = Q = R = 0 and co = 1 exactly (t2 <= 1e-16), so q' = inv q0,
+  // the readback quaternion itself, as the reference's skip leaves it
+  auto update = [&](R co_, R sh_) {
+    const R shi = sh_ * inv;
+    const R P = rot ? p * shi : R(0), Q = rot ? q * shi : R(0), Rr = rot ? r * shi : R(0);
+    const R C = co_ * inv;
+    const R x = q0[0], y = q0[1], z = q0[2], w = q0[3];
+    s.qx = ((C * x + Rr * y) - Q * z) + P * w;
+    s.qy = ((-Rr * x + C * y) + P * z) + Q * w;
+    s.qz = ((Q * x - P * y) + C * z) + Rr * w;
+    s.qw = ((-P * x - Q * y) - Rr * z) + C * w;
   };
-  update(co, sh, inv);
+  update(co, sh);
   // resetBaseVelocity(..., np.dot(rotation, rpy_rates))  :868-872
   if (ANGV) {
     s.ax = (Rm[0] * s.wx + Rm[1] * s.wy) + Rm[2] * s.wz;
@@ -525,7 +580,7 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R
   if (GPD_RARE(__ballot(big) != 0ull)) {
     if (big) {
       const R nrm = g_sqrt(n2), th = nrm * k.hdt;
-      update(g_cos(th), g_sin(th) / nrm, inv);
+      update(g_cos(th), g_sin(th) / nrm);
     }
   }
 }
