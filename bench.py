@@ -196,8 +196,13 @@ def other_configs(device, precision, act):
               initial_xyzs=stag), 4),
         ("4096 HoverAviary envs, ActionType.ONE_D_PID (batched DSLPIDControl + DYN)",
          dict(n_envs=4096, task="hover", act=ActionType.ONE_D_PID, physics=Physics.DYN), 1),
-        ("4096 HoverAviary envs, ActionType.PID (waypoint + DSLPIDControl, PYB force placement)",
+        ("4096 HoverAviary envs, ActionType.PID (waypoint + DSLPIDControl, Physics.PYB)",
          dict(n_envs=4096, task="hover", act=ActionType.PID, physics=Physics.PYB), 3),
+        ("4096 HoverAviary envs, Physics.PYB (HoverAviary default: restated Bullet multibody step)",
+         dict(n_envs=4096, task="hover", act=ActionType(act), physics=Physics.PYB), 4),
+        ("512 MultiHoverAviary x 8 drones, Physics.PYB_GND_DRAG_DW (Bullet step, staggered init)",
+         dict(n_envs=512, drones_per_env=8, task="multihover", act=ActionType.RPM, physics=Physics.PYB_GND_DRAG_DW,
+              initial_xyzs=stag), 4),
     ]
     out = []
     for name, kw, A in cases:

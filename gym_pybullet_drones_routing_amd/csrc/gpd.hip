@@ -158,7 +158,12 @@ Consts<R> make_consts(const gpd_sim* s) {
   for (int k = 0; k < 3; ++k) c.target0[k] = (R)s->target[k];
   c.hover_f32 = (float)s->K.hover_rpm;
   c.model = P.model;
-  c.flags = s->cfg.physics_flags;
+  // the Bullet integrator always places the thrust at the prop links (_physics :698-705)
+  c.flags = s->cfg.physics_flags | ((s->cfg.physics_flags & GPD_F_BULLET) ? GPD_F_GEOM_WRENCH : 0);
+  c.lin_damp = (R)0.04;      // btMultiBody() m_linearDamping (not removed: BaseAviary.py:492-494)
+  c.ang_damp = (R)0.04;      // btMultiBody() m_angularDamping
+  c.max_vel = (R)100.0;      // btMultiBody() m_maxCoordinateVelocity
+  c.ang_thr2 = (R)((0.125 * M_PI) * (0.125 * M_PI));   // (ANGULAR_MOTION_THRESHOLD / 2)^2
   c.nsub = s->nsub;
   const gpd_pid_params& Q = s->pid;
   PidConsts<R>& k = c.pid;
@@ -371,7 +376,7 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   if (C.task == GPD_TASK_HOVER && C.drones_per_env != 1)
     return fail(GPD_EINVAL, "gpd_create: HoverAviary is single-drone (drones_per_env must be 1)");
   if (C.precision != GPD_F32 && C.precision != GPD_F64) return fail(GPD_EINVAL, "gpd_create: bad precision");
-  if (C.physics_flags & ~(GPD_F_GND | GPD_F_DRAG | GPD_F_DW | GPD_F_GEOM_WRENCH))
+  if (C.physics_flags & ~(GPD_F_GND | GPD_F_DRAG | GPD_F_DW | GPD_F_GEOM_WRENCH | GPD_F_BULLET))
     return fail(GPD_EINVAL, "gpd_create: unknown physics flag");
   if (params->model < GPD_MODEL_CF2X || params->model > GPD_MODEL_RACE)
     return fail(GPD_EINVAL, "gpd_create: unknown drone model");

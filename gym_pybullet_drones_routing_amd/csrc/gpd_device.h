@@ -60,7 +60,7 @@ template <> struct PiC<double> { static constexpr double pi = 3.1415926535897932
 
 // ---------------------------------------------------------------- model constants (device memory)
 enum : int { MODEL_CF2X = 0, MODEL_CF2P = 1, MODEL_RACE = 2 };
-enum : int { F_GND = 1, F_DRAG = 2, F_DW = 4, F_GEOM = 8 };
+enum : int { F_GND = 1, F_DRAG = 2, F_DW = 4, F_GEOM = 8, F_BULLET = 16 };
 
 // DSLPIDControl coefficients (control/DSLPIDControl.py:37-60, settable like
 // BaseControl.setPIDCoefficients :138-177) and the controller's own constants.
@@ -90,6 +90,9 @@ struct Consts {
   R rx[4], ry[4], rz[4];                   // prop link origins (cf2x.urdf:42,54,66,78)
   R inv_m;                 // 1/M      (F/M as a multiply; differs from the division by <= 1 ulp)
   R rpm2rad;               // 2*pi/60  (drag: sum(2*pi*rpm/60))
+  R lin_damp, ang_damp;    // btMultiBody m_linearDamping / m_angularDamping defaults (F_BULLET)
+  R max_vel;               // btMultiBody m_maxCoordinateVelocity (F_BULLET)
+  R ang_thr2;              // (ANGULAR_MOTION_THRESHOLD/2)^2: the clamped half angle, squared
   R init0[10];             // reset template of drone 0 (pos, stored quat, rpy): single-drone envs
   R target0[3];            // task target of drone 0 (single-drone envs: no dependent global load)
                            // read it with scalar loads instead of a dependent per-lane load
@@ -465,6 +468,88 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
   tz_out = W[3];
 }
 
+// ---------------------------------------------------------------- one Bullet (PYB*) substep
+// Physics.PYB* (SURVEY.md §8 f3): the forces of _physics / _groundEffect / _drag / _downwash
+// (BaseAviary.py:679-811) on the links of the URDF multibody, then ONE p.stepSimulation()
+// (:369-370) of a free btMultiBody base without contacts, restated from Bullet3 (oracle:
+// oracle/bullet_mb.py, which follows computeAccelerationsArticulatedBodyAlgorithmMultiDof /
+// applyDeltaVeeMultiDof / stepPositionsMultiDof step by step).  Evaluated here in the
+// world-frame form that the base-frame spatial algebra reduces to (the m w x v bias terms cancel
+// and I^-1 I w = w; tests/test_oracle_bullet.py checks the two forms against each other):
+//   w_b   = R^T w                                     (R = basis of the stored orientation)
+//   wdot  = R J^-1 (tau - w_b x J w_b) - k_a (1 + |w|) w
+//   vdot  = (R (0,0,T) [+ drag] - (0,0,M G)) / M - k_l (1 + |v|) v
+//   w, v += dt * (wdot, vdot), each coordinate clamped to +-max_vel; p += dt * v
+//   q_s'  = normalise((a, cos(f dt/2)) (x) q_s),  a = w sin(f dt/2)/f,  f = min(|w|, pi/4 / dt)
+// with q_s = m_baseQuat^-1 (body -> world, what the readback round-trips).  The state's
+// rpy_rates slots hold the world angular velocity (m_realBuf[0:3]); ang_v is its readback copy.
+// The exponential map's half angle is clamped at pi/8 < 0.5, so the cos / sinc series always
+// applies (a select, no branch; below Bullet's f < 0.001 Taylor switch the series agrees with
+// Bullet's two-term expansion to ~1e-30).
+template <typename R, bool ANGV>
+__device__ __forceinline__ void bullet_substep(Drone<R>& s, const R rpm[4], const R W[4], const R last[4], R dwsum,
+                                               R q0[4], R d, const Consts<R>& c, const DynK<R>& k) {
+  R inv, Rm[9];
+  readback_unit<R, true>(q0[0], q0[1], q0[2], q0[3], d, inv, Rm);
+  bool up = true;
+  if (k.flags & F_GND) {   // |self.rpy[0,1]| < pi/2, :742
+    const R qn[4] = {q0[0] * inv, q0[1] * inv, q0[2] * inv, q0[3] * inv};
+    up = upright(attitude_args(qn));
+  }
+  R fz, tx, ty, tz;
+  body_wrench<R, false>(s, Rm, up, rpm, W, c, k, fz, tx, ty, tz);
+  if (k.flags & F_DW) fz = fz + dwsum;
+  // angular: base-frame rate, gyroscopic term, damping on the world rate
+  const R wbx = (Rm[0] * s.wx + Rm[3] * s.wy) + Rm[6] * s.wz;
+  const R wby = (Rm[1] * s.wx + Rm[4] * s.wy) + Rm[7] * s.wz;
+  const R wbz = (Rm[2] * s.wx + Rm[5] * s.wy) + Rm[8] * s.wz;
+  const R jwx = k.jx * wbx, jwy = k.jy * wby, jwz = k.jz * wbz;
+  const R bx = k.ijx * (tx - (wby * jwz - wbz * jwy));
+  const R by = k.ijy * (ty - (wbz * jwx - wbx * jwz));
+  const R bz = k.ijz * (tz - (wbx * jwy - wby * jwx));
+  const R kw = c.ang_damp + c.ang_damp * g_sqrt(s.wx * s.wx + s.wy * s.wy + s.wz * s.wz);
+  const R dwx = ((Rm[0] * bx + Rm[1] * by) + Rm[2] * bz) - kw * s.wx;
+  const R dwy = ((Rm[3] * bx + Rm[4] * by) + Rm[5] * bz) - kw * s.wy;
+  const R dwz = ((Rm[6] * bx + Rm[7] * by) + Rm[8] * bz) - kw * s.wz;
+  const R mv = c.max_vel;
+  auto clampv = [mv](R x) { return x > mv ? mv : (x < -mv ? -mv : x); };
+  s.wx = clampv(s.wx + k.dt * dwx);
+  s.wy = clampv(s.wy + k.dt * dwy);
+  s.wz = clampv(s.wz + k.dt * dwz);
+  // linear
+  R Fx = Rm[2] * fz, Fy = Rm[5] * fz, Fz = Rm[8] * fz;
+  if (k.flags & F_DRAG) {   // _drag :773-781 with last_clipped_action, world force drag_factors * vel
+    const R S = ((last[0] * c.rpm2rad + last[1] * c.rpm2rad) + last[2] * c.rpm2rad) + last[3] * c.rpm2rad;
+    Fx = Fx + (-c.drag_xy * S) * s.vx;
+    Fy = Fy + (-c.drag_xy * S) * s.vy;
+    Fz = Fz + (-c.drag_z * S) * s.vz;
+  }
+  Fz = Fz - k.gravity;
+  const R kv = c.lin_damp + c.lin_damp * g_sqrt(s.vx * s.vx + s.vy * s.vy + s.vz * s.vz);
+  s.vx = clampv(s.vx + k.dt * (Fx * k.inv_m - kv * s.vx));
+  s.vy = clampv(s.vy + k.dt * (Fy * k.inv_m - kv * s.vy));
+  s.vz = clampv(s.vz + k.dt * (Fz * k.inv_m - kv * s.vz));
+  s.px = s.px + k.dt * s.vx;
+  s.py = s.py + k.dt * s.vy;
+  s.pz = s.pz + k.dt * s.vz;
+  // orientation: exponential map with the new world rate, clamped half angle
+  const R t2 = (s.wx * s.wx + s.wy * s.wy + s.wz * s.wz) * k.hdt2;
+  const bool clamp = t2 > c.ang_thr2;
+  R co, sc;
+  cos_sinc(clamp ? c.ang_thr2 : t2, co, sc);
+  // axis = w sin(f dt/2)/f = w (dt/2) sinc(f dt/2), f clamped or not
+  const R sh = k.hdt * sc;
+  const R ax = s.wx * sh, ay = s.wy * sh, az = s.wz * sh;
+  const R x = q0[0], y = q0[1], z = q0[2], w = q0[3];
+  const R nx = ((co * x + ax * w) + ay * z) - az * y;
+  const R ny = ((co * y + ay * w) + az * x) - ax * z;
+  const R nz = ((co * z + az * w) + ax * y) - ay * x;
+  const R nw = ((co * w - ax * x) - ay * y) - az * z;
+  const R rn = g_rsqrt(nx * nx + ny * ny + nz * nz + nw * nw);   // btQuaternion::normalize
+  s.qx = nx * rn; s.qy = ny * rn; s.qz = nz * rn; s.qw = nw * rn;
+  if (ANGV) { s.ax = s.wx; s.ay = s.wy; s.az = s.wz; }   // getBaseVelocity: world rate
+}
+
 // ---------------------------------------------------------------- one DYN substep
 // The readback that precedes the substep (BaseAviary.py:346-347 -> :517, :836) followed by
 // BaseAviary._dynamics (:815-874) + _integrateQ (:876-889), evaluated on the readback
@@ -500,6 +585,10 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R
         d = q0[0] * q0[0] + q0[1] * q0[1] + q0[2] * q0[2] + q0[3] * q0[3];
       }
     }
+  }
+  if (!FAST && (k.flags & F_BULLET)) {
+    bullet_substep<R, ANGV>(s, rpm, W, last, dwsum, q0, d, c, k);
+    return;
   }
   R inv, Rm[9];
   bool up = true;

@@ -20,14 +20,15 @@ _ACTS = {ActionType.RPM: _lib.GPD_ACT_RPM, ActionType.ONE_D_RPM: _lib.GPD_ACT_ON
          ActionType.ONE_D_PID: _lib.GPD_ACT_ONE_D_PID}
 PID_ACTS = (ActionType.PID, ActionType.VEL, ActionType.ONE_D_PID)
 _TASKS = {"none": _lib.GPD_TASK_NONE, "hover": _lib.GPD_TASK_HOVER, "multihover": _lib.GPD_TASK_MULTIHOVER}
-_AERO = {"gnd": _lib.GPD_F_GND, "drag": _lib.GPD_F_DRAG, "dw": _lib.GPD_F_DW, "geom": _lib.GPD_F_GEOM_WRENCH}
+_AERO = {"gnd": _lib.GPD_F_GND, "drag": _lib.GPD_F_DRAG, "dw": _lib.GPD_F_DW, "geom": _lib.GPD_F_GEOM_WRENCH,
+         "bullet": _lib.GPD_F_BULLET}
 _PHYSICS = {
     Physics.DYN: (),
-    Physics.PYB: ("geom",),
-    Physics.PYB_GND: ("geom", "gnd"),
-    Physics.PYB_DRAG: ("geom", "drag"),
-    Physics.PYB_DW: ("geom", "dw"),
-    Physics.PYB_GND_DRAG_DW: ("geom", "gnd", "drag", "dw"),
+    Physics.PYB: ("bullet",),
+    Physics.PYB_GND: ("bullet", "gnd"),
+    Physics.PYB_DRAG: ("bullet", "drag"),
+    Physics.PYB_DW: ("bullet", "dw"),
+    Physics.PYB_GND_DRAG_DW: ("bullet", "gnd", "drag", "dw"),
 }
 _warned_pyb = False
 
@@ -35,10 +36,13 @@ _warned_pyb = False
 def physics_flags(physics=Physics.DYN, aero=()):
     """Map a reference ``Physics`` value (+ extra force terms) to GPD_F_* flags.
 
-    DYN is the reference's explicit integrator (BaseAviary.py:352-353).  The PYB* values are
-    served by the same explicit integrator with the PYB force placement (``_physics``
-    :679-711) and the requested aero terms; Bullet's own integrator/contact is
-    not reproduced, which is reported once with a warning.
+    DYN is the reference's explicit integrator (BaseAviary.py:352-353).  The PYB* values apply
+    the reference's forces (``_physics`` / ``_groundEffect`` / ``_drag`` / ``_downwash``,
+    :679-811) to a restated Bullet3 multibody base step (``p.stepSimulation``, :369-370; SURVEY
+    §8 f3): default damping, world-frame angular velocity, exponential-map orientation.  Bullet's
+    contacts (ground plane, drone-drone) are not reproduced, which is reported once with a
+    warning.  ``aero`` adds terms by name (``gnd``, ``drag``, ``dw``, ``geom``, ``bullet``), e.g.
+    the aero terms on the DYN integrator (BASELINE config 3).
     """
     global _warned_pyb
     physics = Physics(physics)
@@ -46,9 +50,9 @@ def physics_flags(physics=Physics.DYN, aero=()):
     unknown = terms - set(_AERO)
     if unknown:
         raise ValueError(f"unknown aero terms {sorted(unknown)}; expected a subset of {sorted(_AERO)}")
-    if physics != Physics.DYN and not _warned_pyb:
-        warnings.warn(f"{physics}: forces follow BaseAviary._physics/_groundEffect/_drag/_downwash but are "
-                      "integrated by the explicit DYN integrator (no Bullet damping/contact)", stacklevel=3)
+    if "bullet" in terms and not _warned_pyb:
+        warnings.warn(f"{physics}: Bullet3 multibody step restated without contacts (a drone below the ground "
+                      "plane keeps falling; drones do not collide)", stacklevel=3)
         _warned_pyb = True
     flags = 0
     for t in terms:

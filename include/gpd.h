@@ -82,6 +82,10 @@ extern "C" {
 #define GPD_F_DW 4            /* _downwash      BaseAviary.py:785-811 */
 #define GPD_F_GEOM_WRENCH 8   /* prop thrust torque from URDF prop positions (_physics :679-711)
                                  instead of the DYN formula (:846-851) */
+#define GPD_F_BULLET 16       /* Physics.PYB*: the forces go through a restated Bullet3 btMultiBody
+                                 base step (p.stepSimulation, :369-370; default damping 0.04,
+                                 world-frame angular velocity, exponential-map orientation, velocity
+                                 clamp 100; no contacts) instead of _dynamics; implies GEOM_WRENCH */
 
 /* precision */
 #define GPD_F32 0

@@ -44,6 +44,11 @@ same force terms to the explicit DYN integrator as a body wrench:
   world force         F = R (0,0,T) [+ drag_factors * v] - (0,0,M*G)
 and ``wrench='geom'`` swaps the DYN torque formula (with its roll-sign quirk, :847) for the
 torque Bullet would produce from forces at the URDF prop positions (``_physics``, :679-711).
+
+``integrator='bullet'`` (the ``Physics.PYB*`` modes): the same forces are
+handed to the restated ``btMultiBody`` base step of ``bullet_mb.py`` instead of the explicit
+integrator - forces at the prop links, default multibody damping, world-frame angular velocity,
+Bullet's exponential-map orientation update; no contacts.
 """
 import collections
 import math
@@ -51,6 +56,7 @@ import math
 import numpy as np
 
 from .bullet_math import euler_from_quat, quat_from_euler, quat_roundtrip, quat_to_mat
+from .bullet_mb import multibody_step
 from .params import derived
 from .ref_pid import RefDSLPID, pid_action_rpm
 
@@ -72,7 +78,7 @@ class RefAviary:
 
     def __init__(self, model="cf2x", num_drones=1, initial_xyzs=None, initial_rpys=None,
                  pyb_freq=240, ctrl_freq=30, act="rpm", task="hover", aero=(), wrench="dyn",
-                 episode_len_sec=8):
+                 episode_len_sec=8, integrator="dyn"):
         if pyb_freq % ctrl_freq != 0:
             raise ValueError("[ERROR] in BaseAviary.__init__(), pyb_freq is not divisible by env_freq.")
         p = derived(model)
@@ -93,7 +99,10 @@ class RefAviary:
         self.DW_COEFF_1, self.DW_COEFF_2, self.DW_COEFF_3 = p["dw_coeff_1"], p["dw_coeff_2"], p["dw_coeff_3"]
         self.PROP_POS = np.array(p["prop_pos"])
         self.AERO = set(aero)
-        self.WRENCH = wrench
+        if integrator not in ("dyn", "bullet"):
+            raise ValueError("integrator must be 'dyn' or 'bullet'")
+        self.INTEGRATOR = integrator
+        self.WRENCH = "geom" if integrator == "bullet" else wrench   # Bullet: forces at the prop links
         self.ACT = act
         self.A = ACT_WIDTH[act]
         if act in PID_ACTS:                     # BaseRLAviary.py:73-78, 93-95
@@ -204,8 +213,44 @@ class RefAviary:
                     total = total + (-alpha * np.exp(-.5 * (delta_xy / beta) ** 2))
         return total
 
+    def _bullet_physics(self, rpm, i):
+        """PYB* modes: _physics (:679-711) [+ _groundEffect / _drag / _downwash, :715-811] as
+        forces on the links, then one p.stepSimulation() (:369-370) restated by
+        bullet_mb.multibody_step.  Body frame: prop forces (0,0,f_k) at r_k, ground effect
+        (0,0,g_k) at r_k, downwash (0,0,dw) and drag R^T (drag_factors * vel) at the COM link."""
+        forces = np.array(rpm ** 2) * self.KF
+        torques = np.array(rpm ** 2) * self.KM
+        if self.MODEL == "racer":
+            torques = -torques
+        z_torque = (-torques[0] + torques[1] - torques[2] + torques[3])
+        fz = forces[0] + forces[1] + forces[2] + forces[3]
+        tx = 0.0
+        ty = 0.0
+        for k in range(4):
+            tx = tx + self.PROP_POS[k, 1] * forces[k]
+            ty = ty - self.PROP_POS[k, 0] * forces[k]
+        if "gnd" in self.AERO:
+            gz, gx, gy = self._ground_effect_wrench(rpm, i, quat_to_mat(self.quat[i, :]))
+            fz = fz + gz
+            tx = tx + gx
+            ty = ty + gy
+        if "dw" in self.AERO:
+            fz = fz + self._downwash_force(i)
+        f_base = np.array([0.0, 0.0, fz])
+        if "drag" in self.AERO:
+            f_base = f_base + quat_to_mat(self.quat[i, :]).T @ self._drag_force(self.last_clipped_action[i, :], i)
+        p = self.P
+        pos, q_s, vel, omega = multibody_step(self._b_pos[i], self._b_quat[i], self._b_vel[i], self._b_angv[i],
+                                              f_base, np.array([tx, ty, z_torque]),
+                                              np.array([0.0, 0.0, -p["G"]]) * self.M, self.M,
+                                              np.array([p["ixx"], p["iyy"], p["izz"]]), self.PYB_TIMESTEP)
+        self._b_pos[i], self._b_quat[i], self._b_vel[i], self._b_angv[i] = pos, q_s, vel, omega
+        self.rpy_rates[i, :] = omega
+
     def _dynamics(self, rpm, i):
         """BaseAviary._dynamics (:815-874) (+ optional aero wrench, see module doc)."""
+        if self.INTEGRATOR == "bullet":
+            return self._bullet_physics(rpm, i)
         pos = self.pos[i, :]
         quat = self.quat[i, :]
         vel = self.vel[i, :]
@@ -321,8 +366,10 @@ class RefAviary:
     def step(self, action):
         action = np.asarray(action, dtype=np.float32).reshape(self.NUM_DRONES, self.A)
         clipped_action = np.reshape(self._preprocessAction(action), (self.NUM_DRONES, 4))
+        # :346 - plain PYB skips the readback between substeps (its forces do not read it)
+        plain_pyb = self.INTEGRATOR == "bullet" and not self.AERO
         for _ in range(self.PYB_STEPS_PER_CTRL):
-            if self.PYB_STEPS_PER_CTRL > 1:
+            if self.PYB_STEPS_PER_CTRL > 1 and not plain_pyb:
                 self._updateAndStoreKinematicInformation()
             for i in range(self.NUM_DRONES):
                 self._dynamics(clipped_action[i, :], i)
@@ -363,12 +410,14 @@ class RefAviary:
 
     def set_raw_state(self, raw):
         """Seed the physics-client state from a raw [N, 20] array laid out as gpd_get_raw_state:
-        pos(3) quat_as_stored(4) vel(3) rpy_rates(3) ang_v(3) last_clipped_action(4)."""
+        pos(3) quat_as_stored(4) vel(3) rpy_rates(3) ang_v(3) last_clipped_action(4).  With the
+        Bullet integrator rpy_rates(3) is the world angular velocity the step integrates."""
         raw = np.asarray(raw, dtype=np.float64).reshape(self.NUM_DRONES, 20)
         self._b_pos = raw[:, 0:3].copy()
         self._b_quat = raw[:, 3:7].copy()
         self._b_vel = raw[:, 7:10].copy()
         self.rpy_rates = raw[:, 10:13].copy()
-        self._b_angv = raw[:, 13:16].copy()
+        # Bullet: slots 10..12 hold the integrated world angular velocity (m_realBuf[0:3])
+        self._b_angv = raw[:, 10:13].copy() if self.INTEGRATOR == "bullet" else raw[:, 13:16].copy()
         self.last_clipped_action = raw[:, 16:20].copy()
         self._updateAndStoreKinematicInformation()

@@ -36,32 +36,35 @@ def raw_states(rng, n, z=1.0, tilt=0.3, spin=2.0):
     return raw
 
 
-def integrate_fixture(name, n, T, every, aero=(), z=1.0, scale=1.0, seed=0, drones_per_env=1, xyz=None):
+def integrate_fixture(name, n, T, every, aero=(), z=1.0, scale=1.0, seed=0, drones_per_env=1, xyz=None,
+                      integrator="dyn"):
     rng = np.random.default_rng(seed)
     actions = (rng.uniform(-1, 1, (T, n, 4)) * scale).astype(np.float32)
     rpm = rpm_from_action(HOVER, actions)
     if drones_per_env == 1:
         raw0 = raw_states(rng, n, z=z)
-        env = RefAviary(num_drones=n, task="none", aero=aero)
+        env = RefAviary(num_drones=n, task="none", aero=aero, integrator=integrator)
         env.set_raw_state(raw0)
         traj = env.integrate(rpm)
     else:
         raw0 = np.zeros((0, 20))
-        traj = np.concatenate([RefAviary(num_drones=drones_per_env, task="none", aero=aero, initial_xyzs=xyz)
+        traj = np.concatenate([RefAviary(num_drones=drones_per_env, task="none", aero=aero, initial_xyzs=xyz,
+                                         integrator=integrator)
                                .integrate(rpm[:, e * drones_per_env:(e + 1) * drones_per_env])
                                for e in range(n // drones_per_env)], axis=1)
     np.savez_compressed(os.path.join(HERE, name), actions=actions, raw0=raw0, every=every,
                         aero=np.array(list(aero), dtype="U8"), drones_per_env=drones_per_env,
-                        init_xyzs=np.zeros((0, 3)) if xyz is None else xyz,
+                        init_xyzs=np.zeros((0, 3)) if xyz is None else xyz, integrator=integrator,
                         traj=traj[every - 1::every])
 
 
-def step_fixture(name, n_envs, T, act, task, D=1, seed=0, wrench="dyn", scale=1.0):
+def step_fixture(name, n_envs, T, act, task, D=1, seed=0, integrator="dyn", scale=1.0):
     rng = np.random.default_rng(seed)
     A = ACT_WIDTH[act]
     actions = (rng.uniform(-1, 1, (T, n_envs, D, A)) * scale).astype(np.float32)
     envs = []
-    obs, rew, te, tr, tobs = run_vec(actions, n_envs, drones_per_env=D, act=act, task=task, wrench=wrench, envs=envs)
+    obs, rew, te, tr, tobs = run_vec(actions, n_envs, drones_per_env=D, act=act, task=task, integrator=integrator,
+                                     envs=envs)
     extra = {}
     if hasattr(envs[0], "ctrl"):
         extra["ctrl_state"] = np.concatenate([e.ctrl_state() for e in envs])
@@ -71,7 +74,7 @@ def step_fixture(name, n_envs, T, act, task, D=1, seed=0, wrench="dyn", scale=1.
     np.savez_compressed(os.path.join(HERE, name), actions=actions, obs=obs, reward=rew, terminated=te,
                         truncated=tr, terminal_keys=np.array(keys, dtype=np.int64).reshape(-1, 2),
                         terminal_obs=np.array([tobs[k] for k in keys], dtype=np.float32).reshape(len(keys), D, W),
-                        wrench=wrench, **extra)
+                        integrator=integrator, **extra)
 
 
 def main():
@@ -81,14 +84,18 @@ def main():
     step_fixture("hover_rpm_8env.npz", 8, 60, "rpm", "hover", seed=3)
     step_fixture("multihover_2x2.npz", 2, 60, "rpm", "multihover", D=2, seed=4)
     # DSLPIDControl action types; the VEL loop is chaotic, so its horizon is short
-    step_fixture("pid_waypoint_pyb.npz", 4, 60, "pid", "hover", seed=8, wrench="geom", scale=0.5)
+    step_fixture("pid_waypoint_pyb.npz", 4, 60, "pid", "hover", seed=8, integrator="bullet", scale=0.5)
     step_fixture("one_d_pid_dyn.npz", 4, 60, "one_d_pid", "hover", seed=9)
-    step_fixture("vel_pyb.npz", 4, 16, "vel", "hover", seed=10, wrench="geom")
+    step_fixture("vel_pyb.npz", 4, 16, "vel", "hover", seed=10, integrator="bullet")
+    # Physics.PYB (HoverAviary's default): restated Bullet multibody step, RPM actions
+    step_fixture("c1_hover_rpm_pyb.npz", 1, 150, "rpm", "hover", seed=12, integrator="bullet")
     # raw DYN integrator, 5 s (1200 substeps), every 10th substep kept
     integrate_fixture("integrate_dyn_5s.npz", n=8, T=1200, every=10, seed=5)
     integrate_fixture("integrate_gnd_drag.npz", n=8, T=600, every=10, aero=("gnd", "drag"), z=0.06, scale=0.5, seed=6)
     i = np.arange(8)
     xyz = np.stack([0.15 * np.cos(2 * np.pi * i / 8), 0.15 * np.sin(2 * np.pi * i / 8), 0.5 + 0.1 * i], 1)
+    integrate_fixture("integrate_pyb_gnd_drag.npz", n=8, T=600, every=10, aero=("gnd", "drag"), z=0.06, scale=0.5,
+                      seed=13, integrator="bullet")
     integrate_fixture("integrate_downwash_8.npz", n=8, T=600, every=10, aero=("dw",), scale=0.3, seed=7,
                       drones_per_env=8, xyz=xyz)
 

@@ -10,16 +10,19 @@ from oracle.ref_aviary import RefAviary
 
 
 def state_rel_err(a, b):
-    """Per-drone relative L2 error of the state (SURVEY §8(d) gate): pos, quat (sign
-    canonicalised to w >= 0), rpy, vel, ang_v - columns 0..15 of the 20-float state vector.
+    """Per-drone relative L2 error of the state (SURVEY §8(d) gate): pos, quat, rpy, vel, ang_v -
+    columns 0..15 of the 20-float state vector.  q and -q are the same orientation, so the
+    quaternion difference is taken with the sign of b that is closer to a (canonicalising both to
+    w >= 0 would flip one of two nearly equal quaternions whose w straddles 0 near 180 deg).
     The last_clipped_action columns (16..19) are inputs, not integrated state, and are left out
     so that their ~1.4e4 magnitude cannot hide errors."""
     a = np.array(a, dtype=np.float64)[..., :16]
     b = np.array(b, dtype=np.float64)[..., :16]
-    for x in (a, b):
-        s = np.where(x[..., 6:7] < 0, -1.0, 1.0)
-        x[..., 3:7] *= s
-    num = np.linalg.norm(a - b, axis=-1)
+    d = a - b
+    dq_flip = a[..., 3:7] + b[..., 3:7]
+    flip = (dq_flip ** 2).sum(-1, keepdims=True) < (d[..., 3:7] ** 2).sum(-1, keepdims=True)
+    d[..., 3:7] = np.where(flip, dq_flip, d[..., 3:7])
+    num = np.linalg.norm(d, axis=-1)
     den = np.maximum(np.linalg.norm(b, axis=-1), 1e-6)
     return num / den
 

@@ -38,7 +38,9 @@ def test_physics_flag_mapping():
     assert physics_flags(Physics.DYN, ("gnd", "drag")) == _lib.GPD_F_GND | _lib.GPD_F_DRAG
     with pytest.warns(UserWarning):
         f = physics_flags(Physics.PYB_GND_DRAG_DW)
-    assert f == _lib.GPD_F_GND | _lib.GPD_F_DRAG | _lib.GPD_F_DW | _lib.GPD_F_GEOM_WRENCH
+    assert f == _lib.GPD_F_GND | _lib.GPD_F_DRAG | _lib.GPD_F_DW | _lib.GPD_F_BULLET
+    assert physics_flags(Physics.PYB) == _lib.GPD_F_BULLET
+    assert physics_flags(Physics.DYN, ("geom",)) == _lib.GPD_F_GEOM_WRENCH   # PYB force placement on DYN
     with pytest.raises(ValueError):
         physics_flags(Physics.DYN, ("bogus",))
 

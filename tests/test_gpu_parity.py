@@ -108,8 +108,7 @@ def test_integrate_geom_wrench_parity():
     raw0 = _random_raw(rng, n)
     rpms = _rpms(rng, T, n)
     ref = run_integrate(rpms, raw0, wrench="geom")
-    from gym_pybullet_drones_routing_amd.enums import Physics
-    sim = _sim(n_envs=n, task="none", precision="f64", physics=Physics.PYB)
+    sim = _sim(n_envs=n, task="none", precision="f64", aero=("geom",))   # PYB force placement on DYN
     sim.set_raw_state(raw0)
     traj = sim.integrate(rpms, record=True).cpu().numpy()
     assert state_rel_err(traj, ref).max() <= TOL["f64"]

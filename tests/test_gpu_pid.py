@@ -9,7 +9,7 @@ controller state (integral errors, last_rpy; abs <= 1e-9).
 Note: on Physics.DYN the reference's cf2x roll-sign quirk (BaseAviary.py:847) makes the DSL
 PID unstable in roll, so those episodes end in truncations within a few steps - exercised
 here on purpose (auto-resets, controllers persisting across resets); Physics.PYB (prop
-placement of _physics) flies.
+placement of _physics, restated Bullet multibody step) flies.
 """
 import numpy as np
 import pytest
@@ -56,8 +56,8 @@ def test_pid_step_parity(act, physics):
         acts = acts[:16]
         T = 16
     envs = []
-    wrench = "geom" if physics == "pyb" else "dyn"
-    obs_r, rew_r, te_r, tr_r, tobs_r = run_vec(acts, E, act=act, wrench=wrench, envs=envs)
+    integrator = "bullet" if physics == "pyb" else "dyn"
+    obs_r, rew_r, te_r, tr_r, tobs_r = run_vec(acts, E, act=act, integrator=integrator, envs=envs)
     sim = _sim(n_envs=E, task="hover", precision="f64", act=ActionType(act), physics=Physics(physics))
     assert sim.obs.shape == (E, 1, 12 + 15 * WIDTH[act])
     n_done = 0
@@ -73,7 +73,11 @@ def test_pid_step_parity(act, physics):
             n_done += 1
             np.testing.assert_allclose(tobs[e], tobs_r[(t, e)], rtol=1e-5, atol=1e-6)
     err = state_rel_err(sim.state20().cpu().numpy(), _oracle_state20(envs))
-    assert err.max() <= 1e-10, err.max()
+    # PID waypoints on PYB: in the oracle itself a 1e-13 rad/s perturbation of one body rate
+    # grows to 2.8e-8 over these 60 steps (4e-10 in a second env), so rounding-level differences
+    # (the kernel's world-frame Bullet form, the controller's rotation round trip) end near 2e-10
+    gate = 1e-8 if (act, physics) == ("pid", "pyb") else 1e-10
+    assert err.max() <= gate, err.max()
     cs_r = np.concatenate([e.ctrl_state() for e in envs])
     np.testing.assert_allclose(sim.ctrl_state().cpu().numpy(), cs_r, rtol=1e-9, atol=1e-9)
     if physics == "dyn" and act != "one_d_pid":
@@ -102,14 +106,14 @@ def test_pid_coefficients_and_ctrl_state_seeding():
     E, T = 6, 20
     acts = (rng.uniform(-1, 1, (T, E, 1, 3)) * 0.4).astype(np.float32)
     from oracle.ref_aviary import RefAviary
-    envs = [RefAviary(act="pid", task="hover", wrench="geom") for _ in range(E)]
+    envs = [RefAviary(act="pid", task="hover", integrator="bullet") for _ in range(E)]
     cs0 = rng.normal(0, 0.05, (E, 9))
     gains = dict(p_coeff_pos=np.array([.5, .5, 1.5]), d_coeff_att=np.array([15000., 15000., 10000.]))
     for e, env in enumerate(envs):
         env.set_ctrl_state(cs0[e])
         env.ctrl[0].P_COEFF_FOR = gains["p_coeff_pos"]
         env.ctrl[0].D_COEFF_TOR = gains["d_coeff_att"]
-    obs_r, rew_r, te_r, tr_r, _ = run_vec(acts, E, act="pid", wrench="geom", envs=envs)
+    obs_r, rew_r, te_r, tr_r, _ = run_vec(acts, E, act="pid", integrator="bullet", envs=envs)
     sim = _sim(n_envs=E, task="hover", precision="f64", act=ActionType.PID, physics=Physics.PYB)
     sim.set_ctrl_state(torch.from_numpy(cs0).cuda())
     sim.set_pid_coefficients(**gains)
