@@ -10,8 +10,12 @@ advantage normalisation, TimeLimit bootstrapping from ``terminal_observation``) 
 env surface: ``make_vec_env(..., output="torch")`` returns observations, rewards and done
 masks as device tensors, so the whole loop (policy, env step, GAE, update) stays on the GPU.
 
-    python examples/learn.py                     # HoverAviary, 4096 envs, ONE_D_RPM
+    python examples/learn.py                     # HoverAviary, 4096 envs, ONE_D_RPM, Physics.PYB
     python examples/learn.py --multiagent true   # MultiHoverAviary, 2 drones
+    python examples/learn.py --physics dyn       # the explicit DYN integrator instead
+
+Physics defaults to the env classes' default, Physics.PYB (the reference's learn.py does not
+pass one), i.e. the restated Bullet multibody step.
 
 Evaluation follows the reference's EvalCallback(deterministic=True): the mean action of the
 policy on a fresh single env, the return of one full episode.
@@ -61,11 +65,11 @@ class ActorCritic(nn.Module):
         return self.vf(obs).squeeze(-1)
 
 
-def evaluate(policy, multiagent, device, act):
+def evaluate(policy, multiagent, device, act, physics=Physics.PYB):
     """EvalCallback(deterministic=True, n_eval_episodes=1): one episode of a fresh env."""
     D = DEFAULT_AGENTS if multiagent else 1
     sim = BatchedAviarySim(n_envs=1, drones_per_env=D, task="multihover" if multiagent else "hover",
-                           act=act, physics=Physics.DYN, autoreset=False, device=device)
+                           act=act, physics=physics, autoreset=False, device=device)
     obs = sim.reset().clone()
     ret, steps = 0.0, 0
     with torch.no_grad():
@@ -84,10 +88,11 @@ def evaluate(policy, multiagent, device, act):
 def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), lr=3e-4, epochs=10,
           minibatch=16384, gamma=0.99, gae_lambda=0.95, clip=0.2, vf_coef=0.5, max_grad_norm=0.5,
           eval_every=2, seed=0, device="cuda:0", act=DEFAULT_ACT, target_reward=None, max_seconds=None,
-          log=print):
+          log=print, physics=Physics.PYB):
     torch.manual_seed(seed)
     env_cls = MultiHoverAviary if multiagent else HoverAviary
-    kw = dict(obs=DEFAULT_OBS, act=act)
+    physics = Physics(physics)
+    kw = dict(obs=DEFAULT_OBS, act=act, physics=physics)
     if multiagent:
         kw["num_drones"] = DEFAULT_AGENTS
     env = make_vec_env(env_cls, env_kwargs=kw, n_envs=n_envs, seed=seed, output="torch", device=device)
@@ -166,7 +171,7 @@ def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), l
                "rollout_s": round(t_upd - t_roll, 3), "update_s": round(time.time() - t_upd, 3),
                "wall_s": round(time.time() - t0, 1)}
         if it % eval_every == 0:
-            er, el = evaluate(policy, multiagent, device, act)
+            er, el = evaluate(policy, multiagent, device, act, physics)
             rec.update(eval_return=er, eval_len=el)
             best = max(best, er)
         history.append(rec)
@@ -186,12 +191,13 @@ def main():
     p.add_argument("--n_envs", type=int, default=4096)
     p.add_argument("--total_timesteps", type=float, default=2e8)
     p.add_argument("--max_seconds", type=float, default=None)
+    p.add_argument("--physics", default="pyb", help="Physics value (default: pyb, the env classes' default)")
     p.add_argument("--output", default=None, help="JSON file for the training history")
     a = p.parse_args()
     multi = str(a.multiagent).lower() in ("1", "true", "yes")
     policy, hist, best, target = train(multiagent=multi, n_envs=a.n_envs, total_timesteps=int(a.total_timesteps),
-                                       max_seconds=a.max_seconds)
-    out = {"multiagent": multi, "n_envs": a.n_envs, "target_reward": target, "best_eval_return": best,
+                                       max_seconds=a.max_seconds, physics=Physics(a.physics))
+    out = {"multiagent": multi, "physics": a.physics, "n_envs": a.n_envs, "target_reward": target, "best_eval_return": best,
            "reached": best >= target, "history": hist}
     print(json.dumps({k: v for k, v in out.items() if k != "history"}))
     if a.output:

@@ -129,5 +129,5 @@ def make_vec_env(env_cls, n_envs=1, seed=None, env_kwargs=None, **vec_kwargs):
         raise ValueError(f"no batched implementation for {env_cls}")
     for k in ("gui", "record", "neighbourhood_radius"):
         kw.pop(k, None)
-    kw.setdefault("physics", Physics.DYN)
+    kw.setdefault("physics", Physics.PYB)   # the env classes' default (HoverAviary.py:20, MultiHoverAviary.py:22)
     return AviaryVecEnv(n_envs, task=task, num_drones=nd, **kw, **vec_kwargs)

@@ -112,7 +112,8 @@ def test_multihover_aviary_surface():
 def test_vec_env_sb3_semantics(output):
     from gym_pybullet_drones_routing_amd.envs import HoverAviary, make_vec_env
     fx = np.load(os.path.join(GOLDEN, "hover_rpm_8env.npz"))
-    venv = make_vec_env(HoverAviary, n_envs=8, output=output)
+    from gym_pybullet_drones_routing_amd.enums import Physics
+    venv = make_vec_env(HoverAviary, n_envs=8, output=output, env_kwargs=dict(physics=Physics.DYN))
     obs = venv.reset()
     assert tuple(obs.shape) == (8, 1, 72)
     keys = {tuple(k): i for i, k in enumerate(fx["terminal_keys"])}
