@@ -258,12 +258,17 @@ __device__ __forceinline__ float with_sign_word(float mag, int kw) {
 }
 
 // The substep's readback for a quaternion with |q|^2 = d within UnitTol of 1 (dyn_substep
-// re-normalises any other lane first): inv = +-1/|q| with Bullet's sign rule and the rotation
-// matrix entries the substep uses - the third column (thrust direction) and, with FULL, all nine
-// (world-frame ang_v).  The sign key is chosen on the high words only (one select per candidate);
-// the key is never +-0 for a unit quaternion (trace > 0 gives w^2 > 1/4, else the component of
-// the largest diagonal entry has square >= 1/12), so its sign bit is the "< 0" test.
-template <typename R, bool FULL>
+// re-normalises any other lane first): inv = 1/|q| and the rotation matrix entries the substep
+// uses - the third column (thrust direction) and, with FULL, all nine (world-frame ang_v).
+// SIGN: apply Bullet's sign rule to inv (w > 0 when trace > 0, else the component of the largest
+// diagonal entry positive).  The substeps do not need it: the rotation matrix, the attitude
+// predicates and the force terms are quadratic in q, and _integrateQ is linear in q, so a
+// quaternion carried with the opposite sign gives bit-identical physics and a stored quaternion
+// of the opposite sign; the step's final readback (readback_fused) applies the rule for the
+// observation and the state vector.  The sign key is chosen on the high words only (one select
+// per candidate); it is never +-0 for a unit quaternion (trace > 0 gives w^2 > 1/4, else the
+// component of the largest diagonal entry has square >= 1/12), so its sign bit is the "< 0" test.
+template <typename R, bool FULL, bool SIGN = true>
 __device__ __forceinline__ void readback_unit(R x, R y, R z, R w, R d, R& inv, R m[9]) {
   const R inv0 = R(1.5) - R(0.5) * d;                   // 1/|q| (one Newton step from 1)
   const R s = R(2) * (R(2) - d);                         // 2/|q|^2
@@ -271,16 +276,24 @@ __device__ __forceinline__ void readback_unit(R x, R y, R z, R w, R d, R& inv, R
   const R wx = w * xs, wy = w * ys, wz = w * zs;
   const R xx = x * xs, xy = x * ys, xz = x * zs;
   const R yy = y * ys, yz = y * zs, zz = z * zs;
-  m[0] = R(1) - (yy + zz); m[2] = xz + wy;
-  m[4] = R(1) - (xx + zz); m[5] = yz - wx;
+  m[2] = xz + wy;
+  m[5] = yz - wx;
   m[8] = R(1) - (xx + yy);
+  if (FULL || SIGN) {
+    m[0] = R(1) - (yy + zz);
+    m[4] = R(1) - (xx + zz);
+  }
   if (FULL) {
     m[1] = xy - wz; m[3] = xy + wz; m[6] = xz - wy; m[7] = yz + wx;
   }
-  const R trace = m[0] + m[4] + m[8];
-  int kw = m[0] < m[4] ? (m[4] < m[8] ? hi_word(z) : hi_word(y)) : (m[0] < m[8] ? hi_word(z) : hi_word(x));
-  kw = trace > R(0) ? hi_word(w) : kw;
-  inv = with_sign_word(inv0, kw);
+  if (SIGN) {
+    const R trace = m[0] + m[4] + m[8];
+    int kw = m[0] < m[4] ? (m[4] < m[8] ? hi_word(z) : hi_word(y)) : (m[0] < m[8] ? hi_word(z) : hi_word(x));
+    kw = trace > R(0) ? hi_word(w) : kw;
+    inv = with_sign_word(inv0, kw);
+  } else {
+    inv = inv0;
+  }
 }
 
 template <typename R>
@@ -490,7 +503,7 @@ template <typename R, bool ANGV>
 __device__ __forceinline__ void bullet_substep(Drone<R>& s, const R rpm[4], const R W[4], const R last[4], R dwsum,
                                                R q0[4], R d, const Consts<R>& c, const DynK<R>& k) {
   R inv, Rm[9];
-  readback_unit<R, true>(q0[0], q0[1], q0[2], q0[3], d, inv, Rm);
+  readback_unit<R, true, false>(q0[0], q0[1], q0[2], q0[3], d, inv, Rm);
   bool up = true;
   if (k.flags & F_GND) {   // |self.rpy[0,1]| < pi/2, :742
     const R qn[4] = {q0[0] * inv, q0[1] * inv, q0[2] * inv, q0[3] * inv};
@@ -593,7 +606,7 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R
   R inv, Rm[9];
   bool up = true;
   auto readback = [&]() {
-    readback_unit<R, ANGV || !FAST>(q0[0], q0[1], q0[2], q0[3], d, inv, Rm);
+    readback_unit<R, ANGV || !FAST, false>(q0[0], q0[1], q0[2], q0[3], d, inv, Rm);
     if (!FAST && (k.flags & F_GND)) {   // |self.rpy[0,1]| < pi/2, :742
       const R qn[4] = {q0[0] * inv, q0[1] * inv, q0[2] * inv, q0[3] * inv};
       up = upright(attitude_args(qn));
@@ -646,7 +659,8 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R
   s.pz = s.pz + k.dt * s.vz;
   // q' = M(omega) (inv q0) = M'(omega) q0 with the readback's 1/|q| folded into M's entries;
   // below the isclose threshold P = Q = R = 0 and co = 1 exactly (t2 <= 1e-16), so q' = inv q0,
-  // the readback quaternion itself, as the reference's skip leaves it
+  // the readback quaternion itself (up to Bullet's sign, see readback_unit), as the reference's
+  // skip leaves it
   auto update = [&](R co_, R sh_) {
     const R shi = sh_ * inv;
     const R P = rot ? p * shi : R(0), Q = rot ? q * shi : R(0), Rr = rot ? r * shi : R(0);
