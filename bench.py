@@ -129,15 +129,22 @@ def cpu_baseline_openmp(E, seconds=5.0, act="rpm", threads=16):
 
 def time_graph(sim, pool, steps, warmup, per_graph=16):
     """Timed region in hipGraph mode: one graph = `per_graph` consecutive env.step() launches
-    reading distinct pre-filled action slots.  A HIP event pair on the launch stream brackets
-    the replays, so (event time / launches) is the step kernel's average duration including the
-    in-graph kernel boundary (an upper bound; rocprofv3 reports the kernel alone).
-    Returns (wall seconds, steps run, kernel us)."""
+    reading distinct pre-filled action slots, plus one graph of the remaining steps % per_graph
+    launches, so that exactly `steps` steps are timed (and `warmup` untimed ones run first).
+    A HIP event pair on the launch stream brackets the replays, so (event time / launches) is
+    the step kernel's average duration including the in-graph kernel boundary (an upper bound;
+    rocprofv3 reports the kernel alone).  Returns (wall seconds, steps run, kernel us)."""
     P = pool.shape[0]
+    steps = max(1, int(steps))
+    per_graph = min(per_graph, steps)
+    reps, rem = divmod(steps, per_graph)
     graph = sim.capture_graph([pool[k % P] for k in range(per_graph)])
-    reps = max(1, steps // per_graph)
-    for _ in range(max(1, warmup // per_graph)):
+    tail = sim.capture_graph([pool[k % P] for k in range(rem)]) if rem else None
+    wreps, wrem = divmod(max(0, int(warmup)), per_graph)
+    for _ in range(wreps):
         graph.replay()
+    for k in range(wrem):
+        sim.step(pool[k % P])
     stream = torch.cuda.current_stream(sim.device)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(sim.device)
@@ -148,12 +155,14 @@ def time_graph(sim, pool, steps, warmup, per_graph=16):
     ev0.record(stream)
     for _ in range(reps):
         graph.replay()
+    if tail is not None:
+        tail.replay()
     ev1.record(stream)
     torch.cuda.synchronize(sim.device)
     wall = time.perf_counter() - t0
     if torch.distributed.is_initialized():
         torch.distributed.barrier()
-    return wall, reps * per_graph, 1000.0 * ev0.elapsed_time(ev1) / (reps * per_graph)
+    return wall, steps, 1000.0 * ev0.elapsed_time(ev1) / steps
 
 
 def time_steps(sim, pool, steps, warmup):
@@ -321,7 +330,7 @@ def main():
         "value": value, "unit": "drone*dt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f32" if args.precision == "f32" else "f64", "data": "synthetic",
-        "mode": "eager launches" if args.eager else "hipGraph replay, 16 env.step launches per graph",
+        "mode": "eager launches" if args.eager else "hipGraph replay, 16 env.step launches per graph (+ one graph of the remainder)",
         "config": {"workload": f"{E} HoverAviary envs per GPU (cf2x, Physics.DYN, ActionType.{args.act.upper()}, "
                                f"240/30 Hz = {nsub} substeps/step, U[-1,1] actions, SB3 auto-reset)",
                    "n_envs_per_gpu": E, "global_envs": E * world, "drones_per_env": 1,

@@ -132,6 +132,21 @@ int main() {
   run<2>(d_out, d_cyc, iters);
   run<4>(d_out, d_cyc, iters);
   run<8>(d_out, d_cyc, iters);
+  {  // the same 8 chains on a 16-lane wave (thin blocks): does the issue cost follow EXEC?
+    long long c16 = 0;
+    for (int rep = 0; rep < 3; ++rep) {
+      fma_chains<8><<<1, 16>>>(d_out, d_cyc, iters, 0.999999, 1e-7);
+      hipDeviceSynchronize();
+    }
+    hipMemcpy(&c16, d_cyc, 8, hipMemcpyDeviceToHost);
+    printf("f64 fma, 8 chains, 16-lane wave: %.2f cycles per instruction\n", c16 / ((double)iters * 16 * 8));
+    for (int rep = 0; rep < 3; ++rep) {
+      fma_chains<1><<<1, 16>>>(d_out, d_cyc, iters, 0.999999, 1e-7);
+      hipDeviceSynchronize();
+    }
+    hipMemcpy(&c16, d_cyc, 8, hipMemcpyDeviceToHost);
+    printf("f64 fma, 1 chain, 16-lane wave: %.2f cycles per instruction\n", c16 / ((double)iters * 16));
+  }
   long long cyc = 0;
   for (int rep = 0; rep < 3; ++rep) {
     mul_chain32<<<1, 64>>>((float*)d_out, d_cyc, iters, 0.999999f, 1e-7f);
