@@ -63,6 +63,15 @@ def pmc_traffic(grid, precision):
     return best
 
 
+def step_kernel_name(sim, rbytes, act):
+    """The step kernel a plain-DYN single-drone sim launches (rocprofv3 name)."""
+    real = "double" if rbytes == 8 else "float"
+    a = 0 if act == "rpm" else 1
+    if sim.constants.lanes_per_block == 128:
+        return "gpd::step_kernel_duo<%s, %d>" % (real, a)
+    return "gpd::step_kernel<%s, %d, false, true>" % (real, a)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -342,12 +351,11 @@ def main():
         "ctrl_steps_per_s": world * E * args.steps / wall,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "traffic_unit": "bytes per launch",
-                     "kernel": "gpd::step_kernel<%s, %d, false, true>" % ("double" if rbytes == 8 else "float",
-                                                                         0 if args.act == "rpm" else 1),
+                     "kernel": step_kernel_name(sim, rbytes, args.act),
                      "alg_bytes_per_launch": alg},
     }
 
-    grid_lanes = -(-sim.n_drones // sim.constants.drones_per_block) * 64   # launch geometry of the step kernel
+    grid_lanes = -(-sim.n_drones // sim.constants.drones_per_block) * sim.constants.lanes_per_block  # launch geometry
     result["roofline"]["grid_lanes"] = grid_lanes
     tr = pmc_traffic(grid_lanes, args.precision)
     if tr is not None:

@@ -22,7 +22,7 @@ GPD_EUNSUPPORTED = -4
 
 GPD_MODEL_CF2X, GPD_MODEL_CF2P, GPD_MODEL_RACE = 0, 1, 2
 GPD_ACT_RPM, GPD_ACT_ONE_D_RPM, GPD_ACT_PID, GPD_ACT_VEL, GPD_ACT_ONE_D_PID = 0, 1, 2, 3, 4
-GPD_ABI_VERSION = 2
+GPD_ABI_VERSION = 3
 CTRL_COMPS = 9  # integral_pos_e(3) integral_rpy_e(3) last_rpy(3)
 GPD_TASK_NONE, GPD_TASK_HOVER, GPD_TASK_MULTIHOVER = 0, 1, 2
 GPD_F_GND, GPD_F_DRAG, GPD_F_DW, GPD_F_GEOM_WRENCH, GPD_F_BULLET = 1, 2, 4, 8, 16
@@ -75,7 +75,7 @@ class Constants(ctypes.Structure):
         "gravity", "hover_rpm", "max_rpm", "max_thrust", "max_xy_torque", "max_z_torque",
         "gnd_eff_h_clip", "pyb_timestep", "ctrl_timestep")] + [(n, ctypes.c_int) for n in (
             "pyb_steps_per_ctrl", "action_buffer_size", "obs_width", "act_width", "n_drones",
-            "trunc_step_counter", "drones_per_block")]
+            "trunc_step_counter", "drones_per_block", "lanes_per_block")]
 
 
 _lib = None

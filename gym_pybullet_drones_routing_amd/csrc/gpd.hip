@@ -116,6 +116,7 @@ struct gpd_sim {
   int tile_bytes = 0;             // dynamic LDS of the step kernel
   int wt = 0;                     // SimView::wt (write-through store policy)
   int nc_magic = 0;               // SimView::nc_magic
+  bool duo = false;               // step launches step_kernel_duo (two waves per block)
   DwPairs dw_pairs{0, 0};         // SimView::dw_pairs
   double bound_xy;
   std::vector<double> init_tmpl;  // [D][10]
@@ -215,6 +216,9 @@ const void* step_fn_pid(bool multi) {
 }
 template <typename R>
 const void* step_kernel_fn(const gpd_sim* s) {
+  if (s->duo)
+    return s->cfg.act_type == GPD_ACT_RPM ? (const void*)step_kernel_duo<R, ACT_RPM>
+                                          : (const void*)step_kernel_duo<R, ACT_ONE_D_RPM>;
   const bool multi = s->D > 1;
   const bool fast = s->cfg.physics_flags == 0;
   switch (s->cfg.act_type) {
@@ -258,7 +262,8 @@ int launch_step(gpd_sim* s, const float* actions, float* obs, float* reward, uin
   const size_t lds = (size_t)s->tile_bytes;
   typedef void (*StepFn)(R*, const float*, int2*, const Consts<R>*, long long, int, int, SimView<R>, StepIO<R>);
   const StepFn f = (StepFn)step_kernel_fn<R>(s);
-  hipLaunchKernelGGL(f, dim3(grid), dim3(kWave), lds, st, v.state, io.actions, v.ctr, c, v.npad, v.N, v.tpb, v, io);
+  hipLaunchKernelGGL(f, dim3(grid), dim3(s->duo ? 2 * kWave : kWave), lds, st, v.state, io.actions, v.ctr, c, v.npad,
+                     v.N, v.tpb, v, io);
   HIP_TRY(hipGetLastError());
   return GPD_OK;
 }
@@ -442,6 +447,17 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
         delete s;
         return fail(GPD_EUNSUPPORTED, "gpd_create: observation width not supported by the tile copy-out");
       }
+    // two-wave step (step_kernel_duo) for the plain-DYN single-drone RPM path when blocks are
+    // thin (too few envs to give every CU a full wave: the launch is one wave's instruction
+    // stream long); its 128-lane copy-out needs t / NC for t <= 128.  GPD_DUO=0/1 overrides.
+    bool duo = s->D == 1 && C.physics_flags == 0 &&
+               (C.act_type == GPD_ACT_RPM || C.act_type == GPD_ACT_ONE_D_RPM) && s->tpb < kWave;
+    const char* ov = std::getenv("GPD_DUO");
+    if (ov) duo = std::atoi(ov) != 0 && s->D == 1 && C.physics_flags == 0 &&
+                  (C.act_type == GPD_ACT_RPM || C.act_type == GPD_ACT_ONE_D_RPM);
+    for (int t = 0; t <= 2 * kWave && duo; ++t)
+      if ((t * s->nc_magic) >> 16 != t / NC) duo = false;
+    s->duo = duo;
   }
   if (s->tile_bytes > 160 * 1024) {
     delete s;
@@ -469,6 +485,7 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   K.act_width = s->A;
   K.n_drones = s->N;
   K.drones_per_block = s->tpb;
+  K.lanes_per_block = s->duo ? 2 * kWave : kWave;
   {  // truncated iff step_counter / PYB_FREQ > EPISODE_LEN_SEC  (HoverAviary.py:114)
     long long sc = (long long)std::floor(C.episode_len_sec * C.pyb_freq);
     if (sc < 0) sc = 0;

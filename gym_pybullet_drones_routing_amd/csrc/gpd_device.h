@@ -688,6 +688,87 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R
   }
 }
 
+// ---------------------------------------------------------------- FAST substep, split in two
+// Without aero terms the body torques are the propeller wrench alone, so dyn_substep<R, true>
+// falls into two dependency chains that meet once per substep: the body-rate chain (ω and the
+// _integrateQ weights) reads nothing of the pose, and the pose chain (readback, v, p, q) needs
+// only the rate chain's weights for its quaternion update.  step_kernel_duo runs them on two
+// waves.  The operations and their order are dyn_substep's, so results are bit-identical.
+//
+// Rate half: ω' = ω + dt J⁻¹(τ − ω×Jω) (:852-856) and the weights of _integrateQ(q, ω', dt)
+// (:876-889): h = {cos θ, sin θ/|ω'|, p, q, r} with (p, q, r) = ω' above the np.isclose threshold
+// and 0 below it (then cos θ = 1 exactly: the pose half's update returns q/|q|).
+template <typename R>
+__device__ __forceinline__ void rate_half(R& wx, R& wy, R& wz, const R W[4], const DynK<R>& k, R h[5]) {
+  const R jwx = k.jx * wx, jwy = k.jy * wy, jwz = k.jz * wz;
+  const R cx = wy * jwz - wz * jwy;
+  const R cy = wz * jwx - wx * jwz;
+  const R cz = wx * jwy - wy * jwx;
+  const R dwx = k.ijx * (W[1] - cx), dwy = k.ijy * (W[2] - cy), dwz = k.ijz * (W[3] - cz);
+  wx = wx + k.dt * dwx;
+  wy = wy + k.dt * dwy;
+  wz = wz + k.dt * dwz;
+  const R n2 = wx * wx + wy * wy + wz * wz;
+  const bool rot = n2 > R(1e-16);
+  const R t2 = n2 * k.hdt2;
+  R co, sc;
+  cos_sinc(t2, co, sc);
+  R sh = k.hdt * sc;
+  const bool big = t2 >= R(0.25);
+  if (GPD_RARE(__ballot(big) != 0ull)) {
+    if (big) {
+      const R nrm = g_sqrt(n2), th = nrm * k.hdt;
+      co = g_cos(th);
+      sh = g_sin(th) / nrm;
+    }
+  }
+  h[0] = co; h[1] = sh;
+  h[2] = rot ? wx : R(0); h[3] = rot ? wy : R(0); h[4] = rot ? wz : R(0);
+}
+
+// Pose half: the readback of q (1/|q| and the thrust direction; with ANGV all nine entries for
+// the world-frame ang_v of the rates w = ω'), semi-implicit Euler of v and p (:839-841,
+// :855-859) and q' = M(ω') q/|q| from the rate half's weights h.
+template <typename R, bool ANGV>
+__device__ __forceinline__ void pose_half(Drone<R>& s, R fz, const R h[5], const R w[3], const DynK<R>& k) {
+  R q0[4] = {s.qx, s.qy, s.qz, s.qw};
+  R d = q0[0] * q0[0] + q0[1] * q0[1] + q0[2] * q0[2] + q0[3] * q0[3];
+  {
+    const bool unit = g_abs(d - R(1)) < UnitTol<R>::v;   // as in dyn_substep
+    if (GPD_RARE(__ballot(!unit) != 0ull)) {
+      if (!unit) {
+        const R r = g_rsqrt(d);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q0[i] = q0[i] * r;
+        d = q0[0] * q0[0] + q0[1] * q0[1] + q0[2] * q0[2] + q0[3] * q0[3];
+      }
+    }
+  }
+  R inv, Rm[9];
+  readback_unit<R, ANGV, false>(q0[0], q0[1], q0[2], q0[3], d, inv, Rm);
+  R Fx = Rm[2] * fz, Fy = Rm[5] * fz, Fz = Rm[8] * fz;
+  Fz = Fz - k.gravity;
+  s.vx = s.vx + k.dt * (Fx * k.inv_m);
+  s.vy = s.vy + k.dt * (Fy * k.inv_m);
+  s.vz = s.vz + k.dt * (Fz * k.inv_m);
+  s.px = s.px + k.dt * s.vx;
+  s.py = s.py + k.dt * s.vy;
+  s.pz = s.pz + k.dt * s.vz;
+  const R shi = h[1] * inv;
+  const R P = h[2] * shi, Q = h[3] * shi, Rr = h[4] * shi;
+  const R C = h[0] * inv;
+  const R x = q0[0], y = q0[1], z = q0[2], ww = q0[3];
+  s.qx = ((C * x + Rr * y) - Q * z) + P * ww;
+  s.qy = ((-Rr * x + C * y) + P * z) + Q * ww;
+  s.qz = ((Q * x - P * y) + C * z) + Rr * ww;
+  s.qw = ((-P * x - Q * y) - Rr * z) + C * ww;
+  if (ANGV) {
+    s.ax = (Rm[0] * w[0] + Rm[1] * w[1]) + Rm[2] * w[2];
+    s.ay = (Rm[3] * w[0] + Rm[4] * w[1]) + Rm[5] * w[2];
+    s.az = (Rm[6] * w[0] + Rm[7] * w[1]) + Rm[8] * w[2];
+  }
+}
+
 // Summed downwash on drone (px,py,pz) from the env's D drones whose positions sit in LDS
 // (BaseAviary._downwash :798-811).  A wave-wide ballot skips the α/β/exp block whenever no
 // lane of the wave has an active pair (Δz > 0 ∧ Δxy < 10) for neighbour j.

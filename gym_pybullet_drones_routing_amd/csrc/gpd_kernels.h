@@ -211,6 +211,94 @@ __host__ __device__ inline int step_tile_bytes(int A, int ring_len) {
   return A == 4 ? (3 + ring_len) * kPad * 16 : (12 + ring_len * A) * kPad * 4;
 }
 
+// Copy-out of the observation tile: the block's nact rows of NC columns (float4 columns for
+// A == 4, float otherwise), streamed by NL lanes with coalesced (write-through with wt & 1)
+// stores; rows flagged in done_rows also go to terminal_obs (their non-state columns - the
+// state part was stored from registers).  t / NC is (t * nc_magic) >> 16 for t <= NL.
+template <int A, int NL>
+__device__ __forceinline__ void tile_copy_out(const float4* tile4, const float* tilef, int lane, int nact, int NC,
+                                              int nc_magic, int wt, unsigned long long done_rows, float* obs,
+                                              float* terminal_obs, long long n0) {
+  // lane `lane` streams tile elements g = lane, lane+NL, ... (row-major over the block's rows),
+  // six LDS reads in flight per batch.  Branch-free for obs: a lane whose element index passes the
+  // end re-stores the last element (same address, same value).  Rows of envs that finished
+  // this step are also written to terminal_obs (state columns from the extra tile columns).
+  const int total = nact * NC;
+  const int drow = (NL * nc_magic) >> 16, dcol = NL - drow * NC;
+  int row = (lane * nc_magic) >> 16;
+  int col = lane - row * NC;
+  constexpr int U = 6;
+  const int last_row = nact - 1, last_col = NC - 1;
+  const int ncs = A == 4 ? 3 : 12;  // state columns
+  for (int g0 = lane; g0 - lane < total; g0 += U * NL) {
+    if (A == 4) {
+      float4 val[U];
+      int idx[U];
+      int rr[U], cc[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = g0 + u * NL < total;
+        rr[u] = ok ? row : last_row;
+        cc[u] = ok ? col : last_col;
+        val[u] = tile4[__umul24(cc[u], kPad) + rr[u]];   // 24-bit multiply: full-rate VALU
+        idx[u] = ok ? g0 + u * NL : total - 1;
+        col += dcol; row += drow;
+        if (col >= NC) { col -= NC; ++row; }
+      }
+      GPD_STAMP(8);
+      float4* dst = reinterpret_cast<float4*>(obs) + n0 * NC;
+      if (wt & 1) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, 0, total * 16, 0x00020000);
+#pragma unroll
+        for (int u = 0; u < U; ++u) store_wt(r, idx[u] * 16, val[u]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) dst[idx[u]] = val[u];
+      }
+      GPD_STAMP(9);
+      if (done_rows) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if ((done_rows >> rr[u]) & 1ull) {
+            if (cc[u] >= ncs) reinterpret_cast<float4*>(terminal_obs)[n0 * NC + idx[u]] = val[u];
+          }
+        }
+      }
+    } else {
+      float val[U];
+      int idx[U];
+      int rr[U], cc[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = g0 + u * NL < total;
+        rr[u] = ok ? row : last_row;
+        cc[u] = ok ? col : last_col;
+        val[u] = tilef[__umul24(cc[u], kPad) + rr[u]];
+        idx[u] = ok ? g0 + u * NL : total - 1;
+        col += dcol; row += drow;
+        if (col >= NC) { col -= NC; ++row; }
+      }
+      float* dst = obs + n0 * NC;
+      if (wt & 1) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, 0, total * 4, 0x00020000);
+#pragma unroll
+        for (int u = 0; u < U; ++u) store_wt(r, idx[u] * 4, val[u]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) dst[idx[u]] = val[u];
+      }
+      if (done_rows) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if ((done_rows >> rr[u]) & 1ull) {
+            if (cc[u] >= ncs) terminal_obs[n0 * NC + idx[u]] = val[u];
+          }
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // gpd_step: one env.step() for every env (BaseAviary.py:259-383) in ONE launch.
 // ACT: action type (GPD_ACT_*); PID types run DSLPIDControl before the substeps.
@@ -446,86 +534,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
   }
   __syncthreads();
   GPD_STAMP(6);
-  {
-    // lane tid streams tile elements g = tid, tid+64, ... (row-major over the block's rows), six
-    // LDS reads in flight per batch.  Branch-free for obs: a lane whose element index passes the
-    // end re-stores the last element (same address, same value).  Rows of envs that finished
-    // this step are also written to terminal_obs (state columns from the extra tile columns).
-    const int total = nact * NC;
-    const int drow = (kWave * v.nc_magic) >> 16, dcol = kWave - drow * NC;
-    int row = (tid * v.nc_magic) >> 16;
-    int col = tid - row * NC;
-    constexpr int U = 6;
-    const int last_row = nact - 1, last_col = NC - 1;
-    const int ncs = A == 4 ? 3 : 12;  // state columns
-    for (int g0 = tid; g0 - tid < total; g0 += U * kWave) {
-      if (A == 4) {
-        float4 val[U];
-        int idx[U];
-        int rr[U], cc[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const bool ok = g0 + u * kWave < total;
-          rr[u] = ok ? row : last_row;
-          cc[u] = ok ? col : last_col;
-          val[u] = tile4[__umul24(cc[u], kPad) + rr[u]];   // 24-bit multiply: full-rate VALU
-          idx[u] = ok ? g0 + u * kWave : total - 1;
-          col += dcol; row += drow;
-          if (col >= NC) { col -= NC; ++row; }
-        }
-        GPD_STAMP(8);
-        float4* dst = reinterpret_cast<float4*>(io.obs) + n0 * NC;
-        if (v.wt & 1) {
-          const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, 0, total * 16, 0x00020000);
-#pragma unroll
-          for (int u = 0; u < U; ++u) store_wt(r, idx[u] * 16, val[u]);
-        } else {
-#pragma unroll
-          for (int u = 0; u < U; ++u) dst[idx[u]] = val[u];
-        }
-        GPD_STAMP(9);
-        if (done_rows) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            if ((done_rows >> rr[u]) & 1ull) {
-              if (cc[u] >= ncs) reinterpret_cast<float4*>(io.terminal_obs)[n0 * NC + idx[u]] = val[u];
-            }
-          }
-        }
-      } else {
-        float val[U];
-        int idx[U];
-        int rr[U], cc[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const bool ok = g0 + u * kWave < total;
-          rr[u] = ok ? row : last_row;
-          cc[u] = ok ? col : last_col;
-          val[u] = tilef[__umul24(cc[u], kPad) + rr[u]];
-          idx[u] = ok ? g0 + u * kWave : total - 1;
-          col += dcol; row += drow;
-          if (col >= NC) { col -= NC; ++row; }
-        }
-        float* dst = io.obs + n0 * NC;
-        if (v.wt & 1) {
-          const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, 0, total * 4, 0x00020000);
-#pragma unroll
-          for (int u = 0; u < U; ++u) store_wt(r, idx[u] * 4, val[u]);
-        } else {
-#pragma unroll
-          for (int u = 0; u < U; ++u) dst[idx[u]] = val[u];
-        }
-        if (done_rows) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            if ((done_rows >> rr[u]) & 1ull) {
-              if (cc[u] >= ncs) io.terminal_obs[n0 * NC + idx[u]] = val[u];
-            }
-          }
-        }
-      }
-    }
-  }
+  tile_copy_out<A, kWave>(tile4, tilef, tid, nact, NC, v.nc_magic, v.wt, done_rows, io.obs, io.terminal_obs, n0);
   GPD_STAMP(7);
   GPD_RSTAMP(12);
   if (!active) return;
@@ -541,6 +550,247 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
     io.trunc[e] = trunc ? 1 : 0;
     v.ctr[e] = make_int2(do_reset ? 0 : sc + c.nsub, head + 1 == v.ring_len ? 0 : head + 1);
   }
+}
+
+// Workgroup barrier for LDS hand-offs between the waves of a block: waits for this wave's own
+// LDS operations only.  __syncthreads() (a workgroup release fence) would also wait for every
+// vector-memory operation in flight, including an LDS-DMA that nobody reads until much later.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// ---------------------------------------------------------------------------------------
+// step_kernel_duo: step_kernel<R, ACT, false, true> (single-drone envs, plain DYN, RPM action
+// types: the bench path) with every drone's work split over TWO waves of one workgroup.
+// With few envs per CU (4096 envs: one 16-drone wave per CU) a launch lasts as long as one
+// wave's serial instruction stream, and a substep is ~115 issue-bound f64 instructions.
+// Without aero terms it falls into two chains (rate_half / pose_half, gpd_device.h):
+//   wave 1 (rates): ω' and the _integrateQ weights, handed over through LDS;
+//   wave 0 (pose):  readback, v, p, and the quaternion update with those weights.
+// One barrier per substep; the hand-off is double-buffered by substep parity, so wave 1
+// computes substep k+1 while wave 0 finishes substep k.  Wave 1 also issues the history DMA
+// after its first substep and writes the current action (ring + tile); both waves stream the
+// tile copy-out.  Same operations as step_kernel<R, ACT, false, true>, same results.
+template <typename R, int ACT>
+__global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ state_p,
+                                                             const float* __restrict__ actions_p,
+                                                             int2* __restrict__ ctr_p, const Consts<R>* __restrict__ cp,
+                                                             long long npad_p, int n_p, int tpb_p, SimView<R> v,
+                                                             StepIO<R> io) {
+  static_assert(!act_is_pid(ACT), "the duo kernel serves the RPM action types");
+  v.state = state_p; v.ctr = ctr_p; v.npad = npad_p; v.N = n_p; v.tpb = tpb_p;
+  io.actions = actions_p;
+  constexpr int A = act_width(ACT);
+  extern __shared__ float4 tile4[];
+  float* tilef = reinterpret_cast<float*>(tile4);
+  __shared__ R shand[2][5][kWave];        // rate_half -> pose_half, by substep parity
+  __shared__ R sw[3][kWave];              // rpy_rates after the last substep
+  __shared__ unsigned long long sdone;    // done-row mask of the block (tile rows)
+  GPD_RSTAMP(11);
+  GPD_STAMP(0);
+  const Consts<R>& c = *cp;
+  const int tid = threadIdx.x & (kWave - 1);
+  const bool rate_wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >= kWave;   // wave-uniform
+  const long long n0 = (long long)blockIdx.x * v.tpb;
+  const long long n = n0 + tid;
+  const int nact = (int)((v.N - n0) < v.tpb ? (v.N - n0) : v.tpb);
+  const bool active = tid < nact;
+  const long long nn = active ? n : 0;   // inactive lanes compute on drone 0 and store nothing
+  const int nsub = c.nsub;
+  const int nh = v.ring_len - 1;
+  const int NC = A == 4 ? 3 + v.ring_len : 12 + v.ring_len * A;
+
+  float a[A];
+  if (A == 4) {
+    const float4 a4 = *reinterpret_cast<const float4*>(io.actions + nn * 4);
+    a[0] = a4.x; a[1] = a4.y; a[2] = a4.z; a[3] = a4.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < A; ++j) a[j] = io.actions[nn * A + j];
+  }
+  const R* st = v.state + tidx(nn, 0, kStateComps);
+  const DynK<R> dk = dyn_consts(c);
+
+  if (rate_wave) {
+    // ------------------------------------------------------------ wave 1: body rates
+    R wx = st[10 * 64], wy = st[11 * 64], wz = st[12 * 64];
+    const int head = v.ctr[nn].y;
+    asm volatile("" ::"s"(v.ring));
+    R rpm[4], W[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) rpm[k] = (R)action_to_rpm(dk.hover_f32, a[A == 4 ? k : 0]);
+    rpm_wrench<R, true>(rpm, dk, c, W);
+    for (int k = 0; k < nsub; ++k) {
+      R h[5];
+      rate_half(wx, wy, wz, W, dk, h);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) shand[k & 1][j][tid] = h[j];
+      if (k == nsub - 1) { sw[0][tid] = wx; sw[1][tid] = wy; sw[2][tid] = wz; }
+      lds_barrier();   // hand-off k published
+    }
+    // history ring -> obs tile (LDS-DMA): issued once the last hand-off is out, it lands while
+    // the pose wave finishes its last substep, the final readback and the task hooks.  The
+    // env's ring slots are 64*A floats apart in its 64-drone tile.
+    {
+      const float* rb = v.ring + ridx(nn, 0, v.ring_len, A);
+      int slot = head + 1 == v.ring_len ? 0 : head + 1;
+      for (int m = 0; m < nh; ++m) {
+        const float* src = rb + slot * (64 * A);
+        if (A == 4) {
+          __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tile4 + (3 + m) * kPad), 16, 0, 0);
+        } else {
+#pragma unroll
+          for (int j = 0; j < A; ++j)
+            __builtin_amdgcn_global_load_lds((gbl_void_ptr)(src + j), (lds_void_ptr)(tilef + (12 + m * A + j) * kPad), 4,
+                                             0, 0);
+        }
+        slot = slot + 1 == v.ring_len ? 0 : slot + 1;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // history DMA has landed in the tile
+    if (active) {      // current action into the ring (deque.append); the DMA never reads `head`
+      float* ring_cur = v.ring + ridx(n, head, v.ring_len, A);
+      if (A == 4) *reinterpret_cast<float4*>(ring_cur) = make_float4(a[0], a[1], a[2], a[3]);
+      else
+#pragma unroll
+        for (int j = 0; j < A; ++j) ring_cur[j] = a[j];
+    }
+    if (A == 4) {
+      tile4[(3 + nh) * kPad + tid] = make_float4(a[0], a[1], a[2], a[3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < A; ++j) tilef[(12 + nh * A + j) * kPad + tid] = a[j];
+    }
+    lds_barrier();     // tile complete, sdone published
+    tile_copy_out<A, 2 * kWave>(tile4, tilef, threadIdx.x, nact, NC, v.nc_magic, v.wt, sdone, io.obs,
+                                io.terminal_obs, n0);
+#ifdef GPD_STAMPS
+    {   // diagnostic: the rate wave's end (realtime) into phase 13
+      __builtin_amdgcn_sched_barrier(0);
+      unsigned long long t_;
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+      if (tid == 0 && blockIdx.x < 65536) g_stamps[blockIdx.x * kStampPhases + 13] = t_;
+    }
+#endif
+    return;
+  }
+
+  // -------------------------------------------------------------- wave 0: pose
+  Drone<R> s;
+  R last[4];
+  load_drone(v, nn, s, last, false);
+  const int2 cv = v.ctr[nn];
+  const int sc = cv.x;          // step_counter
+  const int head = cv.y;        // ring slot receiving this step's action
+  asm volatile("" ::"s"(v.task), "s"(io.trunc));
+#ifdef GPD_STAMPS
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // diagnostic: loads landed
+  GPD_STAMP(10);
+#endif
+  R fz;
+  {
+    R rpm[4], W[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) rpm[k] = (R)action_to_rpm(dk.hover_f32, a[A == 4 ? k : 0]);
+    rpm_wrench<R, true>(rpm, dk, c, W);
+    fz = W[0];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
+  }
+  const R wnone[3] = {R(0), R(0), R(0)};
+  for (int k = 0; k < nsub - 1; ++k) {
+    lds_barrier();   // hand-off k
+    R h[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) h[j] = shand[k & 1][j][tid];
+    pose_half<R, false>(s, fz, h, wnone, dk);
+    if (k == 0) GPD_STAMP(1);
+  }
+  {
+    lds_barrier();   // last hand-off + final rates
+    const int k = nsub - 1;
+    R h[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) h[j] = shand[k & 1][j][tid];
+    s.wx = sw[0][tid]; s.wy = sw[1][tid]; s.wz = sw[2][tid];
+    const R w[3] = {s.wx, s.wy, s.wz};
+    pose_half<R, true>(s, fz, h, w, dk);
+  }
+  GPD_STAMP(2);
+  // final readback (:374) -> obs / reward / done
+  R qn[4], Rm[9];
+  readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
+  const AttitudeArgs<R> att = attitude_args(qn);
+  float roll, pitch, yaw;
+  obs_euler_f32(qn, att, roll, pitch, yaw);
+  float reward = -1.0f;
+  bool term = false, trunc = false;
+  if (v.task != TASK_NONE) {
+    const R* tg = c.target0;
+    const R tx = tg[0] - s.px, ty = tg[1] - s.py, tz = tg[2] - s.pz;
+    const R d2 = tx * tx + ty * ty + tz * tz;
+    R r = R(2) - d2 * d2;
+    r = r > R(0) ? r : R(0);
+    const bool oob = g_abs(s.px) > v.bound_xy || g_abs(s.py) > v.bound_xy || s.pz > R(2) ||
+                     tilted_beyond(att, R(0.38941834230865049), R(0.42279321873816178));  // sin/tan(0.4)
+    reward = (float)r;
+    term = d2 < R(1e-8);
+    trunc = oob || sc >= v.trunc_sc;
+  }
+  const bool done = term || trunc;
+  const bool do_reset = done && v.autoreset;
+  float row12[12] = {(float)s.px, (float)s.py, (float)s.pz, roll, pitch, yaw,
+                     (float)s.vx, (float)s.vy, (float)s.vz, (float)s.ax, (float)s.ay, (float)s.az};
+  GPD_STAMP(3);
+  GPD_STAMP(4);
+  if (do_reset) {
+    if (active && io.terminal_obs != nullptr) {
+      float* trow = io.terminal_obs + n * v.W;
+      if (A == 4) {
+        float4* t4 = reinterpret_cast<float4*>(trow);
+        t4[0] = make_float4(row12[0], row12[1], row12[2], row12[3]);
+        t4[1] = make_float4(row12[4], row12[5], row12[6], row12[7]);
+        t4[2] = make_float4(row12[8], row12[9], row12[10], row12[11]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) trow[k] = row12[k];
+      }
+    }
+    const R* ini = c.init0;
+    s.px = ini[0]; s.py = ini[1]; s.pz = ini[2];
+    s.qx = ini[3]; s.qy = ini[4]; s.qz = ini[5]; s.qw = ini[6];
+    s.vx = s.vy = s.vz = R(0);
+    s.wx = s.wy = s.wz = R(0);
+    s.ax = s.ay = s.az = R(0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) last[k] = R(0);
+    row12[0] = (float)ini[0]; row12[1] = (float)ini[1]; row12[2] = (float)ini[2];
+    row12[3] = (float)ini[7]; row12[4] = (float)ini[8]; row12[5] = (float)ini[9];
+#pragma unroll
+    for (int k = 6; k < 12; ++k) row12[k] = 0.0f;
+  }
+  const unsigned long long done_rows = __ballot(do_reset && active && io.terminal_obs != nullptr);
+  if (A == 4) {
+    tile4[0 * kPad + tid] = make_float4(row12[0], row12[1], row12[2], row12[3]);
+    tile4[1 * kPad + tid] = make_float4(row12[4], row12[5], row12[6], row12[7]);
+    tile4[2 * kPad + tid] = make_float4(row12[8], row12[9], row12[10], row12[11]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) tilef[k * kPad + tid] = row12[k];
+  }
+  if (tid == 0) sdone = done_rows;
+  GPD_STAMP(5);
+  lds_barrier();     // tile complete, sdone published
+  GPD_STAMP(6);
+  tile_copy_out<A, 2 * kWave>(tile4, tilef, threadIdx.x, nact, NC, v.nc_magic, v.wt, done_rows, io.obs,
+                              io.terminal_obs, n0);
+  GPD_STAMP(7);
+  GPD_RSTAMP(12);
+  if (!active) return;
+  if (v.wt & 2) store_drone_wt(v, n, s, last);
+  else store_drone(v, n, s, last);
+  io.reward[n] = reward;
+  io.term[n] = term ? 1 : 0;
+  io.trunc[n] = trunc ? 1 : 0;
+  v.ctr[n] = make_int2(do_reset ? 0 : sc + c.nsub, head + 1 == v.ring_len ? 0 : head + 1);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define GPD_ABI_VERSION 2
+#define GPD_ABI_VERSION 3
 
 /* return codes */
 #define GPD_OK 0
@@ -123,7 +123,8 @@ typedef struct gpd_constants {
   double pyb_timestep, ctrl_timestep;
   int pyb_steps_per_ctrl, action_buffer_size, obs_width, act_width, n_drones;
   int trunc_step_counter;    /* smallest step_counter with step_counter/PYB_FREQ > EPISODE_LEN_SEC */
-  int drones_per_block;      /* drones per 64-lane block of the step kernel (launch geometry) */
+  int drones_per_block;      /* drones per block of the step kernel (launch geometry) */
+  int lanes_per_block;       /* step kernel block size: 64, or 128 for the two-wave kernel */
 } gpd_constants;
 
 /* DSLPIDControl coefficients and constants (control/DSLPIDControl.py:37-60; GRAVITY and KF

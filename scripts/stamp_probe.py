@@ -38,6 +38,11 @@ for prec in os.environ.get("STAMP_PRECS", "f64 f32").split():
               f"{int((tot > np.median(tot) + 1000).sum())} of {len(tot)}", flush=True)
         # s_memrealtime (100 MHz, shared by the device): block start spread and first-start -> last-end span
         rs, re_ = t[:, 11], t[:, 12]
+        if sim.constants.lanes_per_block == 128 and t[:, 13].min() > 0:   # two-wave kernel: rate wave's end
+            rw = t[:, 13] - rs
+            print(f"    rate wave ends {int(np.median(t[:, 13] - re_)) * 10} ns after the pose wave (median), "
+                  f"duration median {int(np.median(rw)) * 10} ns", flush=True)
+            re_ = np.maximum(re_, t[:, 13])
         if rs.min() > 0:
             print(f"    realtime: start spread {(rs.max() - rs.min()) * 10} ns, block duration median "
                   f"{int(np.median(re_ - rs)) * 10} ns max {int((re_ - rs).max()) * 10} ns, span {(re_.max() - rs.min()) * 10} ns",
