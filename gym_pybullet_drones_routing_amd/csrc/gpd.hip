@@ -447,11 +447,14 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
         delete s;
         return fail(GPD_EUNSUPPORTED, "gpd_create: observation width not supported by the tile copy-out");
       }
-    // two-wave step (step_kernel_duo) for the plain-DYN single-drone RPM path when blocks are
-    // thin (too few envs to give every CU a full wave: the launch is one wave's instruction
-    // stream long); its 128-lane copy-out needs t / NC for t <= 128.  GPD_DUO=0/1 overrides.
+    // two-wave step (step_kernel_duo) for the plain-DYN single-drone RPM path while the launch
+    // is latency-bound: up to 64K drones (<= 4 blocks per CU).  Measured on one MI355X
+    // (scripts/geom_probe.py): 4096 envs 6.28 -> 5.71 us/step, 16384 envs 7.48 -> 6.49,
+    // 65536 envs 10.45 -> 10.31, but 262144 envs 35.8 -> 38.1 (bandwidth-bound: the second
+    // wave only adds occupancy pressure).  Its 128-lane copy-out needs t / NC for t <= 128.
+    // GPD_DUO=0/1 overrides.
     bool duo = s->D == 1 && C.physics_flags == 0 &&
-               (C.act_type == GPD_ACT_RPM || C.act_type == GPD_ACT_ONE_D_RPM) && s->tpb < kWave;
+               (C.act_type == GPD_ACT_RPM || C.act_type == GPD_ACT_ONE_D_RPM) && s->N <= 65536;
     const char* ov = std::getenv("GPD_DUO");
     if (ov) duo = std::atoi(ov) != 0 && s->D == 1 && C.physics_flags == 0 &&
                   (C.act_type == GPD_ACT_RPM || C.act_type == GPD_ACT_ONE_D_RPM);

@@ -693,7 +693,8 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R
 // falls into two dependency chains that meet once per substep: the body-rate chain (ω and the
 // _integrateQ weights) reads nothing of the pose, and the pose chain (readback, v, p, q) needs
 // only the rate chain's weights for its quaternion update.  step_kernel_duo runs them on two
-// waves.  The operations and their order are dyn_substep's, so results are bit-identical.
+// waves.  The operations and their order are dyn_substep's; results agree to rounding (hipcc
+// contracts a few multiply-adds differently in the two code shapes: 1 ulp in f64).
 //
 // Rate half: ω' = ω + dt J⁻¹(τ − ω×Jω) (:852-856) and the weights of _integrateQ(q, ω', dt)
 // (:876-889): h = {cos θ, sin θ/|ω'|, p, q, r} with (p, q, r) = ω' above the np.isclose threshold

@@ -568,7 +568,8 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // One barrier per substep; the hand-off is double-buffered by substep parity, so wave 1
 // computes substep k+1 while wave 0 finishes substep k.  Wave 1 also issues the history DMA
 // after its first substep and writes the current action (ring + tile); both waves stream the
-// tile copy-out.  Same operations as step_kernel<R, ACT, false, true>, same results.
+// tile copy-out.  Same operations as step_kernel<R, ACT, false, true>; results agree to
+// rounding (tests/test_gpu_parity.py::test_duo_kernel_matches_single_wave).
 template <typename R, int ACT>
 __global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ state_p,
                                                              const float* __restrict__ actions_p,

@@ -143,11 +143,14 @@ def test_downwash_multi_parity(prec):
     sim.close()
 
 
+@pytest.mark.parametrize("kernel", ["duo", "single"])
 @pytest.mark.parametrize("prec", ["f64", "f32"])
 @pytest.mark.parametrize("act", ["rpm", "one_d_rpm"])
-def test_step_parity_hover(prec, act):
-    """HoverAviary step(): obs / reward / terminated / truncated with SB3 auto-reset."""
+def test_step_parity_hover(prec, act, kernel, monkeypatch):
+    """HoverAviary step(): obs / reward / terminated / truncated with SB3 auto-reset, through the
+    two-wave step kernel (the default up to 64K drones) and the single-wave one (larger N)."""
     from gym_pybullet_drones_routing_amd.enums import ActionType
+    monkeypatch.setenv("GPD_DUO", "1" if kernel == "duo" else "0")
     rng = np.random.default_rng(4)
     E, T = 16, 80
     A = 4 if act == "rpm" else 1
@@ -158,6 +161,7 @@ def test_step_parity_hover(prec, act):
         acts[:, 4:6] = 1.0   # full collective thrust: climbs through z > 2 -> truncation + reset
     obs_r, rew_r, te_r, tr_r, tobs_r = run_vec(acts, E, act=act)
     sim = _sim(n_envs=E, task="hover", precision=prec, act=ActionType(act))
+    assert sim.constants.lanes_per_block == (128 if kernel == "duo" else 64)
     obs0 = sim.obs.cpu().numpy()
     assert obs0.shape == (E, 1, 12 + 15 * A)
     n_done = 0
@@ -180,6 +184,43 @@ def test_step_parity_hover(prec, act):
             np.testing.assert_allclose(tobs[e], tobs_r[(t, e)], rtol=1e-4, atol=1e-4)
     assert n_done > 0, "test inputs should force at least one auto-reset"
     sim.close()
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+@pytest.mark.parametrize("act", ["rpm", "one_d_rpm"])
+def test_duo_kernel_matches_single_wave(prec, act, monkeypatch):
+    """The two-wave step kernel runs dyn_substep's operations split over two waves: the same
+    obs, reward, done flags and state as the single-wave kernel up to rounding (hipcc contracts
+    a few multiply-adds differently in the two code shapes: measured 1 ulp in f64).  Ragged env
+    count (the last block is partial), full-range actions (resets, tumbling drones past the
+    small-angle series), 60 steps."""
+    from gym_pybullet_drones_routing_amd.enums import ActionType
+    rng = np.random.default_rng(21)
+    E, T = 100, 60
+    A = 4 if act == "rpm" else 1
+    acts = rng.uniform(-1, 1, (T, E, 1, A)).astype(np.float32)
+    acts[:, :50] *= np.float32(0.1)
+    out = {}
+    for kernel in ("duo", "single"):
+        monkeypatch.setenv("GPD_DUO", "1" if kernel == "duo" else "0")
+        sim = _sim(n_envs=E, task="hover", precision=prec, act=ActionType(act))
+        assert sim.constants.lanes_per_block == (128 if kernel == "duo" else 64)
+        rec = []
+        for t in range(T):
+            o, r, te, tr = sim.step(torch.from_numpy(acts[t]).cuda())
+            rec.append((o.cpu().numpy().copy(), r.cpu().numpy().copy(), te.cpu().numpy().copy(),
+                        tr.cpu().numpy().copy(), sim.terminal_obs.cpu().numpy().copy()))
+        out[kernel] = (rec, sim.state20().cpu().numpy())
+        sim.close()
+    (ra, sa), (rb, sb) = out["duo"], out["single"]
+    tol = 1e-12 if prec == "f64" else 1e-4
+    for t in range(T):
+        (oa, rwa, tea, tra, ta), (ob, rwb, teb, trb, tb) = ra[t], rb[t]
+        np.testing.assert_array_equal(tea, teb, err_msg=f"terminated, step {t}")
+        np.testing.assert_array_equal(tra, trb, err_msg=f"truncated, step {t}")
+        for x, y in ((oa, ob), (rwa, rwb), (ta, tb)):
+            np.testing.assert_allclose(x, y, rtol=tol, atol=tol if prec == "f64" else 1e-5, err_msg=f"step {t}")
+    assert state_rel_err(sa, sb).max() <= tol
 
 
 @pytest.mark.parametrize("D", [2, 8])
