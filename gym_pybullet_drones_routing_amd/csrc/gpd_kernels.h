@@ -214,20 +214,21 @@ __host__ __device__ inline int step_tile_bytes(int A, int ring_len) {
 // Copy-out of the observation tile: the block's nact rows of NC columns (float4 columns for
 // A == 4, float otherwise), streamed by NL lanes with coalesced (write-through with wt & 1)
 // stores; rows flagged in done_rows also go to terminal_obs (their non-state columns - the
-// state part was stored from registers).  t / NC is (t * nc_magic) >> 16 for t <= NL.
-template <int A, int NL>
+// state part was stored from registers).  t / NC is (t * nc_magic) >> 16 for t <= NL.  U tile
+// elements per lane per batch (LDS reads in flight); lanes past the end are masked off.
+template <int A, int NL, int U = 6>
 __device__ __forceinline__ void tile_copy_out(const float4* tile4, const float* tilef, int lane, int nact, int NC,
                                               int nc_magic, int wt, unsigned long long done_rows, float* obs,
                                               float* terminal_obs, long long n0) {
-  // lane `lane` streams tile elements g = lane, lane+NL, ... (row-major over the block's rows),
-  // six LDS reads in flight per batch.  Branch-free for obs: a lane whose element index passes the
-  // end re-stores the last element (same address, same value).  Rows of envs that finished
-  // this step are also written to terminal_obs (state columns from the extra tile columns).
+  // lane `lane` streams tile elements g = lane, lane+NL, ... (row-major over the block's rows).
+  // A lane whose element index passes the end reads the last element and stores nothing (an
+  // exec-masked store; re-storing the last element instead would send up to NL*U writes of one
+  // 16-byte word through one L2 channel).  Rows of envs that finished this step are also
+  // written to terminal_obs (state columns from the extra tile columns).
   const int total = nact * NC;
   const int drow = (NL * nc_magic) >> 16, dcol = NL - drow * NC;
   int row = (lane * nc_magic) >> 16;
   int col = lane - row * NC;
-  constexpr int U = 6;
   const int last_row = nact - 1, last_col = NC - 1;
   const int ncs = A == 4 ? 3 : 12;  // state columns
   for (int g0 = lane; g0 - lane < total; g0 += U * NL) {
@@ -235,13 +236,14 @@ __device__ __forceinline__ void tile_copy_out(const float4* tile4, const float* 
       float4 val[U];
       int idx[U];
       int rr[U], cc[U];
+      bool ok[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const bool ok = g0 + u * NL < total;
-        rr[u] = ok ? row : last_row;
-        cc[u] = ok ? col : last_col;
+        ok[u] = g0 + u * NL < total;
+        rr[u] = ok[u] ? row : last_row;
+        cc[u] = ok[u] ? col : last_col;
         val[u] = tile4[__umul24(cc[u], kPad) + rr[u]];   // 24-bit multiply: full-rate VALU
-        idx[u] = ok ? g0 + u * NL : total - 1;
+        idx[u] = ok[u] ? g0 + u * NL : total - 1;
         col += dcol; row += drow;
         if (col >= NC) { col -= NC; ++row; }
       }
@@ -250,16 +252,18 @@ __device__ __forceinline__ void tile_copy_out(const float4* tile4, const float* 
       if (wt & 1) {
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, 0, total * 16, 0x00020000);
 #pragma unroll
-        for (int u = 0; u < U; ++u) store_wt(r, idx[u] * 16, val[u]);
+        for (int u = 0; u < U; ++u)
+          if (ok[u]) store_wt(r, idx[u] * 16, val[u]);
       } else {
 #pragma unroll
-        for (int u = 0; u < U; ++u) dst[idx[u]] = val[u];
+        for (int u = 0; u < U; ++u)
+          if (ok[u]) dst[idx[u]] = val[u];
       }
       GPD_STAMP(9);
       if (done_rows) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          if ((done_rows >> rr[u]) & 1ull) {
+          if (ok[u] && ((done_rows >> rr[u]) & 1ull)) {
             if (cc[u] >= ncs) reinterpret_cast<float4*>(terminal_obs)[n0 * NC + idx[u]] = val[u];
           }
         }
@@ -268,13 +272,14 @@ __device__ __forceinline__ void tile_copy_out(const float4* tile4, const float* 
       float val[U];
       int idx[U];
       int rr[U], cc[U];
+      bool ok[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const bool ok = g0 + u * NL < total;
-        rr[u] = ok ? row : last_row;
-        cc[u] = ok ? col : last_col;
+        ok[u] = g0 + u * NL < total;
+        rr[u] = ok[u] ? row : last_row;
+        cc[u] = ok[u] ? col : last_col;
         val[u] = tilef[__umul24(cc[u], kPad) + rr[u]];
-        idx[u] = ok ? g0 + u * NL : total - 1;
+        idx[u] = ok[u] ? g0 + u * NL : total - 1;
         col += dcol; row += drow;
         if (col >= NC) { col -= NC; ++row; }
       }
@@ -282,15 +287,17 @@ __device__ __forceinline__ void tile_copy_out(const float4* tile4, const float* 
       if (wt & 1) {
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, 0, total * 4, 0x00020000);
 #pragma unroll
-        for (int u = 0; u < U; ++u) store_wt(r, idx[u] * 4, val[u]);
+        for (int u = 0; u < U; ++u)
+          if (ok[u]) store_wt(r, idx[u] * 4, val[u]);
       } else {
 #pragma unroll
-        for (int u = 0; u < U; ++u) dst[idx[u]] = val[u];
+        for (int u = 0; u < U; ++u)
+          if (ok[u]) dst[idx[u]] = val[u];
       }
       if (done_rows) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          if ((done_rows >> rr[u]) & 1ull) {
+          if (ok[u] && ((done_rows >> rr[u]) & 1ull)) {
             if (cc[u] >= ncs) terminal_obs[n0 * NC + idx[u]] = val[u];
           }
         }
@@ -661,7 +668,7 @@ __global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ sta
       for (int j = 0; j < A; ++j) tilef[(12 + nh * A + j) * kPad + tid] = a[j];
     }
     lds_barrier();     // tile complete, sdone published
-    tile_copy_out<A, 2 * kWave>(tile4, tilef, threadIdx.x, nact, NC, v.nc_magic, v.wt, sdone, io.obs,
+    tile_copy_out<A, 2 * kWave, 3>(tile4, tilef, threadIdx.x, nact, NC, v.nc_magic, v.wt, sdone, io.obs,
                                 io.terminal_obs, n0);
 #ifdef GPD_STAMPS
     {   // diagnostic: the rate wave's end (realtime) into phase 13
@@ -781,7 +788,7 @@ __global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ sta
   GPD_STAMP(5);
   lds_barrier();     // tile complete, sdone published
   GPD_STAMP(6);
-  tile_copy_out<A, 2 * kWave>(tile4, tilef, threadIdx.x, nact, NC, v.nc_magic, v.wt, done_rows, io.obs,
+  tile_copy_out<A, 2 * kWave, 3>(tile4, tilef, threadIdx.x, nact, NC, v.nc_magic, v.wt, done_rows, io.obs,
                               io.terminal_obs, n0);
   GPD_STAMP(7);
   GPD_RSTAMP(12);

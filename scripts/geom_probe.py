@@ -27,8 +27,7 @@ def probe(E, dpb, duo, reps=30, G=16):
     return geo, 1000 * s.elapsed_time(e) / (reps * G)
 
 
-cases = [(4096, 16, 0), (4096, 16, 1), (4096, 8, 1), (4096, 32, 1), (4096, 64, 1), (16384, 64, 0), (16384, 16, 1),
-         (16384, 64, 1), (65536, 64, 0), (65536, 64, 1), (262144, 64, 0), (262144, 64, 1)]
+cases = [tuple(int(x) for x in c.split(",")) for c in os.environ.get("GEOM_CASES", "4096,16,0 4096,16,1 4096,8,1 4096,32,1 4096,64,1 16384,64,0 16384,16,1 16384,64,1 65536,64,0 65536,64,1 262144,64,0 262144,64,1").split()]
 for E, dpb, duo in cases:
     geo, us = probe(E, dpb, duo)
     print(f"E {E:7d} drones/block {geo[0]:2d} lanes/block {geo[1]:3d}: {us:8.2f} us/step  "
