@@ -730,11 +730,14 @@ __device__ __forceinline__ void rate_half(R& wx, R& wy, R& wz, const R W[4], con
 // Pose half: the readback of q (1/|q| and the thrust direction; with ANGV all nine entries for
 // the world-frame ang_v of the rates w = ω'), semi-implicit Euler of v and p (:839-841,
 // :855-859) and q' = M(ω') q/|q| from the rate half's weights h.
-template <typename R, bool ANGV>
+// CHECK: the |q|^2 ~ 1 test of dyn_substep (re-normalising a quaternion set from outside).  Only
+// the first substep of a step needs it: from a quaternion with |d - 1| < UnitTol the update
+// M(ω') q/|q| is orthogonal to rounding, so every later substep starts within a few ulp of 1.
+template <typename R, bool ANGV, bool CHECK>
 __device__ __forceinline__ void pose_half(Drone<R>& s, R fz, const R h[5], const R w[3], const DynK<R>& k) {
   R q0[4] = {s.qx, s.qy, s.qz, s.qw};
   R d = q0[0] * q0[0] + q0[1] * q0[1] + q0[2] * q0[2] + q0[3] * q0[3];
-  {
+  if (CHECK) {
     const bool unit = g_abs(d - R(1)) < UnitTol<R>::v;   // as in dyn_substep
     if (GPD_RARE(__ballot(!unit) != 0ull)) {
       if (!unit) {
