@@ -109,28 +109,32 @@ struct DynK {
   R dt, inv_m, gravity, jx, jy, jz, ijx, ijy, ijz, hdt, hdt2;
   R kf, km, L, Ls2;        // propeller wrench (rpm_wrench)
   float hover_f32;         // action -> RPM
-  int model, flags;
+  int model, flags, nsub;
 };
 template <typename R>
 __device__ __forceinline__ R vpin(R x) {
   asm volatile("" : "+v"(x));
   return x;
 }
+// warm0 / warm1: optional kernel-argument values to have in SGPRs by the same wait (their
+// scalar loads then go out in the same batch as the constant block's).
 template <typename R>
-__device__ __forceinline__ DynK<R> dyn_consts(const Consts<R>& c) {
+__device__ __forceinline__ DynK<R> dyn_consts(const Consts<R>& c, int warm0 = 0, const void* warm1 = nullptr) {
   DynK<R> k;
   k.dt = c.dt; k.inv_m = c.inv_m; k.gravity = c.gravity;
   k.jx = c.jx; k.jy = c.jy; k.jz = c.jz;
   k.ijx = c.ijx; k.ijy = c.ijy; k.ijz = c.ijz;
   k.hdt = c.hdt; k.hdt2 = c.hdt2;
   k.kf = c.kf; k.km = c.km; k.L = c.L; k.Ls2 = c.Ls2; k.hover_f32 = c.hover_f32; k.model = c.model;
-  k.flags = c.flags;
+  k.flags = c.flags; k.nsub = c.nsub;
   // one statement for all of them: hipcc issues the scalar loads of every constant-block line
   // back to back and waits once (K$ misses in parallel), instead of a load + wait pair per use
   // behind each model / flag branch
   asm volatile("" : "+v"(k.dt), "+v"(k.inv_m), "+v"(k.gravity), "+v"(k.jx), "+v"(k.jy), "+v"(k.jz),
                "+v"(k.ijx), "+v"(k.ijy), "+v"(k.ijz), "+v"(k.hdt), "+v"(k.hdt2), "+v"(k.kf), "+v"(k.km),
-               "+v"(k.L), "+v"(k.Ls2), "+v"(k.hover_f32), "+s"(k.model), "+s"(k.flags));
+               "+v"(k.L), "+v"(k.Ls2), "+v"(k.hover_f32), "+s"(k.model), "+s"(k.flags),
+               "+s"(k.nsub)
+               : "s"(warm0), "s"(warm1));
   return k;
 }
 

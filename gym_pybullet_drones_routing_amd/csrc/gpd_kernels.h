@@ -411,19 +411,19 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
   rpm_wrench<R, FAST>(rpm, dk, c, W);
   // substeps 1..nsub-1 skip the (write-only) world ang_v; the last one produces it
   // (the first substep is peeled so the loop body stays one basic block)
-  if (c.nsub > 1) {
+  if (dk.nsub > 1) {
     substep_block<R, MULTI, FAST, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
     GPD_STAMP(1);
     history_dma();
-    for (int it = 1; it < c.nsub - 1; ++it)
+    for (int it = 1; it < dk.nsub - 1; ++it)
       substep_block<R, MULTI, FAST, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
   }
   substep_block<R, MULTI, FAST, true>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
 #pragma unroll
   for (int k = 0; k < 4; ++k) last[k] = rpm[k];
-  if (c.nsub == 1) history_dma();
+  if (dk.nsub == 1) history_dma();
   GPD_STAMP(2);
   // final readback (:374) -> obs / reward / done
   R qn[4], Rm[9];
@@ -555,7 +555,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
     io.reward[e] = reward;
     io.term[e] = term ? 1 : 0;
     io.trunc[e] = trunc ? 1 : 0;
-    v.ctr[e] = make_int2(do_reset ? 0 : sc + c.nsub, head + 1 == v.ring_len ? 0 : head + 1);
+    v.ctr[e] = make_int2(do_reset ? 0 : sc + dk.nsub, head + 1 == v.ring_len ? 0 : head + 1);
   }
 }
 
@@ -603,9 +603,6 @@ __global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ sta
   const int nact = (int)((v.N - n0) < v.tpb ? (v.N - n0) : v.tpb);
   const bool active = tid < nact;
   const long long nn = active ? n : 0;   // inactive lanes compute on drone 0 and store nothing
-  const int nsub = c.nsub;
-  const int nh = v.ring_len - 1;
-  const int NC = A == 4 ? 3 + v.ring_len : 12 + v.ring_len * A;
 
   float a[A];
   if (A == 4) {
@@ -616,13 +613,16 @@ __global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ sta
     for (int j = 0; j < A; ++j) a[j] = io.actions[nn * A + j];
   }
   const R* st = v.state + tidx(nn, 0, kStateComps);
-  const DynK<R> dk = dyn_consts(c);
+  // each wave issues its state loads first and only then pins the step's constants into VGPRs
+  // (dyn_consts waits for the scalar loads): one exposed memory round trip, not two
 
   if (rate_wave) {
     // ------------------------------------------------------------ wave 1: body rates
     R wx = st[10 * 64], wy = st[11 * 64], wz = st[12 * 64];
     const int head = v.ctr[nn].y;
-    asm volatile("" ::"s"(v.ring));
+    const DynK<R> dk = dyn_consts(c);   // the ring fields are first needed after the substeps
+    const int nsub = dk.nsub, nh = v.ring_len - 1;
+    const int NC = A == 4 ? 3 + v.ring_len : 12 + v.ring_len * A;
     R rpm[4], W[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) rpm[k] = (R)action_to_rpm(dk.hover_f32, a[A == 4 ? k : 0]);
@@ -689,7 +689,9 @@ __global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ sta
   const int2 cv = v.ctr[nn];
   const int sc = cv.x;          // step_counter
   const int head = cv.y;        // ring slot receiving this step's action
-  asm volatile("" ::"s"(v.task), "s"(io.trunc));
+  const DynK<R> dk = dyn_consts(c, v.task, io.trunc);
+  const int nsub = dk.nsub;
+  const int NC = A == 4 ? 3 + v.ring_len : 12 + v.ring_len * A;
 #ifdef GPD_STAMPS
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // diagnostic: loads landed
   GPD_STAMP(10);
@@ -806,7 +808,7 @@ __global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ sta
   io.reward[n] = reward;
   io.term[n] = term ? 1 : 0;
   io.trunc[n] = trunc ? 1 : 0;
-  v.ctr[n] = make_int2(do_reset ? 0 : sc + c.nsub, head + 1 == v.ring_len ? 0 : head + 1);
+  v.ctr[n] = make_int2(do_reset ? 0 : sc + nsub, head + 1 == v.ring_len ? 0 : head + 1);
 }
 
 // ---------------------------------------------------------------------------------------
