@@ -13,7 +13,8 @@ collective inside the timed loop.  The RCCL all-gather of the observation batch 
 on rank 0 (config 5) is timed separately and reported under "gather".
 
 Extra JSON fields: "roofline" (step kernel, HIP events on the launch stream), "cpu_baseline"
-(the oracle, rank 0 at N=1), "sweep" (large-N roofline), "kernel_us".
+(the oracle, rank 0 at N=1), "parity" (the metric's state-L2 leg: GPU vs the C oracle over 5 s,
+beside the CPU baseline), "sweep" (large-N roofline), "kernel_us".
 """
 import argparse
 import json
@@ -134,6 +135,46 @@ def cpu_baseline_openmp(E, seconds=5.0, act="rpm", threads=16):
     return {"value": E * 8 * steps / el, "unit": "drone*dt/s", "cores": threads, "kind": "port",
             "sample": f"{steps} steps of {E} HoverAviary envs (C fp64 restatement, OpenMP, {threads} threads of "
                       f"'{model}') in {el:.1f} s"}
+
+
+def state_parity(device, precision, E=256, T=150, seed=0):
+    """The metric's "state L2" leg, run beside the CPU baseline (the oracle as the checker only):
+    E HoverAviary envs (cf2x, DYN, RPM, auto-reset) stepped T = 150 ctrl steps (5 s, 1200
+    substeps) on the GPU and by the C fp64 restatement of BaseAviary.step (oracle/gpd_oracle.c)
+    on the same actions; per-drone relative L2 error of pos/quat/rpy/vel/ang_v after every step
+    (tests/oracle_runs.py::state_rel_err, the parity tests' metric).  PyBullet itself is not
+    available anywhere in this pipeline."""
+    from gym_pybullet_drones_routing_amd.enums import ActionType
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+    from oracle.c_oracle import COracle
+
+    def rel_err(a, b):
+        a, b = a[..., :16], b[..., :16]
+        d = a - b
+        dq_flip = a[..., 3:7] + b[..., 3:7]
+        flip = (dq_flip ** 2).sum(-1, keepdims=True) < (d[..., 3:7] ** 2).sum(-1, keepdims=True)
+        d[..., 3:7] = np.where(flip, dq_flip, d[..., 3:7])
+        return np.sqrt((d ** 2).sum(-1)) / np.maximum(np.sqrt((b ** 2).sum(-1)), 1e-6)
+
+    rng = np.random.default_rng(seed)
+    acts = np.clip(rng.normal(0, 0.1, (T, E, 1, 4)), -1, 1).astype(np.float32)
+    acts[:, : E // 8] = rng.uniform(-1, 1, (T, E // 8, 1, 4)).astype(np.float32)   # forces resets
+    sim = BatchedAviarySim(n_envs=E, task="hover", act=ActionType.RPM, precision=precision, autoreset=True,
+                           device=device)
+    orc = COracle(n_envs=E, task="hover", act="rpm")
+    errs, n_done = [], 0
+    for t in range(T):
+        _, _, te, tr = sim.step(torch.from_numpy(acts[t]).to(device))
+        _, _, te_o, tr_o = orc.step(acts[t])
+        n_done += int(te_o.sum() + tr_o.sum())
+        errs.append(rel_err(sim.state20().cpu().numpy(), orc.state20()))
+    sim.close()
+    orc.close()
+    e = np.stack(errs)
+    return {"state_rel_l2_max": float(e.max()), "state_rel_l2_median": float(np.median(e)),
+            "gate": 1e-10 if precision == "f64" else 1e-3, "envs": E, "ctrl_steps": T, "substeps": T * 8,
+            "episode_ends": n_done,
+            "vs": "C fp64 restatement of BaseAviary.step (oracle/gpd_oracle.c); PyBullet is unavailable"}
 
 
 def time_graph(sim, pool, steps, warmup, per_graph=16):
@@ -410,6 +451,10 @@ def main():
                                                                 threads=min(16, os.cpu_count() or 1))
         except Exception as exc:  # the C oracle is optional for the bench
             result["cpu_baseline_openmp"] = {"error": str(exc)}
+        try:
+            result["parity"] = state_parity(device, args.precision)
+        except Exception as exc:
+            result["parity"] = {"error": str(exc)}
 
     if rank == 0:
         print(json.dumps(result), flush=True)
