@@ -410,6 +410,13 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     const int full = (kWave / s->D) * s->D;
     const long long per_cu = (Nll + 255) / 256;
     int want = (int)std::min<long long>(full, std::max<long long>(16, per_cu));
+    if (s->D > 1 && (C.physics_flags & GPD_F_DW)) {
+      // downwash envs: the per-substep pair work is spread over a block's lanes, and about four
+      // blocks per CU measured best (scripts/geom_probe_multi.py, D = 8, staggered init:
+      // 512 envs 8 drones/block 13.2 us vs 16: 14.7; 2048 envs 16: 16.1 vs 64: 23.2;
+      // 8192 envs 64: 27.3 vs 16: 50.3)
+      want = (int)std::min<long long>(full, Nll / 1024);
+    }
     want = std::max(s->D, (want / s->D) * s->D);
     const char* ov = std::getenv("GPD_DRONES_PER_BLOCK");
     if (ov) want = std::max(s->D, std::min(full, (std::atoi(ov) / s->D) * s->D));
