@@ -1,0 +1,174 @@
+"""Parity at BASELINE.json's full configuration sizes, through the C ABI.
+
+The small-E parity tests (test_gpu_parity.py) check every code path against the numpy
+restatement; here the C fp64 restatement (oracle/gpd_oracle.c, itself checked against the numpy
+one in test_c_oracle.py) is fast enough to follow the bench configurations at their real sizes
+for a whole 5 s run (150 ctrl steps = 1200 substeps, SB3 auto-reset on):
+
+  * C2: 4096 HoverAviary envs, DYN, RPM (and ONE_D_RPM);
+  * C3: C2 + ground effect + drag on the DYN integrator;
+  * C4: 512 MultiHoverAviary x 8 drones + downwash, staggered init;
+  * C5: 32768 envs as 8 shards of 4096 (seed 1000 + rank) - bit-identical to one 32768-env sim.
+
+Tolerances: f64 state per-drone relative L2 <= 1e-10 after every step (the parity gate),
+terminated / truncated exact, obs (float32) and reward to float32 rounding.
+
+Size-independent properties at the bandwidth-regime sizes the bench sweeps (1M envs, the
+single-wave kernel): envs fed the same actions as env (j mod 4096) end bit-identical to it, and
+hover RPM keeps every env at its initial state (KAT-1).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.c_oracle import COracle
+from tests.oracle_runs import state_rel_err
+
+pytestmark = pytest.mark.gpu
+
+T = 150          # ctrl steps = 5 s at 30 Hz
+STAG = [[0.15 * math.cos(2 * math.pi * i / 8), 0.15 * math.sin(2 * math.pi * i / 8), 0.5 + 0.1 * i]
+        for i in range(8)]
+
+
+def _actions(rng, E, D, A):
+    """Hover-biased actions keep most episodes alive; an eighth of the envs get full-range
+    actions so that episodes end and auto-reset throughout the run."""
+    a = np.clip(rng.normal(0, 0.1, (T, E, D, A)), -1, 1).astype(np.float32)
+    a[:, : E // 8] = rng.uniform(-1, 1, (T, E // 8, D, A)).astype(np.float32)
+    if A == 1:
+        a[:, E // 8: E // 4] = 1.0   # full collective thrust: climbs through z > 2 -> truncation + reset
+    return a
+
+
+CASES = {
+    "C2_rpm": dict(n_envs=4096, act="rpm", task="hover", aero=()),
+    "C2_one_d_rpm": dict(n_envs=4096, act="one_d_rpm", task="hover", aero=()),
+    "C3_gnd_drag": dict(n_envs=4096, act="rpm", task="hover", aero=("gnd", "drag")),
+    "C4_multihover_dw": dict(n_envs=512, drones_per_env=8, act="rpm", task="multihover", aero=("dw",),
+                             initial_xyzs=STAG),
+}
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_fullsize_config_parity(case):
+    from gym_pybullet_drones_routing_amd.enums import ActionType
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+    kw = dict(CASES[case])
+    E, D = kw["n_envs"], kw.get("drones_per_env", 1)
+    A = 4 if kw["act"] == "rpm" else 1
+    xyz = kw.pop("initial_xyzs", None)
+    acts = _actions(np.random.default_rng(11), E, D, A)
+    sim = BatchedAviarySim(n_envs=E, drones_per_env=D, task=kw["task"], act=ActionType(kw["act"]),
+                           aero=kw["aero"], precision="f64", autoreset=True, device="cuda:0",
+                           initial_xyzs=xyz)
+    orc = COracle(n_envs=E, drones_per_env=D, task=kw["task"], act=kw["act"], aero=kw["aero"],
+                  initial_xyzs=None if xyz is None else np.asarray(xyz, dtype=np.float64))
+    worst, n_done = 0.0, 0
+    for t in range(T):
+        o, r, te, tr = sim.step(torch.from_numpy(acts[t]).cuda())
+        o_o, r_o, te_o, tr_o = orc.step(acts[t])
+        te, tr = te.cpu().numpy().astype(bool), tr.cpu().numpy().astype(bool)
+        np.testing.assert_array_equal(te, te_o, err_msg=f"terminated differs at step {t}")
+        np.testing.assert_array_equal(tr, tr_o, err_msg=f"truncated differs at step {t}")
+        np.testing.assert_allclose(o.cpu().numpy(), o_o, rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(r.cpu().numpy(), r_o, rtol=1e-6, atol=1e-6)
+        done = te | tr
+        if done.any():
+            n_done += int(done.sum())
+            np.testing.assert_allclose(sim.terminal_obs.cpu().numpy()[done], orc.terminal_obs[done],
+                                       rtol=1e-5, atol=1e-6)
+        err = state_rel_err(sim.state20().cpu().numpy(), orc.state20())
+        worst = max(worst, float(err.max()))
+        assert worst <= 1e-10, f"state rel L2 {worst:.3g} at step {t}"
+    assert n_done > E // 16, "the run should exercise auto-reset"
+    if "dw" in kw["aero"]:
+        # the downwash really acted: the lower drones sink relative to a run without it
+        nodw = COracle(n_envs=E, drones_per_env=D, task=kw["task"], act=kw["act"],
+                       initial_xyzs=np.asarray(xyz, dtype=np.float64))
+        for t in range(4):
+            nodw.step(acts[t])
+        ref = COracle(n_envs=E, drones_per_env=D, task=kw["task"], act=kw["act"], aero=kw["aero"],
+                      initial_xyzs=np.asarray(xyz, dtype=np.float64))
+        for t in range(4):
+            ref.step(acts[t])
+        assert np.abs(nodw.state20()[:, 2] - ref.state20()[:, 2]).max() > 1e-6
+    sim.close()
+    orc.close()
+    print(f"{case}: {E}x{D} drones, {T} steps, {n_done} episode ends, max state rel L2 {worst:.3g}")
+
+
+def test_c5_shards_match_one_sim():
+    """C5: 32768 envs as 8 rank shards of 4096 (contiguous env blocks, per-rank action streams)
+    give bit-identical obs / reward / done / state to one 32768-env sim (envs are independent
+    worlds, so sharding must not change a single bit)."""
+    from gym_pybullet_drones_routing_amd.shard import env_shard, rank_seed
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+    G, E_glob, steps = 8, 32768, 60
+    per = E_glob // G
+    gen = [torch.Generator(device="cuda:0").manual_seed(rank_seed(1000, r)) for r in range(G)]
+    whole = BatchedAviarySim(n_envs=E_glob, task="hover", device="cuda:0")
+    shards = [BatchedAviarySim(n_envs=per, task="hover", device="cuda:0") for _ in range(G)]
+    for t in range(steps):
+        parts = [(torch.rand((per, 1, 4), generator=gen[r], device="cuda:0") * 2 - 1) for r in range(G)]
+        o, rw, te, tr = [x.clone() for x in whole.step(torch.cat(parts).contiguous())]
+        for r, s in enumerate(shards):
+            lo, n = env_shard(E_glob, r, G)
+            so, sr, ste, stt = s.step(parts[r])
+            assert torch.equal(so, o[lo:lo + n]) and torch.equal(sr, rw[lo:lo + n])
+            assert torch.equal(ste, te[lo:lo + n]) and torch.equal(stt, tr[lo:lo + n])
+    st = whole.state20()
+    for r, s in enumerate(shards):
+        assert torch.equal(s.state20(), st[r * per:(r + 1) * per])
+        s.close()
+    whole.close()
+
+
+def test_large_n_periodic_actions_bit_identical():
+    """1M envs (the bench sweep's size, single-wave kernel): env j is fed env (j mod 4096)'s
+    actions, so it must end bit-identical to it; the 4096 envs themselves must match a separate
+    4096-env sim (the two-wave kernel, oracle-checked above) to rounding."""
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+    E, P, steps = 1 << 20, 4096, 40
+    big = BatchedAviarySim(n_envs=E, task="hover", device="cuda:0")
+    small = BatchedAviarySim(n_envs=P, task="hover", device="cuda:0")
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    for t in range(steps):
+        a = (torch.rand((P, 1, 4), generator=g, device="cuda:0") * 2 - 1).contiguous()
+        o, _, te, tr = big.step(a.repeat(E // P, 1, 1).contiguous())
+        so, _, ste, stt = small.step(a)
+        ob = o.view(E // P, P, *o.shape[1:])
+        assert torch.equal(ob, ob[:1].expand_as(ob)), f"periodic obs differ at step {t}"
+        torch.testing.assert_close(ob[0], so, rtol=1e-5, atol=1e-6)
+        assert torch.equal(te.view(E // P, P)[0], ste) and torch.equal(tr.view(E // P, P)[0], stt)
+    s_big = big.state20().view(E // P, P, 20)
+    assert torch.equal(s_big, s_big[:1].expand_as(s_big))
+    err = state_rel_err(s_big[0].cpu().numpy(), small.state20().cpu().numpy())
+    assert err.max() <= 1e-12
+    big.close()
+    small.close()
+
+
+def test_large_n_hover_kat():
+    """KAT-1 at 1M envs through step(): action 0 maps to HOVER_RPM in float32 (numpy-1.x
+    semantics of _preprocessAction), whose rounding leaves a residual vertical acceleration of
+    ~1e-7 m/s^2, so the drones drift by ~1e-5 m over 5 s instead of staying put.  Every env must
+    be bit-identical to every other and match the C oracle's single env (<= 1e-10), and no
+    episode may end (||e|| = 0.8875, inside every bound)."""
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+    E = 1 << 20
+    sim = BatchedAviarySim(n_envs=E, task="hover", device="cuda:0")
+    orc = COracle(n_envs=1, task="hover", act="rpm")
+    a = torch.zeros((E, 1, 4), device="cuda:0")
+    for _ in range(T):
+        _, _, te, tr = sim.step(a)
+        orc.step(np.zeros((1, 1, 4), np.float32))
+        assert not bool(te.any()) and not bool(tr.any())
+    st = sim.state20()
+    assert torch.equal(st, st[:1].expand_as(st))
+    assert state_rel_err(st[:1].cpu().numpy(), orc.state20()).max() <= 1e-10
+    assert abs(float(st[0, 2]) - 0.1125) < 1e-4      # hovering (drift from the f32 action map only)
+    sim.close()
+    orc.close()
