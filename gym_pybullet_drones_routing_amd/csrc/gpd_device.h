@@ -54,6 +54,23 @@ __device__ __forceinline__ float g_rsqrt(float x) {
   return fmaf(y, e, y);
 }
 
+// 1/x for finite x != 0: the hardware estimate (v_rcp_*) refined by Newton steps
+// y <- y + y*(1 - x*y); two steps for double (within ~1 ulp of the IEEE quotient), one for float.
+// An IEEE f64 divide is a ~10-instruction dependent sequence (div_scale / rcp / 4 fma /
+// div_fmas / div_fixup).  Only for operands bounded away from 0 and inf (the ground-effect prop
+// heights are clipped at GND_EFF_H_CLIP > 0).
+__device__ __forceinline__ double g_rcp(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-x, y, 1.0);
+  return fma(y, e, y);
+}
+__device__ __forceinline__ float g_rcp(float x) {
+  const float y = __builtin_amdgcn_rcpf(x);
+  return fmaf(y, fmaf(-x, y, 1.0f), y);
+}
+
 template <typename R> struct PiC;
 template <> struct PiC<float> { static constexpr float pi = 3.14159265358979323846f; };
 template <> struct PiC<double> { static constexpr double pi = 3.14159265358979323846; };
@@ -468,7 +485,7 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
     for (int k = 0; k < 4; ++k) {
       R h = s.pz + ((Rm[6] * c.rx[k] + Rm[7] * c.ry[k]) + Rm[8] * c.rz[k]);
       h = h < c.ge_clip ? c.ge_clip : h;
-      const R qq = c.prop_r / (R(4) * h);
+      const R qq = c.prop_r * g_rcp(R(4) * h);   // h >= GND_EFF_H_CLIP > 0
       g[k] = ((rpm[k] * rpm[k]) * c.kf * c.ge_coeff) * (qq * qq);
     }
     const R gz = ((g[0] + g[1]) + g[2]) + g[3];
