@@ -205,14 +205,38 @@ SimView<R> make_view(const gpd_sim* s) {
 
 // The step_kernel instantiation of a sim: action type x (D > 1) x (plain DYN fast path).  The
 // fast specialisation exists for the RPM action types only (the bench path).
+// Physics-flag sets compiled into their own kernels (pf_on): the BASELINE configs' combinations
+// (config 3: ground effect + drag; config 4: downwash; Physics.PYB and PYB_GND_DRAG_DW) for the
+// RPM action types, plain DYN and Physics.PYB for the single-drone PID types; every other
+// combination tests Consts::flags at run time.
+constexpr int kPfAero = F_GND | F_DRAG;
+constexpr int kPfPyb = F_BULLET | F_GEOM;
+constexpr int kPfPybAll = F_BULLET | F_GEOM | F_GND | F_DRAG | F_DW;
 template <typename R, int ACT>
-const void* step_fn_act(bool multi, bool fast) {
-  if (multi) return fast ? (const void*)step_kernel<R, ACT, true, true> : (const void*)step_kernel<R, ACT, true, false>;
-  return fast ? (const void*)step_kernel<R, ACT, false, true> : (const void*)step_kernel<R, ACT, false, false>;
+const void* step_fn_act(bool multi, int flags) {
+  if (multi) {
+    switch (flags) {
+      case 0: return (const void*)step_kernel<R, ACT, true, 0>;
+      case F_DW: return (const void*)step_kernel<R, ACT, true, F_DW>;
+      case kPfPybAll: return (const void*)step_kernel<R, ACT, true, kPfPybAll>;
+      default: return (const void*)step_kernel<R, ACT, true, kPfRuntime>;
+    }
+  }
+  switch (flags) {
+    case 0: return (const void*)step_kernel<R, ACT, false, 0>;
+    case kPfAero: return (const void*)step_kernel<R, ACT, false, kPfAero>;
+    case kPfPyb: return (const void*)step_kernel<R, ACT, false, kPfPyb>;
+    default: return (const void*)step_kernel<R, ACT, false, kPfRuntime>;
+  }
 }
 template <typename R, int ACT>
-const void* step_fn_pid(bool multi) {
-  return multi ? (const void*)step_kernel<R, ACT, true, false> : (const void*)step_kernel<R, ACT, false, false>;
+const void* step_fn_pid(bool multi, int flags) {
+  if (multi) return (const void*)step_kernel<R, ACT, true, kPfRuntime>;
+  switch (flags) {
+    case 0: return (const void*)step_kernel<R, ACT, false, 0>;
+    case kPfPyb: return (const void*)step_kernel<R, ACT, false, kPfPyb>;
+    default: return (const void*)step_kernel<R, ACT, false, kPfRuntime>;
+  }
 }
 template <typename R>
 const void* step_kernel_fn(const gpd_sim* s) {
@@ -220,13 +244,14 @@ const void* step_kernel_fn(const gpd_sim* s) {
     return s->cfg.act_type == GPD_ACT_RPM ? (const void*)step_kernel_duo<R, ACT_RPM>
                                           : (const void*)step_kernel_duo<R, ACT_ONE_D_RPM>;
   const bool multi = s->D > 1;
-  const bool fast = s->cfg.physics_flags == 0;
+  // the flags the kernel sees (Consts::flags, make_consts)
+  const int pf = s->cfg.physics_flags | ((s->cfg.physics_flags & GPD_F_BULLET) ? GPD_F_GEOM_WRENCH : 0);
   switch (s->cfg.act_type) {
-    case GPD_ACT_RPM: return step_fn_act<R, ACT_RPM>(multi, fast);
-    case GPD_ACT_ONE_D_RPM: return step_fn_act<R, ACT_ONE_D_RPM>(multi, fast);
-    case GPD_ACT_PID: return step_fn_pid<R, ACT_PID>(multi);
-    case GPD_ACT_VEL: return step_fn_pid<R, ACT_VEL>(multi);
-    default: return step_fn_pid<R, ACT_ONE_D_PID>(multi);
+    case GPD_ACT_RPM: return step_fn_act<R, ACT_RPM>(multi, pf);
+    case GPD_ACT_ONE_D_RPM: return step_fn_act<R, ACT_ONE_D_RPM>(multi, pf);
+    case GPD_ACT_PID: return step_fn_pid<R, ACT_PID>(multi, pf);
+    case GPD_ACT_VEL: return step_fn_pid<R, ACT_VEL>(multi, pf);
+    default: return step_fn_pid<R, ACT_ONE_D_PID>(multi, pf);
   }
 }
 

@@ -78,6 +78,14 @@ template <> struct PiC<double> { static constexpr double pi = 3.1415926535897932
 // ---------------------------------------------------------------- model constants (device memory)
 enum : int { MODEL_CF2X = 0, MODEL_CF2P = 1, MODEL_RACE = 2 };
 enum : int { F_GND = 1, F_DRAG = 2, F_DW = 4, F_GEOM = 8, F_BULLET = 16 };
+// PF, the physics flags a kernel is compiled for: 0 = plain DYN (the FAST path), a flag set =
+// those terms compiled in (no flag tests, one basic block per substep), kPfRuntime = the terms
+// selected at run time from Consts::flags (every other combination).
+constexpr int kPfRuntime = -1;
+template <int PF>
+__device__ __forceinline__ bool pf_on(int flags, int f) {
+  return PF == kPfRuntime ? (flags & f) != 0 : (PF & f) != 0;
+}
 
 // DSLPIDControl coefficients (control/DSLPIDControl.py:37-60, settable like
 // BaseControl.setPIDCoefficients :138-177) and the controller's own constants.
@@ -439,7 +447,7 @@ __device__ __forceinline__ float action_to_rpm(float hover_f32, float a) {
 // following add, so four equal RPMs (every ONE_D_RPM action, the hover equilibrium) would leave
 // a residual roll/pitch torque instead of the reference's exact zero.
 // W = {fz, tx, ty, tz} in the body frame.
-template <typename R, bool FAST>
+template <typename R, int PF>
 __device__ __forceinline__ void rpm_wrench(const R rpm[4], const DynK<R>& k, const Consts<R>& c, R W[4]) {
 #pragma clang fp contract(off)
   R f[4], zt[4];
@@ -455,7 +463,7 @@ __device__ __forceinline__ void rpm_wrench(const R rpm[4], const DynK<R>& k, con
   }
   W[0] = ((f[0] + f[1]) + f[2]) + f[3];                // np.sum(forces) :839
   W[3] = ((-zt[0] + zt[1]) - zt[2]) + zt[3];           // :845
-  if (!FAST && (k.flags & F_GEOM)) {                   // _physics: forces at prop links :698-705
+  if (pf_on<PF>(k.flags, F_GEOM)) {                   // _physics: forces at prop links :698-705
     R tx = R(0), ty = R(0);
 #pragma unroll
     for (int m = 0; m < 4; ++m) { tx = tx + c.ry[m] * f[m]; ty = ty - c.rx[m] * f[m]; }
@@ -471,13 +479,13 @@ __device__ __forceinline__ void rpm_wrench(const R rpm[4], const DynK<R>& k, con
 
 // Body wrench of one substep: the propeller wrench W plus, with F_GND, the ground effect
 // (_groundEffect :732-750) at the current pose.
-template <typename R, bool FAST>
+template <typename R, int PF>
 __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bool gnd_upright, const R rpm[4],
                                             const R W[4], const Consts<R>& c, const DynK<R>& kk, R& fz_out, R& tx_out,
                                             R& ty_out, R& tz_out) {
 #pragma clang fp contract(off)
   R fz = W[0], tx = W[1], ty = W[2];
-  if (!FAST && (kk.flags & F_GND)) {
+  if (pf_on<PF>(kk.flags, F_GND)) {
     // prop COM heights via forward kinematics, clipped, +z link force at each prop; applied only
     // while upright (a select, not a branch)
     R g[4];
@@ -520,19 +528,19 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
 // The exponential map's half angle is clamped at pi/8 < 0.5, so the cos / sinc series always
 // applies (a select, no branch; below Bullet's f < 0.001 Taylor switch the series agrees with
 // Bullet's two-term expansion to ~1e-30).
-template <typename R, bool ANGV>
+template <typename R, int PF, bool ANGV>
 __device__ __forceinline__ void bullet_substep(Drone<R>& s, const R rpm[4], const R W[4], const R last[4], R dwsum,
                                                R q0[4], R d, const Consts<R>& c, const DynK<R>& k) {
   R inv, Rm[9];
   readback_unit<R, true, false>(q0[0], q0[1], q0[2], q0[3], d, inv, Rm);
   bool up = true;
-  if (k.flags & F_GND) {   // |self.rpy[0,1]| < pi/2, :742
+  if (pf_on<PF>(k.flags, F_GND)) {   // |self.rpy[0,1]| < pi/2, :742
     const R qn[4] = {q0[0] * inv, q0[1] * inv, q0[2] * inv, q0[3] * inv};
     up = upright(attitude_args(qn));
   }
   R fz, tx, ty, tz;
-  body_wrench<R, false>(s, Rm, up, rpm, W, c, k, fz, tx, ty, tz);
-  if (k.flags & F_DW) fz = fz + dwsum;
+  body_wrench<R, PF>(s, Rm, up, rpm, W, c, k, fz, tx, ty, tz);
+  if (pf_on<PF>(k.flags, F_DW)) fz = fz + dwsum;
   // angular: base-frame rate, gyroscopic term, damping on the world rate
   const R wbx = (Rm[0] * s.wx + Rm[3] * s.wy) + Rm[6] * s.wz;
   const R wby = (Rm[1] * s.wx + Rm[4] * s.wy) + Rm[7] * s.wz;
@@ -552,7 +560,7 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, const R rpm[4], cons
   s.wz = clampv(s.wz + k.dt * dwz);
   // linear
   R Fx = Rm[2] * fz, Fy = Rm[5] * fz, Fz = Rm[8] * fz;
-  if (k.flags & F_DRAG) {   // _drag :773-781 with last_clipped_action, world force drag_factors * vel
+  if (pf_on<PF>(k.flags, F_DRAG)) {   // _drag :773-781 with last_clipped_action, world force drag_factors * vel
     const R S = ((last[0] * c.rpm2rad + last[1] * c.rpm2rad) + last[2] * c.rpm2rad) + last[3] * c.rpm2rad;
     Fx = Fx + (-c.drag_xy * S) * s.vx;
     Fy = Fy + (-c.drag_xy * S) * s.vy;
@@ -601,7 +609,7 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, const R rpm[4], cons
 // written before the readback and the two dependency chains interleave.  Lanes with
 // |theta| >= 0.5 (|omega| >= 240 rad/s at 240 Hz: library sin/cos) are redone in a
 // wave-uniform branch at the end.
-template <typename R, bool FAST, bool ANGV = true>
+template <typename R, int PF, bool ANGV = true>
 __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R W[4], const R last[4], R dwsum,
                                             const Consts<R>& c, const DynK<R>& k) {
   R q0[4] = {s.qx, s.qy, s.qz, s.qw};
@@ -620,23 +628,23 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R
       }
     }
   }
-  if (!FAST && (k.flags & F_BULLET)) {
-    bullet_substep<R, ANGV>(s, rpm, W, last, dwsum, q0, d, c, k);
+  if (pf_on<PF>(k.flags, F_BULLET)) {
+    bullet_substep<R, PF, ANGV>(s, rpm, W, last, dwsum, q0, d, c, k);
     return;
   }
   R inv, Rm[9];
   bool up = true;
   auto readback = [&]() {
-    readback_unit<R, ANGV || !FAST, false>(q0[0], q0[1], q0[2], q0[3], d, inv, Rm);
-    if (!FAST && (k.flags & F_GND)) {   // |self.rpy[0,1]| < pi/2, :742
+    readback_unit<R, ANGV || PF != 0, false>(q0[0], q0[1], q0[2], q0[3], d, inv, Rm);
+    if (pf_on<PF>(k.flags, F_GND)) {   // |self.rpy[0,1]| < pi/2, :742
       const R qn[4] = {q0[0] * inv, q0[1] * inv, q0[2] * inv, q0[3] * inv};
       up = upright(attitude_args(qn));
     }
   };
-  if (!FAST) readback();
+  if (PF != 0) readback();
   R fz, tx, ty, tz;
-  body_wrench<R, FAST>(s, Rm, up, rpm, W, c, k, fz, tx, ty, tz);
-  if (!FAST && (k.flags & F_DW)) fz = fz + dwsum;      // _downwash :801-811 (body z)
+  body_wrench<R, PF>(s, Rm, up, rpm, W, c, k, fz, tx, ty, tz);
+  if (pf_on<PF>(k.flags, F_DW)) fz = fz + dwsum;      // _downwash :801-811 (body z)
   // torques - ω × (Jω); ω̇ = J⁻¹ τ                     :852-854
   const R jwx = k.jx * s.wx, jwy = k.jy * s.wy, jwz = k.jz * s.wz;
   const R cx = s.wy * jwz - s.wz * jwy;
@@ -661,10 +669,10 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R
   cos_sinc(t2, co, sc);
   const R sh = k.hdt * sc;                             // sin(theta)/|omega|
   const bool big = t2 >= R(0.25);
-  if (FAST) readback();
+  if (PF == 0) readback();
   // R·(0,0,fz) - (0,0,GRAVITY) [+ drag]                 :839-841
   R Fx = Rm[2] * fz, Fy = Rm[5] * fz, Fz = Rm[8] * fz;
-  if (!FAST && (k.flags & F_DRAG)) {                   // _drag :773-774 with last_clipped_action
+  if (pf_on<PF>(k.flags, F_DRAG)) {                   // _drag :773-774 with last_clipped_action
     const R S = ((last[0] * c.rpm2rad + last[1] * c.rpm2rad) + last[2] * c.rpm2rad) + last[3] * c.rpm2rad;
     Fx = Fx + (-c.drag_xy * S) * s.vx;
     Fy = Fy + (-c.drag_xy * S) * s.vy;

@@ -178,12 +178,12 @@ __device__ __forceinline__ void store_drone(const SimView<R>& v, long long n, co
 
 // One physics substep of every drone of the block, including the readback that precedes it
 // (BaseAviary.py:343-372 loop body).  MULTI: envs have D > 1 drones and may need downwash.
-template <typename R, bool MULTI, bool FAST, bool ANGV = true>
+template <typename R, bool MULTI, int PF, bool ANGV = true>
 __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const R W[4], const R last[4],
                                               const Consts<R>& c, const DynK<R>& k, R* sx, R* sy, R* sz, int tid,
                                               int base, int D, DwPairs pairs = DwPairs{0, 0}, R* spair = nullptr) {
   R dw = R(0);
-  if (MULTI && !FAST && (k.flags & F_DW)) {
+  if (MULTI && pf_on<PF>(k.flags, F_DW)) {
     sx[tid] = s.px; sy[tid] = s.py; sz[tid] = s.pz;
     __syncthreads();
     if (pairs.n > 0) {
@@ -201,7 +201,7 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
     }
     __syncthreads();
   }
-  dyn_substep<R, FAST, ANGV>(s, rpm, W, last, dw, c, k);
+  dyn_substep<R, PF, ANGV>(s, rpm, W, last, dw, c, k);
 }
 
 // Bytes of dynamic LDS the step kernel needs for its observation tile: the row's columns
@@ -309,8 +309,9 @@ __device__ __forceinline__ void tile_copy_out(const float4* tile4, const float* 
 // ---------------------------------------------------------------------------------------
 // gpd_step: one env.step() for every env (BaseAviary.py:259-383) in ONE launch.
 // ACT: action type (GPD_ACT_*); PID types run DSLPIDControl before the substeps.
-// FAST: physics_flags == 0 (plain DYN, the bench path) - the aero / PYB-wrench code is compiled out.
-template <typename R, int ACT, bool MULTI, bool FAST>
+// PF: the physics flags compiled in (pf_on): 0 = plain DYN (the bench path, aero / PYB-wrench code
+// compiled out), a flag set for the BASELINE configs' combinations, kPfRuntime for the rest.
+template <typename R, int ACT, bool MULTI, int PF>
 // The leading scalar arguments duplicate the SimView / StepIO fields the first loads need: the
 // library is built with kernarg preloading, so they arrive in SGPRs at wave launch instead of
 // through an s_load round trip on the kernel-argument segment before the first state load.
@@ -339,7 +340,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
   const bool active = tid < nact;
   const long long nn = active ? n : 0;  // inactive lanes compute on drone 0 and store nothing
   const long long e = MULTI ? nn / D : nn;
-  const bool drag = !FAST && (c.flags & F_DRAG) != 0;
+  const bool drag = pf_on<PF>(c.flags, F_DRAG);
 
   Drone<R> s;
   R last[4];
@@ -408,19 +409,19 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
   };
   // propeller wrench: the same RPMs drive every substep of the control step (:349-367)
   R W[4];
-  rpm_wrench<R, FAST>(rpm, dk, c, W);
+  rpm_wrench<R, PF>(rpm, dk, c, W);
   // substeps 1..nsub-1 skip the (write-only) world ang_v; the last one produces it
   // (the first substep is peeled so the loop body stays one basic block)
   if (dk.nsub > 1) {
-    substep_block<R, MULTI, FAST, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
+    substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
     GPD_STAMP(1);
     history_dma();
     for (int it = 1; it < dk.nsub - 1; ++it)
-      substep_block<R, MULTI, FAST, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
+      substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
   }
-  substep_block<R, MULTI, FAST, true>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
+  substep_block<R, MULTI, PF, true>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
 #pragma unroll
   for (int k = 0; k < 4; ++k) last[k] = rpm[k];
   if (dk.nsub == 1) history_dma();
@@ -626,7 +627,7 @@ __global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ sta
     R rpm[4], W[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) rpm[k] = (R)action_to_rpm(dk.hover_f32, a[A == 4 ? k : 0]);
-    rpm_wrench<R, true>(rpm, dk, c, W);
+    rpm_wrench<R, 0>(rpm, dk, c, W);
     for (int k = 0; k < nsub; ++k) {
       R h[5];
       rate_half(wx, wy, wz, W, dk, h);
@@ -701,7 +702,7 @@ __global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ sta
     R rpm[4], W[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) rpm[k] = (R)action_to_rpm(dk.hover_f32, a[A == 4 ? k : 0]);
-    rpm_wrench<R, true>(rpm, dk, c, W);
+    rpm_wrench<R, 0>(rpm, dk, c, W);
     fz = W[0];
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
@@ -845,8 +846,8 @@ __global__ __launch_bounds__(kWave) void integrate_kernel(SimView<R> v, const Co
       nxt[0] = src[0]; nxt[1] = src[1]; nxt[2] = src[2]; nxt[3] = src[3];
     }
     R W[4];
-    rpm_wrench<R, false>(rpm, dk, c, W);
-    substep_block<R, MULTI, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D);
+    rpm_wrench<R, kPfRuntime>(rpm, dk, c, W);
+    substep_block<R, MULTI, kPfRuntime>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];
     if (traj && active) {
