@@ -70,7 +70,7 @@ def step_kernel_name(sim, rbytes, act):
     a = 0 if act == "rpm" else 1
     if sim.constants.lanes_per_block == 128:
         return "gpd::step_kernel_duo<%s, %d>" % (real, a)
-    return "gpd::step_kernel<%s, %d, false, true>" % (real, a)
+    return "gpd::step_kernel<%s, %d, false, 0>" % (real, a)
 
 
 def log(*a):

@@ -250,10 +250,11 @@ __device__ __forceinline__ void tile_copy_out(const float4* tile4, const float* 
       GPD_STAMP(8);
       float4* dst = reinterpret_cast<float4*>(obs) + n0 * NC;
       if (wt & 1) {
+        // masked-off elements get an offset past num_records: the buffer unit drops the store
+        // (no exec-mask branch per element)
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, 0, total * 16, 0x00020000);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (ok[u]) store_wt(r, idx[u] * 16, val[u]);
+        for (int u = 0; u < U; ++u) store_wt(r, ok[u] ? idx[u] * 16 : total * 16, val[u]);
       } else {
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -287,8 +288,7 @@ __device__ __forceinline__ void tile_copy_out(const float4* tile4, const float* 
       if (wt & 1) {
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, 0, total * 4, 0x00020000);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (ok[u]) store_wt(r, idx[u] * 4, val[u]);
+        for (int u = 0; u < U; ++u) store_wt(r, ok[u] ? idx[u] * 4 : total * 4, val[u]);
       } else {
 #pragma unroll
         for (int u = 0; u < U; ++u)
