@@ -176,6 +176,11 @@ __device__ __forceinline__ void store_drone(const SimView<R>& v, long long n, co
   st[16 * 64] = last[0]; st[17 * 64] = last[1]; st[18 * 64] = last[2]; st[19 * 64] = last[3];
 }
 
+// Workgroup barrier for LDS exchanges within a block (between its waves, or its lanes): waits for this wave's own
+// LDS operations only.  __syncthreads() (a workgroup release fence) would also wait for every
+// vector-memory operation in flight, including an LDS-DMA that nobody reads until much later.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // One physics substep of every drone of the block, including the readback that precedes it
 // (BaseAviary.py:343-372 loop body).  MULTI: envs have D > 1 drones and may need downwash.
 template <typename R, bool MULTI, int PF, bool ANGV = true>
@@ -185,7 +190,7 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
   R dw = R(0);
   if (MULTI && pf_on<PF>(k.flags, F_DW)) {
     sx[tid] = s.px; sy[tid] = s.py; sz[tid] = s.pz;
-    __syncthreads();
+    lds_barrier();
     if (pairs.n > 0) {
       for (int p = tid; p < pairs.n; p += kWave) {
         const int i = (p * pairs.dmagic) >> 20;          // drone of the block
@@ -193,13 +198,13 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
         const int ib = ((i * pairs.dmagic) >> 20) * D;   // the env's first drone in the block
         spair[p] = dw_pair(sx[i], sy[i], sz[i], sx[ib + j], sy[ib + j], sz[ib + j], c);
       }
-      __syncthreads();
+      lds_barrier();
       if (tid * D < pairs.n)
         for (int j = 0; j < D; ++j) dw = dw + spair[tid * D + j];
     } else {
       dw = downwash_sum(s.px, s.py, s.pz, sx, sy, sz, base, D, c);
     }
-    __syncthreads();
+    lds_barrier();
   }
   dyn_substep<R, PF, ANGV>(s, rpm, W, last, dw, c, k);
 }
@@ -451,7 +456,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
       srew[tid] = (float)r;
       sdist[tid] = (float)dist;
       sflag[tid] = oob ? 1 : 0;
-      __syncthreads();
+      lds_barrier();   // not __syncthreads(): its fence would wait for the history DMA in flight
       if (d == 0) {
         // MultiHoverAviary: summed reward, sum of distances < 1e-4, any drone out of bounds
         float rs = 0.0f, ds = 0.0f;
@@ -463,7 +468,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
         sflag[tid] = (term ? 1 : 0) | (trunc ? 2 : 0);
         srew[tid] = reward;
       }
-      __syncthreads();
+      lds_barrier();
       const int fl = sflag[base];
       term = fl & 1;
       trunc = (fl >> 1) & 1;
@@ -560,10 +565,6 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
   }
 }
 
-// Workgroup barrier for LDS hand-offs between the waves of a block: waits for this wave's own
-// LDS operations only.  __syncthreads() (a workgroup release fence) would also wait for every
-// vector-memory operation in flight, including an LDS-DMA that nobody reads until much later.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ---------------------------------------------------------------------------------------
 // step_kernel_duo: step_kernel<R, ACT, false, true> (single-drone envs, plain DYN, RPM action
