@@ -634,14 +634,17 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R
   }
   R inv, Rm[9];
   bool up = true;
+  // the torques depend on the pose only through the ground effect (downwash and drag are forces):
+  // without it the rotation chain goes ahead of the readback, as on the plain path
+  constexpr bool kPoseFirst = PF == kPfRuntime || (PF & F_GND) != 0;
   auto readback = [&]() {
-    readback_unit<R, ANGV || PF != 0, false>(q0[0], q0[1], q0[2], q0[3], d, inv, Rm);
+    readback_unit<R, ANGV || kPoseFirst, false>(q0[0], q0[1], q0[2], q0[3], d, inv, Rm);
     if (pf_on<PF>(k.flags, F_GND)) {   // |self.rpy[0,1]| < pi/2, :742
       const R qn[4] = {q0[0] * inv, q0[1] * inv, q0[2] * inv, q0[3] * inv};
       up = upright(attitude_args(qn));
     }
   };
-  if (PF != 0) readback();
+  if (kPoseFirst) readback();
   R fz, tx, ty, tz;
   body_wrench<R, PF>(s, Rm, up, rpm, W, c, k, fz, tx, ty, tz);
   if (pf_on<PF>(k.flags, F_DW)) fz = fz + dwsum;      // _downwash :801-811 (body z)
@@ -669,7 +672,7 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R
   cos_sinc(t2, co, sc);
   const R sh = k.hdt * sc;                             // sin(theta)/|omega|
   const bool big = t2 >= R(0.25);
-  if (PF == 0) readback();
+  if (!kPoseFirst) readback();
   // R·(0,0,fz) - (0,0,GRAVITY) [+ drag]                 :839-841
   R Fx = Rm[2] * fz, Fy = Rm[5] * fz, Fz = Rm[8] * fz;
   if (pf_on<PF>(k.flags, F_DRAG)) {                   // _drag :773-774 with last_clipped_action
