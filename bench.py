@@ -216,26 +216,31 @@ def time_graph(sim, pool, steps, warmup, per_graph=16):
 
 
 def time_steps(sim, pool, steps, warmup):
-    """Eager launches with a HIP event pair around every gpd_step on the launch stream;
-    returns (wall seconds, mean kernel us)."""
+    """Eager launches (one BatchedAviarySim.step() call per env.step, as an SB3-style caller
+    makes them): the wall time of `steps` back-to-back calls, then a second pass with a HIP event
+    pair around every gpd_step on the launch stream for the per-launch kernel time.
+    Returns (wall seconds, mean kernel us)."""
     P = pool.shape[0]
     for k in range(warmup):
         sim.step(pool[k % P])
     torch.cuda.synchronize(sim.device)
-    stream = torch.cuda.current_stream(sim.device)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     if torch.distributed.is_initialized():
         torch.distributed.barrier()
     torch.cuda.synchronize(sim.device)
     t0 = time.perf_counter()
     for k in range(steps):
-        ev[k][0].record(stream)
         sim.step(pool[(warmup + k) % P])
-        ev[k][1].record(stream)
     torch.cuda.synchronize(sim.device)
     wall = time.perf_counter() - t0
     if torch.distributed.is_initialized():
         torch.distributed.barrier()
+    stream = torch.cuda.current_stream(sim.device)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for k in range(steps):
+        ev[k][0].record(stream)
+        sim.step(pool[(warmup + k) % P])
+        ev[k][1].record(stream)
+    torch.cuda.synchronize(sim.device)
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     return wall, 1000.0 * float(np.mean(kern_ms))
 

@@ -64,6 +64,17 @@ def _stream(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+_raw_stream_fn = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _raw_stream(index):
+    """The current stream of device `index` as an integer handle (torch's raw accessor when this
+    build has it: the eager step() is host-bound, and the Stream object costs a microsecond)."""
+    if _raw_stream_fn is not None:
+        return _raw_stream_fn(index)
+    return torch.cuda.current_stream(index).cuda_stream
+
+
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -127,6 +138,11 @@ class BatchedAviarySim:
         self.reward = torch.zeros((E,), dtype=torch.float32, device=dev)
         self.terminated = torch.zeros((E,), dtype=torch.uint8, device=dev)
         self.truncated = torch.zeros((E,), dtype=torch.uint8, device=dev)
+        # the sim-owned output buffers never move: their ctypes pointers are built once (the eager
+        # step() is host-bound at 4096 envs, a few microseconds per call)
+        self._step_fn = self._lib.gpd_step
+        self._out_ptrs = (_ptr(self.obs), _ptr(self.reward), _ptr(self.terminated), _ptr(self.truncated))
+        self._tobs_ptr = _ptr(self.terminal_obs)
         self.reset()
 
     # ------------------------------------------------------------------ lifecycle
@@ -167,10 +183,14 @@ class BatchedAviarySim:
             a = torch.as_tensor(a, dtype=torch.float32, device=self.device).contiguous()
         if a.numel() != self.n_drones * self.act_width:
             raise ValueError(f"actions must have {self.n_envs}x{self.drones_per_env}x{self.act_width} elements")
-        with torch.cuda.device(self.device):
-            self._call("gpd_step", _ptr(a), _ptr(self.obs), _ptr(self.reward), _ptr(self.terminated),
-                       _ptr(self.truncated), _ptr(self.terminal_obs) if terminal_obs else None,
-                       _stream(self.device))
+        tptr = self._tobs_ptr if terminal_obs else None
+        if torch.cuda.current_device() == self.device.index:
+            rc = self._step_fn(self._h, a.data_ptr(), *self._out_ptrs, tptr, _raw_stream(self.device.index))
+        else:
+            with torch.cuda.device(self.device):
+                rc = self._step_fn(self._h, a.data_ptr(), *self._out_ptrs, tptr, _stream(self.device))
+        if rc != 0:
+            _lib.check("gpd_step", rc)
         return self.obs, self.reward, self.terminated, self.truncated
 
     def capture_graph(self, actions_seq, terminal_obs=True):
