@@ -181,6 +181,15 @@ __device__ __forceinline__ void store_drone(const SimView<R>& v, long long n, co
 // vector-memory operation in flight, including an LDS-DMA that nobody reads until much later.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// LDS exchange among the lanes of ONE wave (the step / integrate kernels' blocks are one wave):
+// a wave's LDS instructions execute in order, so a later ds_read sees an earlier ds_write of
+// any lane without a wait or a hardware barrier; the fence only keeps the compiler from
+// reordering the accesses.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // One physics substep of every drone of the block, including the readback that precedes it
 // (BaseAviary.py:343-372 loop body).  MULTI: envs have D > 1 drones and may need downwash.
 template <typename R, bool MULTI, int PF, bool ANGV = true>
@@ -190,7 +199,7 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
   R dw = R(0);
   if (MULTI && pf_on<PF>(k.flags, F_DW)) {
     sx[tid] = s.px; sy[tid] = s.py; sz[tid] = s.pz;
-    lds_barrier();
+    wave_lds_sync();
     if (pairs.n > 0) {
       for (int p = tid; p < pairs.n; p += kWave) {
         const int i = (p * pairs.dmagic) >> 20;          // drone of the block
@@ -198,13 +207,13 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
         const int ib = ((i * pairs.dmagic) >> 20) * D;   // the env's first drone in the block
         spair[p] = dw_pair(sx[i], sy[i], sz[i], sx[ib + j], sy[ib + j], sz[ib + j], c);
       }
-      lds_barrier();
+      wave_lds_sync();
       if (tid * D < pairs.n)
         for (int j = 0; j < D; ++j) dw = dw + spair[tid * D + j];
     } else {
       dw = downwash_sum(s.px, s.py, s.pz, sx, sy, sz, base, D, c);
     }
-    lds_barrier();
+    wave_lds_sync();
   }
   dyn_substep<R, PF, ANGV>(s, rpm, W, last, dw, c, k);
 }
