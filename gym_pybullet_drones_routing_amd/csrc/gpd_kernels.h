@@ -465,7 +465,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
       srew[tid] = (float)r;
       sdist[tid] = (float)dist;
       sflag[tid] = oob ? 1 : 0;
-      lds_barrier();   // not __syncthreads(): its fence would wait for the history DMA in flight
+      wave_lds_sync();   // one-wave block; no __syncthreads(): its fence would wait for the history DMA
       if (d == 0) {
         // MultiHoverAviary: summed reward, sum of distances < 1e-4, any drone out of bounds
         float rs = 0.0f, ds = 0.0f;
@@ -477,7 +477,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, co
         sflag[tid] = (term ? 1 : 0) | (trunc ? 2 : 0);
         srew[tid] = reward;
       }
-      lds_barrier();
+      wave_lds_sync();
       const int fl = sflag[base];
       term = fl & 1;
       trunc = (fl >> 1) & 1;
