@@ -298,10 +298,17 @@ int launch_integrate(gpd_sim* s, const void* rpm, int n_sub, void* traj, hipStre
   const SimView<R> v = make_view<R>(s);
   const Consts<R>* c = (const Consts<R>*)s->d_consts;
   const unsigned grid = grid_for(s->N, s->tpb);
-  if (s->D > 1)
-    hipLaunchKernelGGL((integrate_kernel<R, true>), dim3(grid), dim3(kWave), 0, st, v, c, (const R*)rpm, n_sub, (R*)traj);
-  else
-    hipLaunchKernelGGL((integrate_kernel<R, false>), dim3(grid), dim3(kWave), 0, st, v, c, (const R*)rpm, n_sub, (R*)traj);
+  // plain DYN (the raw-integrator bench) compiled without flag tests; everything else at run time
+  const bool plain = s->cfg.physics_flags == 0;
+  const R* r = (const R*)rpm;
+  R* tr = (R*)traj;
+  if (s->D > 1) {
+    if (plain) hipLaunchKernelGGL((integrate_kernel<R, true, 0>), dim3(grid), dim3(kWave), 0, st, v, c, r, n_sub, tr);
+    else hipLaunchKernelGGL((integrate_kernel<R, true, kPfRuntime>), dim3(grid), dim3(kWave), 0, st, v, c, r, n_sub, tr);
+  } else {
+    if (plain) hipLaunchKernelGGL((integrate_kernel<R, false, 0>), dim3(grid), dim3(kWave), 0, st, v, c, r, n_sub, tr);
+    else hipLaunchKernelGGL((integrate_kernel<R, false, kPfRuntime>), dim3(grid), dim3(kWave), 0, st, v, c, r, n_sub, tr);
+  }
   HIP_TRY(hipGetLastError());
   return GPD_OK;
 }

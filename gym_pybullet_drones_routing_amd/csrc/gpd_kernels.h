@@ -27,6 +27,7 @@
 //   * the tile is then streamed out with coalesced write-through 16-byte (A=4) / 4-byte
 //     (A=1, 3) stores.
 #pragma once
+#include <type_traits>
 #include "gpd_ctrl.h"
 #include "gpd_device.h"
 
@@ -824,7 +825,8 @@ __global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ sta
 
 // ---------------------------------------------------------------------------------------
 // gpd_integrate: n_sub raw substeps with explicit per-substep RPMs, each followed by a readback.
-template <typename R, bool MULTI>
+// PF as in step_kernel: 0 (plain DYN, the raw-integrator bench) or kPfRuntime.
+template <typename R, bool MULTI, int PF>
 __global__ __launch_bounds__(kWave) void integrate_kernel(SimView<R> v, const Consts<R>* __restrict__ cp,
                                                           const R* __restrict__ rpm_in, int n_sub, R* __restrict__ traj) {
   __shared__ R sx[MULTI ? 2 * kWave : 1], sy[MULTI ? 2 * kWave : 1], sz[MULTI ? 2 * kWave : 1];
@@ -842,22 +844,32 @@ __global__ __launch_bounds__(kWave) void integrate_kernel(SimView<R> v, const Co
   load_drone(v, nn, s, last, true);
   const long long N = v.N;
   const DynK<R> dk = dyn_consts(c);
-  // RPMs of substep t+1 are loaded while substep t integrates (one load round trip per launch
-  // instead of one per substep)
-  R nxt[4];
-  {
-    const R* src = rpm_in + nn * 4;
-    nxt[0] = src[0]; nxt[1] = src[1]; nxt[2] = src[2]; nxt[3] = src[3];
-  }
+  // RPMs are loaded two substeps ahead of their use (substeps t+1 and t+2 in flight while t
+  // integrates): more bytes in flight per wave for the HBM stream.  A drone's 4 RPMs are one
+  // aligned 4*sizeof(R)-byte vector (rows of the [T][N][4] tensor).
+  using V = typename std::conditional<sizeof(R) == 8, double2, float4>::type;
+  auto load4 = [&](int t, R out[4]) {
+    const R* src = rpm_in + ((long long)t * N + nn) * 4;
+    if (sizeof(R) == 8) {
+      const double2 a = reinterpret_cast<const double2*>(src)[0], b = reinterpret_cast<const double2*>(src)[1];
+      out[0] = (R)a.x; out[1] = (R)a.y; out[2] = (R)b.x; out[3] = (R)b.y;
+    } else {
+      const float4 a = *reinterpret_cast<const float4*>(src);
+      out[0] = (R)a.x; out[1] = (R)a.y; out[2] = (R)a.z; out[3] = (R)a.w;
+    }
+  };
+  (void)sizeof(V);
+  R nxt[4], nxt2[4];
+  if (n_sub > 0) load4(0, nxt);
+  if (n_sub > 1) load4(1, nxt2);
   for (int t = 0; t < n_sub; ++t) {
     R rpm[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
-    if (t + 1 < n_sub) {
-      const R* src = rpm_in + ((long long)(t + 1) * N + nn) * 4;
-      nxt[0] = src[0]; nxt[1] = src[1]; nxt[2] = src[2]; nxt[3] = src[3];
-    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) nxt[k] = nxt2[k];
+    if (t + 2 < n_sub) load4(t + 2, nxt2);
     R W[4];
-    rpm_wrench<R, kPfRuntime>(rpm, dk, c, W);
-    substep_block<R, MULTI, kPfRuntime>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D);
+    rpm_wrench<R, PF>(rpm, dk, c, W);
+    substep_block<R, MULTI, PF>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];
     if (traj && active) {
