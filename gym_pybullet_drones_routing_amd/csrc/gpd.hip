@@ -302,13 +302,17 @@ int launch_integrate(gpd_sim* s, const void* rpm, int n_sub, void* traj, hipStre
   const bool plain = s->cfg.physics_flags == 0;
   const R* r = (const R*)rpm;
   R* tr = (R*)traj;
-  if (s->D > 1) {
-    if (plain) hipLaunchKernelGGL((integrate_kernel<R, true, 0>), dim3(grid), dim3(kWave), 0, st, v, c, r, n_sub, tr);
-    else hipLaunchKernelGGL((integrate_kernel<R, true, kPfRuntime>), dim3(grid), dim3(kWave), 0, st, v, c, r, n_sub, tr);
+  const void* f;
+  if (tr) {
+    f = s->D > 1 ? (const void*)integrate_kernel<R, true, kPfRuntime, true>
+                 : (const void*)integrate_kernel<R, false, kPfRuntime, true>;
+  } else if (s->D > 1) {
+    f = plain ? (const void*)integrate_kernel<R, true, 0, false> : (const void*)integrate_kernel<R, true, kPfRuntime, false>;
   } else {
-    if (plain) hipLaunchKernelGGL((integrate_kernel<R, false, 0>), dim3(grid), dim3(kWave), 0, st, v, c, r, n_sub, tr);
-    else hipLaunchKernelGGL((integrate_kernel<R, false, kPfRuntime>), dim3(grid), dim3(kWave), 0, st, v, c, r, n_sub, tr);
+    f = plain ? (const void*)integrate_kernel<R, false, 0, false> : (const void*)integrate_kernel<R, false, kPfRuntime, false>;
   }
+  void* args[] = {(void*)&v, (void*)&c, (void*)&r, (void*)&n_sub, (void*)&tr};
+  HIP_TRY(hipLaunchKernel(f, dim3(grid), dim3(kWave), args, 0, st));
   HIP_TRY(hipGetLastError());
   return GPD_OK;
 }

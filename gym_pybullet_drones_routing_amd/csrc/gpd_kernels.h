@@ -34,6 +34,16 @@
 namespace gpd {
 
 constexpr int kStateComps = 20;
+
+// Minimum waves per SIMD the compiler must fit (register budget), for occupancy experiments
+// (-DGPD_INTEGRATE_WPE=n / -DGPD_STEP_WPE=n).  1 = no constraint: forcing 4 waves on the
+// integrate kernel spills to scratch and measured slower (scripts/ab_raw.sh).
+#ifndef GPD_INTEGRATE_WPE
+#define GPD_INTEGRATE_WPE 1
+#endif
+#ifndef GPD_STEP_WPE
+#define GPD_STEP_WPE 1
+#endif
 constexpr int kWave = 64;
 constexpr int kPad = kWave + 1;  // tile column stride (elements)
 
@@ -330,7 +340,7 @@ template <typename R, int ACT, bool MULTI, int PF>
 // The leading scalar arguments duplicate the SimView / StepIO fields the first loads need: the
 // library is built with kernarg preloading, so they arrive in SGPRs at wave launch instead of
 // through an s_load round trip on the kernel-argument segment before the first state load.
-__global__ __launch_bounds__(kWave) void step_kernel(R* __restrict__ state_p, const float* __restrict__ actions_p,
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_WPE))) void step_kernel(R* __restrict__ state_p, const float* __restrict__ actions_p,
                                                      int2* __restrict__ ctr_p, const Consts<R>* __restrict__ cp,
                                                      long long npad_p, int n_p, int tpb_p, SimView<R> v, StepIO<R> io) {
   v.state = state_p; v.ctr = ctr_p; v.npad = npad_p; v.N = n_p; v.tpb = tpb_p;
@@ -825,9 +835,10 @@ __global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ sta
 
 // ---------------------------------------------------------------------------------------
 // gpd_integrate: n_sub raw substeps with explicit per-substep RPMs, each followed by a readback.
-// PF as in step_kernel: 0 (plain DYN, the raw-integrator bench) or kPfRuntime.
-template <typename R, bool MULTI, int PF>
-__global__ __launch_bounds__(kWave) void integrate_kernel(SimView<R> v, const Consts<R>* __restrict__ cp,
+// PF as in step_kernel: 0 (plain DYN, the raw-integrator bench) or kPfRuntime; TRAJ: record the
+// [n_sub][N][20] trajectory.
+template <typename R, bool MULTI, int PF, bool TRAJ>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_INTEGRATE_WPE))) void integrate_kernel(SimView<R> v, const Consts<R>* __restrict__ cp,
                                                           const R* __restrict__ rpm_in, int n_sub, R* __restrict__ traj) {
   __shared__ R sx[MULTI ? 2 * kWave : 1], sy[MULTI ? 2 * kWave : 1], sz[MULTI ? 2 * kWave : 1];
   const Consts<R>& c = *cp;
@@ -872,7 +883,7 @@ __global__ __launch_bounds__(kWave) void integrate_kernel(SimView<R> v, const Co
     substep_block<R, MULTI, PF>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];
-    if (traj && active) {
+    if (TRAJ && active) {   // TRAJ: the trajectory variant (its readback / Euler registers stay out of the other)
       R qn[4], Rm[9], roll, pitch, yaw;
       readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
       quat_to_euler(qn, roll, pitch, yaw);
