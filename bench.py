@@ -64,6 +64,24 @@ def pmc_traffic(grid, precision):
     return best
 
 
+def rocprof_kernel_us(kernel, grid, precision):
+    """Mean duration of `kernel` at `grid` lanes in the newest committed rocprofv3 kernel trace
+    (profiles/*_summary.json "kernels" rows): the rocprof figure the live event time must match."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("precision", "f64") != precision:
+            continue
+        for row in d.get("kernels", []):
+            if row.get("kernel") == kernel and row.get("grid") == grid and "bench" in row.get("trace", ""):
+                best = (row["mean_us"], os.path.relpath(f, ROOT))
+    return best
+
+
 def step_kernel_name(sim, rbytes, act):
     """The step kernel a plain-DYN single-drone sim launches (rocprofv3 name)."""
     real = "double" if rbytes == 8 else "float"
@@ -113,6 +131,54 @@ def cpu_baseline(seconds=10.0, act="rpm"):
             "sample": f"{steps} HoverAviary env.step() calls (cf2x, DYN, RPM, U[-1,1] actions, auto-reset) "
                       f"in {el:.1f} s on 1 core of '{model}' ({ncpu} host CPUs); numpy fp64 restatement of "
                       "BaseAviary.step without pybullet call overhead (flatters the reference)"}
+
+
+def _cpu_env_worker(args):
+    seconds, act, seed = args
+    from oracle.ref_aviary import RefAviary
+    A = 4 if act == "rpm" else 1
+    rng = np.random.default_rng(seed)
+    env = RefAviary(act=act, task="hover")
+    env.reset()
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        a = rng.uniform(-1, 1, (1, A)).astype(np.float32)
+        _, _, te, tr, _ = env.step(a)
+        if te or tr:
+            env.reset()
+        steps += 1
+    return steps, time.perf_counter() - t0
+
+
+def job_cpus():
+    """CPUs this job may use: the scheduler affinity, capped by the pool's per-job share
+    (OMP_NUM_THREADS is set to it on the GPU box; os.cpu_count() there is the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
+
+
+def cpu_baseline_procs(procs, seconds=10.0, act="rpm"):
+    """The reference's own parallelism (SubprocVecEnv / make_vec_env(n_envs=...), examples/learn.py:53-57):
+    one reference-shaped numpy env per process, `procs` processes stepping concurrently; value =
+    the sum of their drone*dt/s."""
+    import multiprocessing as mp
+    with mp.get_context("spawn").Pool(procs) as pool:
+        res = pool.map(_cpu_env_worker, [(seconds, act, 100 + i) for i in range(procs)])
+    steps = sum(r[0] for r in res)
+    rate = sum(r[0] / r[1] for r in res) * 8
+    model, ncpu = cpu_info()
+    return {"value": rate, "unit": "drone*dt/s", "cores": procs, "kind": "port",
+            "per_core": rate / procs,
+            "sample": f"{procs} processes x one HoverAviary env (numpy fp64 restatement, DYN, RPM, U[-1,1], "
+                      f"auto-reset), {steps} env.step() calls in {seconds:.0f} s on '{model}' "
+                      f"({procs} of {ncpu} host CPUs: the job's CPU share)"}
 
 
 def cpu_baseline_openmp(E, seconds=5.0, act="rpm", threads=16):
@@ -177,10 +243,12 @@ def state_parity(device, precision, E=256, T=150, seed=0):
             "vs": "C fp64 restatement of BaseAviary.step (oracle/gpd_oracle.c); PyBullet is unavailable"}
 
 
-def time_graph(sim, pool, steps, warmup, per_graph=16):
+def time_graph(sim, pool, steps, warmup, per_graph=256):
     """Timed region in hipGraph mode: one graph = `per_graph` consecutive env.step() launches
     reading distinct pre-filled action slots, plus one graph of the remaining steps % per_graph
-    launches, so that exactly `steps` steps are timed (and `warmup` untimed ones run first).
+    launches, so that exactly `steps` steps are timed.  Before the timed region every captured
+    graph is replayed at least once (the first replay of a graph pays its upload to the device),
+    then `warmup` further untimed steps run, whatever `warmup` is.
     A HIP event pair on the launch stream brackets the replays, so (event time / launches) is
     the step kernel's average duration including the in-graph kernel boundary (an upper bound;
     rocprofv3 reports the kernel alone).  Returns (wall seconds, steps run, kernel us)."""
@@ -190,6 +258,10 @@ def time_graph(sim, pool, steps, warmup, per_graph=16):
     reps, rem = divmod(steps, per_graph)
     graph = sim.capture_graph([pool[k % P] for k in range(per_graph)])
     tail = sim.capture_graph([pool[k % P] for k in range(rem)]) if rem else None
+    # first replays (graph upload) outside the timed region, then the requested warm-up steps
+    graph.replay()
+    if tail is not None:
+        tail.replay()
     wreps, wrem = divmod(max(0, int(warmup)), per_graph)
     for _ in range(wreps):
         graph.replay()
@@ -321,9 +393,10 @@ def make_pool(E, A, device, seed, pool=64):
     return (torch.rand((pool, E, 1, A), generator=g, device=device) * 2 - 1).contiguous()
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without WORLD_SIZE in the env, bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
@@ -331,13 +404,63 @@ def main():
     ap.add_argument("--precision", default="f64", choices=["f32", "f64"],
                     help="f64 (default) is the parity-gated path (<=1e-10 vs the fp64 oracle)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="processes of the all-core CPU baseline (0 = the CPUs this job may use)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of hipGraph replays")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the real multi-GPU path); gloo only to rehearse several ranks on one GPU")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_entry(rank, world, port, argv):
+    """A self-launched rank (fresh interpreter, torch.multiprocessing spawn): the torchrun env."""
+    os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    run(parse_args(argv))
+
+
+def main():
+    args = parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}; launch one rank per GPU")
+        run(args)
+        return
+    if args.gpus <= 1:
+        run(args)
+        return
+    # --gpus N without a launcher: start N rank processes before anything touches the GPU
+    # (device_count() does not initialise HIP on this image)
+    n_dev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and n_dev < args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs for RCCL, {n_dev} visible "
+                         "(--dist-backend gloo rehearses several ranks on one GPU)")
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_entry, args=(r, args.gpus, port, sys.argv[1:])) for r in range(args.gpus)]
+    for p in procs:
+        p.start()
+    codes = []
+    for p in procs:
+        p.join()
+        codes.append(p.exitcode)
+    bad = [c for c in codes if c != 0]
+    if bad:
+        raise SystemExit(f"bench.py: rank exit codes {codes}")
+
+
+def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -355,7 +478,7 @@ def main():
     torch.cuda.set_device(device)
 
     from gym_pybullet_drones_routing_amd.enums import ActionType
-    from gym_pybullet_drones_routing_amd.shard import gather_batch, max_over_ranks, rank_seed
+    from gym_pybullet_drones_routing_amd.shard import LearnerHandoff, max_over_ranks, rank_seed
     from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
 
     E = args.envs
@@ -403,28 +526,41 @@ def main():
 
     grid_lanes = -(-sim.n_drones // sim.constants.drones_per_block) * sim.constants.lanes_per_block  # launch geometry
     result["roofline"]["grid_lanes"] = grid_lanes
+    rp = rocprof_kernel_us(result["roofline"]["kernel"], grid_lanes, args.precision)
+    if rp is not None:
+        result["roofline"]["kernel_us_rocprof"] = rp[0]
+        result["roofline"]["kernel_us_rocprof_source"] = rp[1]
     tr = pmc_traffic(grid_lanes, args.precision)
     if tr is not None:
         result["roofline"]["traffic"] = tr[0]
         result["roofline"]["traffic_source"] = tr[1] + " (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate passes)"
     if world > 1:
-        # config 5: RCCL all-gather of the observation batch (+ reward / done) to the learner
-        obs_all = torch.empty((world * E,) + tuple(sim.obs.shape[1:]), dtype=sim.obs.dtype, device=device)
-        rew_all = torch.empty((world * E,), dtype=torch.float32, device=device)
+        # config 5: the learner hand-off (shard.LearnerHandoff): rank 0 scatters the global action
+        # batch, every rank steps its shard, one all-gather of the output packs (obs, reward,
+        # terminated, truncated, terminal rows) returns the step to the learner
+        handoff = LearnerHandoff(sim, E * world)
+        gpool = None
+        if rank == 0:
+            gpool = make_pool(E * world, A, device, seed=11, pool=8)
+        G = max(10, args.steps // 3)
+        for k in range(3):
+            handoff.step(gpool[k % 8] if rank == 0 else None)
+        torch.cuda.synchronize(device)
         torch.distributed.barrier()
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
-        G = max(10, args.steps // 3)
         for k in range(G):
-            sim.step(pool[k % pool.shape[0]])
-            gather_batch(sim.obs, obs_all)
-            gather_batch(sim.reward, rew_all)
+            handoff.step(gpool[k % 8] if rank == 0 else None)
         torch.cuda.synchronize(device)
         gw = max_over_ranks(time.perf_counter() - t0, device)
-        coll = "RCCL" if args.dist_backend == "nccl" else "gloo (rehearsal)"
-        result["gather"] = {"mode": f"eager step + {coll} all_gather of obs and reward per step",
+        coll = "RCCL" if args.dist_backend == "nccl" else "gloo (rehearsal, through host memory)"
+        act_b, pack_b = handoff.bytes_per_step()
+        result["gather"] = {"mode": f"learner hand-off per step: {coll} scatter of actions from rank 0, eager "
+                                    "shard step, all_gather_into_tensor of the output packs (obs, reward, "
+                                    "terminated, truncated, terminal obs)",
                             "ms_per_step": 1000 * gw / G, "value": world * E * nsub * G / gw,
-                            "bytes_per_step": int(obs_all.numel() * 4 + rew_all.numel() * 4)}
+                            "action_bytes_per_step": act_b, "gathered_bytes_per_step": pack_b,
+                            "pack_bytes_per_rank": handoff.nbytes}
 
     if rank == 0 and world == 1 and not args.no_sweep:
         sweep = []
@@ -449,11 +585,18 @@ def main():
         result["raw_integrator"] = raw_integrator(device, args.precision)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.act)
+        # the reference's parallelism: one numpy env per process on every CPU of the job's share
+        # (cpu_baseline), beside the same on 1 core and the C/OpenMP restatement on those CPUs
+        ncores = args.cpu_procs or job_cpus()
+        one = cpu_baseline(args.cpu_seconds, args.act)
+        try:
+            result["cpu_baseline"] = cpu_baseline_procs(ncores, args.cpu_seconds, args.act)
+        except Exception as exc:
+            result["cpu_baseline"] = dict(one, error_all_cores=str(exc))
+        result["cpu_baseline_1core"] = one
         result["speedup_vs_cpu_baseline"] = value / result["cpu_baseline"]["value"]
         try:
-            result["cpu_baseline_openmp"] = cpu_baseline_openmp(E, args.cpu_seconds, args.act,
-                                                                threads=min(16, os.cpu_count() or 1))
+            result["cpu_baseline_openmp"] = cpu_baseline_openmp(E, args.cpu_seconds, args.act, threads=ncores)
         except Exception as exc:  # the C oracle is optional for the bench
             result["cpu_baseline_openmp"] = {"error": str(exc)}
         try:

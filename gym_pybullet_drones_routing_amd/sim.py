@@ -79,6 +79,21 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+def pack_layout(n_envs, drones_per_env, obs_width, align=256):
+    """Byte layout of a sim's output pack: {field: (offset, nbytes)}, "total", and "prefix" = the
+    bytes up to the end of the truncated flags (the hand-off without terminal rows)."""
+    E, D, W = n_envs, drones_per_env, obs_width
+    out, off = {}, 0
+    for name, nbytes in (("obs", E * D * W * 4), ("reward", E * 4), ("terminated", E), ("truncated", E),
+                         ("terminal_obs", E * D * W * 4)):
+        out[name] = (off, nbytes)
+        if name == "truncated":
+            out["prefix"] = off + nbytes
+        off += -(-nbytes // align) * align
+    out["total"] = off
+    return out
+
+
 class BatchedAviarySim:
     """``n_envs`` x ``drones_per_env`` Crazyflie-class drones stepped in lockstep on one GPU."""
 
@@ -133,17 +148,28 @@ class BatchedAviarySim:
         self.pyb_steps_per_ctrl = k.pyb_steps_per_ctrl
         E, D, W = self.n_envs, self.drones_per_env, self.obs_width
         dev = self.device
-        self.obs = torch.zeros((E, D, W), dtype=torch.float32, device=dev)
-        self.terminal_obs = torch.zeros((E, D, W), dtype=torch.float32, device=dev)
-        self.reward = torch.zeros((E,), dtype=torch.float32, device=dev)
-        self.terminated = torch.zeros((E,), dtype=torch.uint8, device=dev)
-        self.truncated = torch.zeros((E,), dtype=torch.uint8, device=dev)
+        # every per-step output lives in ONE device buffer ("out pack"), so that a sharded run hands
+        # a step to the learner with a single collective over the kernel's own output bytes
+        # (shard.LearnerHandoff): [obs | reward | terminated | truncated | terminal_obs], each field
+        # 256-B aligned; the terminal rows come last so that a hand-off without them is a prefix
+        self.pack_layout = pack_layout(E, D, W)
+        L = self.pack_layout
+        self.out_pack = torch.zeros((L["total"],), dtype=torch.uint8, device=dev)
+        self.obs = self._field("obs", torch.float32, (E, D, W))
+        self.reward = self._field("reward", torch.float32, (E,))
+        self.terminated = self._field("terminated", torch.uint8, (E,))
+        self.truncated = self._field("truncated", torch.uint8, (E,))
+        self.terminal_obs = self._field("terminal_obs", torch.float32, (E, D, W))
         # the sim-owned output buffers never move: their ctypes pointers are built once (the eager
         # step() is host-bound at 4096 envs, a few microseconds per call)
         self._step_fn = self._lib.gpd_step
         self._out_ptrs = (_ptr(self.obs), _ptr(self.reward), _ptr(self.terminated), _ptr(self.truncated))
         self._tobs_ptr = _ptr(self.terminal_obs)
         self.reset()
+
+    def _field(self, name, dtype, shape):
+        off, n = self.pack_layout[name]
+        return self.out_pack[off:off + n].view(dtype).view(shape)
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):

@@ -83,3 +83,87 @@ def test_env_shard_split():
     assert [env_shard(32768, r, 8) for r in (0, 7)] == [(0, 4096), (28672, 4096)]
     with pytest.raises(ValueError):
         env_shard(10, 0, 3)
+
+
+class _PackedOracleShard:
+    """C oracle with the HIP sim's output pack (sim.pack_layout): what LearnerHandoff gathers."""
+
+    def __init__(self, n_envs, drones_per_env=1, **kw):
+        from gym_pybullet_drones_routing_amd.sim import pack_layout
+        from oracle.c_oracle import COracle
+        self.o = COracle(n_envs=n_envs, drones_per_env=drones_per_env, threads=1, **kw)
+        self.n_envs, self.drones_per_env, self.obs_width = n_envs, drones_per_env, self.o.W
+        self.act_width = self.o.A
+        self.pack_layout = pack_layout(n_envs, drones_per_env, self.o.W)
+        self.out_pack = torch.zeros((self.pack_layout["total"],), dtype=torch.uint8)
+
+    def _put(self, name, arr):
+        off, n = self.pack_layout[name]
+        self.out_pack[off:off + n] = torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8).reshape(-1))
+
+    def reset(self):
+        self._put("obs", self.o.reset())
+
+    def step(self, actions, terminal_obs=True):
+        self.o.step(actions.numpy())
+        for name in ("obs", "reward", "terminated", "truncated", "terminal_obs"):
+            self._put(name, getattr(self.o, name))
+
+
+def _handoff_worker(rank, world, port, E, T, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gym_pybullet_drones_routing_amd.shard import LearnerHandoff, env_shard
+        _, count = env_shard(E, rank, world)
+        h = LearnerHandoff(_PackedOracleShard(count, task="hover"), E)
+        rng = np.random.default_rng(1)
+        acts = rng.uniform(-1, 1, (T, E, 1, 4)).astype(np.float32)
+        acts[:, :2] *= 0.05                          # long-lived envs beside ones that end early
+        outs = [h.reset()]
+        for t in range(T):
+            # only the learner holds the action batch
+            r = h.step(torch.from_numpy(acts[t]) if rank == 0 else None)
+            assert (r is None) == (rank != 0)
+            if rank == 0:
+                outs.append(tuple(x.numpy().copy() for x in r))
+        if rank == 0:
+            q.put((outs, h.bytes_per_step()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_learner_handoff_gloo_matches_one_process():
+    """Rank-0 learner scatters actions, shards step, one all-gather of the output packs: the
+    learner's batch (incl. terminal rows after auto-resets) equals one process stepping all envs."""
+    from oracle.c_oracle import COracle
+    E, T, world = 8, 40, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_handoff_worker, args=(r, world, port, E, T, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs, (act_bytes, pack_bytes) = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert act_bytes == E * 4 * 4 and pack_bytes > 2 * E * 72 * 4
+    ref = COracle(n_envs=E, task="hover", threads=1)
+    np.testing.assert_array_equal(outs[0], ref.reset())
+    rng = np.random.default_rng(1)
+    acts = rng.uniform(-1, 1, (T, E, 1, 4)).astype(np.float32)
+    acts[:, :2] *= 0.05
+    n_done = 0
+    for t in range(T):
+        o, r, te, tr = ref.step(acts[t])
+        obs, rew, gte, gtr, tobs = outs[t + 1]
+        np.testing.assert_array_equal(obs, o)
+        np.testing.assert_array_equal(rew, r)
+        np.testing.assert_array_equal(gte.astype(bool), te)
+        np.testing.assert_array_equal(gtr.astype(bool), tr)
+        done = te | tr
+        n_done += int(done.sum())
+        np.testing.assert_array_equal(tobs[done], ref.terminal_obs[done])
+    assert n_done > 0

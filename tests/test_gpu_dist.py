@@ -1,0 +1,85 @@
+"""Config-5 learner hand-off driving the HIP sims: two ranks on one GPU (gloo), each stepping
+its own BatchedAviarySim shard through the C ABI, rank 0 scattering the actions and receiving
+the all-gathered output packs.  The learner's batch must be bit-identical to ONE sim stepping
+all envs (envs are independent worlds, BaseAviary.py:170; caller examples/learn.py:52-94)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _actions(E, T, D, A, seed):
+    rng = np.random.default_rng(seed)
+    acts = rng.uniform(-1, 1, (T, E, D, A)).astype(np.float32)
+    acts[:, : E // 2] *= np.float32(0.05)        # long-lived envs beside ones that end early
+    return acts
+
+
+def _worker(rank, world, port, kw, E, T, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gym_pybullet_drones_routing_amd.shard import LearnerHandoff, env_shard
+        from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+        _, count = env_shard(E, rank, world)
+        sim = BatchedAviarySim(n_envs=count, device="cuda:0", **kw)
+        h = LearnerHandoff(sim, E)
+        acts = _actions(E, T, sim.drones_per_env, sim.act_width, 5)
+        outs = [h.reset().cpu().numpy()]
+        for t in range(T):
+            r = h.step(torch.from_numpy(acts[t]).cuda() if rank == 0 else None)
+            if rank == 0:
+                outs.append(tuple(x.cpu().numpy() for x in r))
+        sim.close()
+        if rank == 0:
+            q.put(outs)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kw", [
+    dict(task="hover"),
+    dict(task="multihover", drones_per_env=4, aero=("dw", "gnd", "drag")),
+], ids=["hover", "multihover4_dw"])
+def test_handoff_two_ranks_bit_identical_to_one_sim(kw):
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+    E, T, world = 64, 260, 2          # 260 ctrl steps: past the 242-step time truncation
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kw, E, T, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sim = BatchedAviarySim(n_envs=E, device="cuda:0", **kw)
+    acts = _actions(E, T, sim.drones_per_env, sim.act_width, 5)
+    np.testing.assert_array_equal(outs[0], sim.reset().cpu().numpy())
+    n_done = 0
+    for t in range(T):
+        o, r, te, tr = sim.step(torch.from_numpy(acts[t]).cuda())
+        obs, rew, gte, gtr, tobs = outs[t + 1]
+        np.testing.assert_array_equal(obs, o.cpu().numpy())
+        np.testing.assert_array_equal(rew, r.cpu().numpy())
+        np.testing.assert_array_equal(gte, te.cpu().numpy())
+        np.testing.assert_array_equal(gtr, tr.cpu().numpy())
+        done = (gte | gtr).astype(bool)
+        n_done += int(done.sum())
+        np.testing.assert_array_equal(tobs[done], sim.terminal_obs.cpu().numpy()[done])
+    sim.close()
+    assert n_done > 0
