@@ -813,12 +813,19 @@ __device__ __forceinline__ void pose_half(Drone<R>& s, R fz, const R h[5], const
 // beta = DW2 dz + DW3, f = -alpha exp(-0.5 (dxy/beta)^2); |dxy|^2 needs no square root, and
 // beta = 0 keeps numpy's IEEE result (dxy^2/0 = inf -> exp(-inf) = 0; 0/0 = nan at dxy = 0).
 // The ballot skips the exp block for a whole wave when no lane has an active pair.
+template <typename R> struct DwCull;
+template <> struct DwCull<double> { static constexpr double v = 99.999999999999985789145284797996282577514648437500; };
+template <> struct DwCull<float> { static constexpr float v = 99.99999237060546875f; };
+
 template <typename R>
 __device__ __forceinline__ R dw_pair(R px, R py, R pz, R qx, R qy, R qz, const Consts<R>& c) {
   const R dz = qz - pz;
   const R ddx = qx - px, ddy = qy - py;
   const R dxy2 = ddx * ddx + ddy * ddy;
-  const bool hit = (dz > R(0)) && (dxy2 < R(100));       // delta_z > 0 and delta_xy < 10
+  // delta_z > 0 and delta_xy < 10 (:801).  sqrt is correctly rounded and monotonic, so
+  // sqrt(s) < 10 <=> s < the smallest s' whose sqrt rounds to 10, which is the predecessor of
+  // 100 in both double and float: the exact cull without a square root per pair
+  const bool hit = (dz > R(0)) && (dxy2 < DwCull<R>::v);
   R f = R(0);
   if (__ballot(hit) != 0ull) {
     if (hit) {

@@ -349,7 +349,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
   extern __shared__ float4 tile4[];          // A == 4: [3+L][kPad] float4
   float* tilef = reinterpret_cast<float*>(tile4);  // A == 1, 3: [12+L*A][kPad] float
   __shared__ R sx[MULTI ? 2 * kWave : 1], sy[MULTI ? 2 * kWave : 1], sz[MULTI ? 2 * kWave : 1];
-  __shared__ float srew[MULTI ? 2 * kWave : 1], sdist[MULTI ? 2 * kWave : 1];
+  // per-drone reward / distance in the compute precision: MultiHoverAviary sums both in fp64
+  // (MultiHoverAviary.py:75-106) and tests the summed distance against 1e-4
+  __shared__ R srew[MULTI ? 2 * kWave : 1], sdist[MULTI ? 2 * kWave : 1];
   __shared__ int sflag[MULTI ? 2 * kWave : 1];
   __shared__ R spair[MULTI ? kPairMax : 1];
   GPD_RSTAMP(11);
@@ -464,26 +466,26 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
   if (v.task != TASK_NONE) {
     const R* tg = MULTI ? v.target + d * 3 : c.target0;
     const R tx = tg[0] - s.px, ty = tg[1] - s.py, tz = tg[2] - s.pz;
-    // |e|^2: the reward max(0, 2 - |e|^4) and HoverAviary's |e| < 1e-4 need no square root;
-    // MultiHoverAviary sums the distances themselves
+    // |e|^2 gives the reward max(0, 2 - |e|^4); the done test is made on |e| itself, as the
+    // reference's np.linalg.norm(...) < .0001 (HoverAviary.py:92, MultiHoverAviary.py:101-104)
     const R d2 = tx * tx + ty * ty + tz * tz;
-    const R dist = MULTI ? g_sqrt(d2) : R(0);
+    const R dist = g_sqrt(d2);
     R r = R(2) - d2 * d2;
     r = r > R(0) ? r : R(0);
     const bool oob = g_abs(s.px) > v.bound_xy || g_abs(s.py) > v.bound_xy || s.pz > R(2) ||
                      tilted_beyond(att, R(0.38941834230865049), R(0.42279321873816178));  // sin/tan(0.4)
     if (MULTI) {
-      srew[tid] = (float)r;
-      sdist[tid] = (float)dist;
+      srew[tid] = r;
+      sdist[tid] = dist;
       sflag[tid] = oob ? 1 : 0;
       wave_lds_sync();   // one-wave block; no __syncthreads(): its fence would wait for the history DMA
       if (d == 0) {
         // MultiHoverAviary: summed reward, sum of distances < 1e-4, any drone out of bounds
-        float rs = 0.0f, ds = 0.0f;
+        R rs = R(0), ds = R(0);
         int anyo = 0;
         for (int j = 0; j < D; ++j) { rs += srew[base + j]; ds += sdist[base + j]; anyo |= sflag[base + j]; }
-        reward = rs;
-        term = ds < 1e-4f;
+        reward = (float)rs;
+        term = ds < R(1e-4);
         trunc = anyo != 0 || sc >= v.trunc_sc;
         sflag[tid] = (term ? 1 : 0) | (trunc ? 2 : 0);
         srew[tid] = reward;
@@ -492,10 +494,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
       const int fl = sflag[base];
       term = fl & 1;
       trunc = (fl >> 1) & 1;
-      reward = srew[base];
+      reward = (float)srew[base];
     } else {
       reward = (float)r;
-      term = d2 < R(1e-8);
+      term = dist < R(1e-4);
       trunc = oob || sc >= v.trunc_sc;
     }
   }
@@ -772,7 +774,7 @@ __global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ sta
     const bool oob = g_abs(s.px) > v.bound_xy || g_abs(s.py) > v.bound_xy || s.pz > R(2) ||
                      tilted_beyond(att, R(0.38941834230865049), R(0.42279321873816178));  // sin/tan(0.4)
     reward = (float)r;
-    term = d2 < R(1e-8);
+    term = g_sqrt(d2) < R(1e-4);   // np.linalg.norm(...) < .0001 (HoverAviary.py:92)
     trunc = oob || sc >= v.trunc_sc;
   }
   const bool done = term || trunc;

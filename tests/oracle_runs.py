@@ -58,3 +58,13 @@ def run_vec(actions, n_envs, drones_per_env=1, act="rpm", task="hover", envs=Non
             row.append(o)
         obs_l.append(np.stack(row))
     return np.stack(obs_l), rew, te, tr, term_obs
+
+
+def assert_obs_match(gpu, ref, rtol=1e-5, atol=1e-6, err_msg=""):
+    """KIN observation rows [..., 12 + 15A]: the 12 kinematic columns within tolerance, the 15A
+    action-history columns (float32 copies of past actions placed by ring index,
+    BaseRLAviary.py:307-319) bit-exact."""
+    gpu, ref = np.asarray(gpu), np.asarray(ref)
+    assert gpu.shape == ref.shape, (gpu.shape, ref.shape)
+    np.testing.assert_array_equal(gpu[..., 12:], ref[..., 12:], err_msg=f"action history {err_msg}")
+    np.testing.assert_allclose(gpu[..., :12], ref[..., :12], rtol=rtol, atol=atol, err_msg=err_msg)

@@ -7,7 +7,7 @@ import pytest
 
 from oracle.c_oracle import COracle
 from oracle.ref_aviary import RefAviary, rpm_from_action
-from tests.oracle_runs import run_vec, state_rel_err
+from tests.oracle_runs import assert_obs_match, run_vec, state_rel_err
 
 HOVER = 14468.429183500699
 
@@ -71,8 +71,8 @@ def test_step_c_vs_numpy(act, task, D):
         o, r, te, tr = c.step(acts[t])
         np.testing.assert_array_equal(te, te_r[t])
         np.testing.assert_array_equal(tr, tr_r[t])
-        np.testing.assert_allclose(o, obs_r[t], rtol=1e-6, atol=1e-7)
+        assert_obs_match(o, obs_r[t], 1e-6, 1e-7)
         np.testing.assert_allclose(r, rew_r[t], rtol=1e-6, atol=1e-6)
         for e in np.nonzero(te | tr)[0]:
-            np.testing.assert_allclose(c.terminal_obs[e], tobs_r[(t, e)], rtol=1e-6, atol=1e-7)
+            assert_obs_match(c.terminal_obs[e], tobs_r[(t, e)], 1e-6, 1e-7)
     c.close()

@@ -9,6 +9,8 @@ import numpy as np
 import pytest
 import torch
 
+from tests.oracle_runs import assert_obs_match
+
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
@@ -84,9 +86,9 @@ def test_hover_aviary_gym_surface(fixture, act):
         obs, r, te, tr, info = env.step(fx["actions"][t, 0])
         assert isinstance(r, float) and isinstance(te, bool) and isinstance(tr, bool)
         if te or tr:       # the fixture was made with auto-reset; the Gym view resets explicitly
-            np.testing.assert_allclose(obs, fx["terminal_obs"][keys[(t, 0)]], rtol=1e-5, atol=1e-5)
+            assert_obs_match(obs, fx["terminal_obs"][keys[(t, 0)]], 1e-5, 1e-5)
             obs, _ = env.reset()
-        np.testing.assert_allclose(obs, fx["obs"][t, 0], rtol=1e-5, atol=1e-5)
+        assert_obs_match(obs, fx["obs"][t, 0], 1e-5, 1e-5)
         assert te == bool(fx["terminated"][t, 0]) and tr == bool(fx["truncated"][t, 0])
     s = env._getDroneStateVector(0)
     assert s.shape == (20,)
@@ -122,7 +124,7 @@ def test_vec_env_sb3_semantics(output):
         if output == "torch":
             obs, rew, done = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy()
             tobs = infos["terminal_observation"].cpu().numpy()
-        np.testing.assert_allclose(obs, fx["obs"][t], rtol=1e-5, atol=1e-5)
+        assert_obs_match(obs, fx["obs"][t], 1e-5, 1e-5)
         np.testing.assert_allclose(rew, fx["reward"][t], rtol=1e-5, atol=1e-5)
         np.testing.assert_array_equal(done, fx["terminated"][t] | fx["truncated"][t])
         for e in np.nonzero(done)[0]:

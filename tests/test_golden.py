@@ -12,7 +12,7 @@ import pytest
 from oracle.c_oracle import COracle
 from oracle.params import derived
 from oracle.ref_aviary import RefAviary, rpm_from_action
-from tests.oracle_runs import run_vec, state_rel_err
+from tests.oracle_runs import assert_obs_match, run_vec, state_rel_err
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 HOVER = derived("cf2x")["hover_rpm"]
@@ -45,12 +45,12 @@ def test_fixture_set_complete():
 def _check_step_outputs(fx, t, o, r, te, tr, tobs, obs_tol, rew_tol):
     np.testing.assert_array_equal(te, fx["terminated"][t])
     np.testing.assert_array_equal(tr, fx["truncated"][t])
-    np.testing.assert_allclose(o, fx["obs"][t], rtol=obs_tol, atol=obs_tol)
+    assert_obs_match(o, fx["obs"][t], obs_tol, obs_tol)
     np.testing.assert_allclose(r, fx["reward"][t], rtol=rew_tol, atol=rew_tol)
     keys = [tuple(k) for k in fx["terminal_keys"]]
     for i, (tt, e) in enumerate(keys):
         if tt == t:
-            np.testing.assert_allclose(tobs[e], fx["terminal_obs"][i], rtol=obs_tol, atol=obs_tol)
+            assert_obs_match(tobs[e], fx["terminal_obs"][i], obs_tol, obs_tol)
 
 
 @pytest.mark.parametrize("name,act,task,D", STEP_FIX)
@@ -59,7 +59,7 @@ def test_numpy_oracle_reproduces_step_fixture(name, act, task, D):
     acts = fx["actions"]
     obs, rew, te, tr, tobs = run_vec(acts, acts.shape[1], drones_per_env=D, act=act, task=task,
                                      integrator=_integrator(fx))
-    np.testing.assert_allclose(obs, fx["obs"], rtol=1e-6, atol=1e-7)
+    assert_obs_match(obs, fx["obs"], 1e-6, 1e-7)
     np.testing.assert_array_equal(te, fx["terminated"])
     np.testing.assert_array_equal(tr, fx["truncated"])
 
@@ -82,7 +82,7 @@ def test_numpy_oracle_reproduces_pid_fixture(name, act):
     acts = fx["actions"]
     envs = []
     obs, rew, te, tr, tobs = run_vec(acts, acts.shape[1], act=act, task="hover", integrator=_integrator(fx), envs=envs)
-    np.testing.assert_allclose(obs, fx["obs"], rtol=1e-6, atol=1e-7)
+    assert_obs_match(obs, fx["obs"], 1e-6, 1e-7)
     np.testing.assert_array_equal(te, fx["terminated"])
     np.testing.assert_array_equal(tr, fx["truncated"])
     np.testing.assert_allclose(np.concatenate([e.ctrl_state() for e in envs]), fx["ctrl_state"], rtol=1e-12, atol=1e-12)

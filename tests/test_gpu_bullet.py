@@ -12,7 +12,7 @@ import pytest
 import torch
 
 from oracle.ref_aviary import RefAviary
-from tests.oracle_runs import run_integrate, run_vec, state_rel_err
+from tests.oracle_runs import assert_obs_match, run_integrate, run_vec, state_rel_err
 from tests.test_gpu_parity import HOVER, TOL, TOL_MEDIAN, _random_raw, _rpms, _sim, _staggered
 
 pytestmark = pytest.mark.gpu
@@ -115,12 +115,12 @@ def test_step_parity_hover_pyb(act):
         te, tr = te.cpu().numpy().astype(bool), tr.cpu().numpy().astype(bool)
         np.testing.assert_array_equal(te, te_r[t])
         np.testing.assert_array_equal(tr, tr_r[t])
-        np.testing.assert_allclose(o.cpu().numpy(), obs_r[t], rtol=1e-5, atol=1e-6)
+        assert_obs_match(o.cpu().numpy(), obs_r[t], 1e-5, 1e-6)
         np.testing.assert_allclose(r.cpu().numpy(), rew_r[t], rtol=1e-6, atol=1e-6)
         tobs = sim.terminal_obs.cpu().numpy()
         for e in np.nonzero(te | tr)[0]:
             n_done += 1
-            np.testing.assert_allclose(tobs[e], tobs_r[(t, e)], rtol=1e-5, atol=1e-6)
+            assert_obs_match(tobs[e], tobs_r[(t, e)], 1e-5, 1e-6)
     assert n_done > 0
     err = state_rel_err(sim.state20().cpu().numpy(), np.concatenate([e.state20() for e in envs]))
     assert err.max() <= TOL["f64"], err.max()
@@ -145,7 +145,7 @@ def test_step_parity_multihover_pyb_all_terms():
         o, r, te, tr = sim.step(torch.from_numpy(acts[t]).cuda())
         np.testing.assert_array_equal(te.cpu().numpy().astype(bool), te_r[t])
         np.testing.assert_array_equal(tr.cpu().numpy().astype(bool), tr_r[t])
-        np.testing.assert_allclose(o.cpu().numpy(), obs_r[t], rtol=1e-5, atol=1e-6)
+        assert_obs_match(o.cpu().numpy(), obs_r[t], 1e-5, 1e-6)
         np.testing.assert_allclose(r.cpu().numpy(), rew_r[t], rtol=1e-6, atol=1e-5)
     err = state_rel_err(sim.state20().cpu().numpy(), np.concatenate([e.state20() for e in envs]))
     assert err.max() <= TOL["f64"], err.max()

@@ -2,7 +2,9 @@
 its own BatchedAviarySim shard through the C ABI, rank 0 scattering the actions and receiving
 the all-gathered output packs.  The learner's batch must be bit-identical to ONE sim stepping
 all envs (envs are independent worlds, BaseAviary.py:170; caller examples/learn.py:52-94)."""
+import datetime
 import os
+import queue
 import socket
 
 import numpy as np
@@ -30,7 +32,7 @@ def _actions(E, T, D, A, seed):
 def _worker(rank, world, port, kw, E, T, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
     try:
         from gym_pybullet_drones_routing_amd.shard import LearnerHandoff, env_shard
         from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
@@ -38,7 +40,8 @@ def _worker(rank, world, port, kw, E, T, q):
         sim = BatchedAviarySim(n_envs=count, device="cuda:0", **kw)
         h = LearnerHandoff(sim, E)
         acts = _actions(E, T, sim.drones_per_env, sim.act_width, 5)
-        outs = [h.reset().cpu().numpy()]
+        o0 = h.reset()
+        outs = [o0.cpu().numpy() if rank == 0 else None]
         for t in range(T):
             r = h.step(torch.from_numpy(acts[t]).cuda() if rank == 0 else None)
             if rank == 0:
@@ -48,6 +51,28 @@ def _worker(rank, world, port, kw, E, T, q):
             q.put(outs)
     finally:
         dist.destroy_process_group()
+
+
+def _collect(q, procs, limit=150):
+    """Rank 0's result; fails as soon as a rank dies instead of waiting out the collective."""
+    for _ in range(limit):
+        try:
+            outs = q.get(timeout=1)
+            break
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead:
+                for p in procs:
+                    p.kill()
+                raise AssertionError(f"a rank exited with {dead}")
+    else:
+        for p in procs:
+            p.kill()
+        raise AssertionError("ranks did not finish")
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return outs
 
 
 @pytest.mark.parametrize("kw", [
@@ -63,10 +88,7 @@ def test_handoff_two_ranks_bit_identical_to_one_sim(kw):
     procs = [ctx.Process(target=_worker, args=(r, world, port, kw, E, T, q)) for r in range(world)]
     for p in procs:
         p.start()
-    outs = q.get(timeout=240)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    outs = _collect(q, procs)
     sim = BatchedAviarySim(n_envs=E, device="cuda:0", **kw)
     acts = _actions(E, T, sim.drones_per_env, sim.act_width, 5)
     np.testing.assert_array_equal(outs[0], sim.reset().cpu().numpy())

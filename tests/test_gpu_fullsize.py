@@ -24,7 +24,7 @@ import pytest
 import torch
 
 from oracle.c_oracle import COracle
-from tests.oracle_runs import state_rel_err
+from tests.oracle_runs import assert_obs_match, state_rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -73,13 +73,12 @@ def test_fullsize_config_parity(case):
         te, tr = te.cpu().numpy().astype(bool), tr.cpu().numpy().astype(bool)
         np.testing.assert_array_equal(te, te_o, err_msg=f"terminated differs at step {t}")
         np.testing.assert_array_equal(tr, tr_o, err_msg=f"truncated differs at step {t}")
-        np.testing.assert_allclose(o.cpu().numpy(), o_o, rtol=1e-5, atol=1e-6)
+        assert_obs_match(o.cpu().numpy(), o_o, 1e-5, 1e-6)
         np.testing.assert_allclose(r.cpu().numpy(), r_o, rtol=1e-6, atol=1e-6)
         done = te | tr
         if done.any():
             n_done += int(done.sum())
-            np.testing.assert_allclose(sim.terminal_obs.cpu().numpy()[done], orc.terminal_obs[done],
-                                       rtol=1e-5, atol=1e-6)
+            assert_obs_match(sim.terminal_obs.cpu().numpy()[done], orc.terminal_obs[done], 1e-5, 1e-6)
         err = state_rel_err(sim.state20().cpu().numpy(), orc.state20())
         worst = max(worst, float(err.max()))
         assert worst <= 1e-10, f"state rel L2 {worst:.3g} at step {t}"

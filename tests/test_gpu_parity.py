@@ -14,7 +14,7 @@ import pytest
 import torch
 
 from oracle.ref_aviary import RefAviary, rpm_from_action
-from tests.oracle_runs import run_integrate, run_vec, state_rel_err
+from tests.oracle_runs import assert_obs_match, run_integrate, run_vec, state_rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -171,17 +171,17 @@ def test_step_parity_hover(prec, act, kernel, monkeypatch):
         if prec == "f64":
             np.testing.assert_array_equal(te, te_r[t])
             np.testing.assert_array_equal(tr, tr_r[t])
-            np.testing.assert_allclose(o, obs_r[t], rtol=1e-5, atol=1e-6)
+            assert_obs_match(o, obs_r[t], 1e-5, 1e-6)
             np.testing.assert_allclose(r, rew_r[t], rtol=1e-6, atol=1e-6)
         else:
             same = (te == te_r[t]) & (tr == tr_r[t])
             assert same.all(), f"done flags differ at step {t}"
-            np.testing.assert_allclose(o, obs_r[t], rtol=1e-4, atol=1e-4)
+            assert_obs_match(o, obs_r[t], 1e-4, 1e-4)
             np.testing.assert_allclose(r, rew_r[t], rtol=1e-4, atol=1e-4)
         tobs = sim.terminal_obs.cpu().numpy()
         for e in np.nonzero(te | tr)[0]:
             n_done += 1
-            np.testing.assert_allclose(tobs[e], tobs_r[(t, e)], rtol=1e-4, atol=1e-4)
+            assert_obs_match(tobs[e], tobs_r[(t, e)], 1e-4, 1e-4)
     assert n_done > 0, "test inputs should force at least one auto-reset"
     sim.close()
 
@@ -218,8 +218,9 @@ def test_duo_kernel_matches_single_wave(prec, act, monkeypatch):
         (oa, rwa, tea, tra, ta), (ob, rwb, teb, trb, tb) = ra[t], rb[t]
         np.testing.assert_array_equal(tea, teb, err_msg=f"terminated, step {t}")
         np.testing.assert_array_equal(tra, trb, err_msg=f"truncated, step {t}")
-        for x, y in ((oa, ob), (rwa, rwb), (ta, tb)):
-            np.testing.assert_allclose(x, y, rtol=tol, atol=tol if prec == "f64" else 1e-5, err_msg=f"step {t}")
+        for x, y in ((oa, ob), (ta, tb)):
+            assert_obs_match(x, y, tol, tol if prec == "f64" else 1e-5, err_msg=f"step {t}")
+        np.testing.assert_allclose(rwa, rwb, rtol=tol, atol=tol if prec == "f64" else 1e-5, err_msg=f"step {t}")
     assert state_rel_err(sa, sb).max() <= tol
 
 
@@ -234,7 +235,7 @@ def test_step_parity_multihover(D):
         o, r, te, tr = sim.step(torch.from_numpy(acts[t]).cuda())
         np.testing.assert_array_equal(te.cpu().numpy().astype(bool), te_r[t])
         np.testing.assert_array_equal(tr.cpu().numpy().astype(bool), tr_r[t])
-        np.testing.assert_allclose(o.cpu().numpy(), obs_r[t], rtol=1e-5, atol=1e-6)
+        assert_obs_match(o.cpu().numpy(), obs_r[t], 1e-5, 1e-6)
         np.testing.assert_allclose(r.cpu().numpy(), rew_r[t], rtol=1e-6, atol=1e-5)
     sim.close()
 
@@ -354,7 +355,7 @@ def test_step_parity_aero_configs(case):
         o, r, te, tr = sim.step(torch.from_numpy(acts[t]).cuda())
         np.testing.assert_array_equal(te.cpu().numpy().astype(bool), te_r[t])
         np.testing.assert_array_equal(tr.cpu().numpy().astype(bool), tr_r[t])
-        np.testing.assert_allclose(o.cpu().numpy(), obs_r[t], rtol=1e-5, atol=1e-6)
+        assert_obs_match(o.cpu().numpy(), obs_r[t], 1e-5, 1e-6)
         np.testing.assert_allclose(r.cpu().numpy(), rew_r[t], rtol=1e-6, atol=1e-5)
     ref = np.concatenate([e.state20() for e in envs])
     err = state_rel_err(sim.state20().cpu().numpy(), ref)
