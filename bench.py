@@ -86,8 +86,8 @@ def step_kernel_name(sim, rbytes, act):
     """The step kernel a plain-DYN single-drone sim launches (rocprofv3 name)."""
     real = "double" if rbytes == 8 else "float"
     a = 0 if act == "rpm" else 1
-    if sim.constants.lanes_per_block == 128:
-        return "gpd::step_kernel_duo<%s, %d>" % (real, a)
+    if sim.constants.lanes_per_block in (128, 192):
+        return "gpd::step_kernel_duo<%s, %d, %s>" % (real, a, "true" if sim.constants.lanes_per_block == 192 else "false")
     return "gpd::step_kernel<%s, %d, false, 0>" % (real, a)
 
 

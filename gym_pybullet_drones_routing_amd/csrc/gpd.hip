@@ -116,7 +116,8 @@ struct gpd_sim {
   int tile_bytes = 0;             // dynamic LDS of the step kernel
   int wt = 0;                     // SimView::wt (write-through store policy)
   int nc_magic = 0;               // SimView::nc_magic
-  bool duo = false;               // step launches step_kernel_duo (two waves per block)
+  bool duo = false;               // step launches step_kernel_duo (two or three waves per block)
+  int step_waves = 1;             // waves per step block (1, 2, or 3 with the io wave)
   DwPairs dw_pairs{0, 0};         // SimView::dw_pairs
   double bound_xy;
   std::vector<double> init_tmpl;  // [D][10]
@@ -240,9 +241,12 @@ const void* step_fn_pid(bool multi, int flags) {
 }
 template <typename R>
 const void* step_kernel_fn(const gpd_sim* s) {
+  if (s->step_waves == 3)
+    return s->cfg.act_type == GPD_ACT_RPM ? (const void*)step_kernel_duo<R, ACT_RPM, true>
+                                          : (const void*)step_kernel_duo<R, ACT_ONE_D_RPM, true>;
   if (s->duo)
-    return s->cfg.act_type == GPD_ACT_RPM ? (const void*)step_kernel_duo<R, ACT_RPM>
-                                          : (const void*)step_kernel_duo<R, ACT_ONE_D_RPM>;
+    return s->cfg.act_type == GPD_ACT_RPM ? (const void*)step_kernel_duo<R, ACT_RPM, false>
+                                          : (const void*)step_kernel_duo<R, ACT_ONE_D_RPM, false>;
   const bool multi = s->D > 1;
   // the flags the kernel sees (Consts::flags, make_consts)
   const int pf = s->cfg.physics_flags | ((s->cfg.physics_flags & GPD_F_BULLET) ? GPD_F_GEOM_WRENCH : 0);
@@ -287,7 +291,7 @@ int launch_step(gpd_sim* s, const float* actions, float* obs, float* reward, uin
   const size_t lds = (size_t)s->tile_bytes;
   typedef void (*StepFn)(R*, const float*, int2*, const Consts<R>*, long long, int, int, SimView<R>, StepIO<R>);
   const StepFn f = (StepFn)step_kernel_fn<R>(s);
-  hipLaunchKernelGGL(f, dim3(grid), dim3(s->duo ? 2 * kWave : kWave), lds, st, v.state, io.actions, v.ctr, c, v.npad,
+  hipLaunchKernelGGL(f, dim3(grid), dim3(s->step_waves * kWave), lds, st, v.state, io.actions, v.ctr, c, v.npad,
                      v.N, v.tpb, v, io);
   HIP_TRY(hipGetLastError());
   return GPD_OK;
@@ -454,8 +458,7 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
       want = (int)std::min<long long>(full, Nll / 1024);
     }
     want = std::max(s->D, (want / s->D) * s->D);
-    const char* ov = std::getenv("GPD_DRONES_PER_BLOCK");
-    if (ov) want = std::max(s->D, std::min(full, (std::atoi(ov) / s->D) * s->D));
+    if (C.drones_per_block > 0) want = std::max(s->D, std::min(full, (C.drones_per_block / s->D) * s->D));
     s->tpb = want;
   }
   s->npad = ((long long)s->N + 63) / 64 * 64;
@@ -472,10 +475,9 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   {
     // write-through (sc1) stores for the obs rows (bit 0) and the state (bit 1), default both:
     // measured on one MI355X, 4096 envs 8.60 -> 8.37 us/step and 65536 envs 15.3 -> 13.7 us,
-    // large N unchanged (GPD_WT overrides).  State only while its byte offsets fit the 32-bit
-    // buffer offset.
-    const char* wt = std::getenv("GPD_WT");
-    s->wt = wt ? std::atoi(wt) : 3;
+    // large N unchanged (gpd_config::store_policy overrides).  State only while its byte
+    // offsets fit the 32-bit buffer offset.
+    s->wt = C.store_policy > 0 ? ((C.store_policy - 1) & 3) : 3;
     const size_t state_bytes = (size_t)kStateComps * s->npad * (C.precision == GPD_F64 ? 8 : 4);
     if (state_bytes >= 0x7fffffffULL) s->wt &= ~2;
   }
@@ -495,18 +497,19 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     // (scripts/geom_probe.py): 4096 envs 6.28 -> 5.71 us/step, 16384 envs 7.48 -> 6.49,
     // 65536 envs 10.45 -> 10.31, but 262144 envs 35.8 -> 38.1 (bandwidth-bound: the second
     // wave only adds occupancy pressure).  Its 128-lane copy-out needs t / NC for t <= 128.
-    // GPD_DUO=0/1 overrides.
-    bool duo = s->D == 1 && C.physics_flags == 0 &&
-               (C.act_type == GPD_ACT_RPM || C.act_type == GPD_ACT_ONE_D_RPM) && s->N <= 65536;
-    const char* ov = std::getenv("GPD_DUO");
-    if (ov) duo = std::atoi(ov) != 0 && s->D == 1 && C.physics_flags == 0 &&
-                  (C.act_type == GPD_ACT_RPM || C.act_type == GPD_ACT_ONE_D_RPM);
-    for (int t = 0; t <= 2 * kWave && duo; ++t)
-      if ((t * s->nc_magic) >> 16 != t / NC) duo = false;
-    s->duo = duo;
-    // the two-wave kernel stores its state plainly (measured 4096 envs 5.47 -> 5.37 us/step);
+    // A third (io) wave takes the history columns off the critical path (step_waves = 3).
+    // gpd_config::step_waves overrides (1, 2 or 3).
+    const bool duo_ok = s->D == 1 && C.physics_flags == 0 &&
+                        (C.act_type == GPD_ACT_RPM || C.act_type == GPD_ACT_ONE_D_RPM);
+    int waves = duo_ok && s->N <= 65536 ? 3 : 1;
+    if (C.step_waves > 0) waves = duo_ok ? std::min(3, C.step_waves) : 1;
+    for (int t = 0; t <= 2 * kWave && waves == 2; ++t)
+      if ((t * s->nc_magic) >> 16 != t / NC) waves = 1;
+    s->step_waves = waves;
+    s->duo = waves >= 2;
+    // the multi-wave kernels store their state plainly (measured 4096 envs 5.47 -> 5.37 us/step);
     // the single-wave kernel keeps write-through state stores (262144 envs 36.7 -> 35.9 us)
-    if (duo && !std::getenv("GPD_WT")) s->wt &= ~2;
+    if (s->duo && C.store_policy <= 0) s->wt &= ~2;
   }
   if (s->tile_bytes > 160 * 1024) {
     delete s;
@@ -534,7 +537,7 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   K.act_width = s->A;
   K.n_drones = s->N;
   K.drones_per_block = s->tpb;
-  K.lanes_per_block = s->duo ? 2 * kWave : kWave;
+  K.lanes_per_block = s->step_waves * kWave;
   {  // truncated iff step_counter / PYB_FREQ > EPISODE_LEN_SEC  (HoverAviary.py:114)
     long long sc = (long long)std::floor(C.episode_len_sec * C.pyb_freq);
     if (sc < 0) sc = 0;

@@ -602,8 +602,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
 // + tile); both waves stream the tile copy-out.  (Moving the final Euler angles to wave 1 as
 // well measured slower: 5.56 -> 5.89 us at 4096 envs.)  Same operations as step_kernel<R, ACT, false, true>; results agree to
 // rounding (tests/test_gpu_parity.py::test_duo_kernel_matches_single_wave).
-template <typename R, int ACT>
-__global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ state_p,
+// IO = true adds a third wave ("io wave") that writes the action-history columns of the
+// observation rows (83 % of a row's bytes, independent of the physics: ring slots head+1.. and
+// the current action) WHILE the pose / rate waves integrate, and appends the action to the
+// ring.  The pose wave then stores only the 12 state columns of its rows straight from
+// registers, so the LDS observation tile and its copy-out leave the critical path.
+template <typename R, int ACT, bool IO>
+__global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R* __restrict__ state_p,
                                                              const float* __restrict__ actions_p,
                                                              int2* __restrict__ ctr_p, const Consts<R>* __restrict__ cp,
                                                              long long npad_p, int n_p, int tpb_p, SimView<R> v,
@@ -621,12 +626,87 @@ __global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ sta
   GPD_STAMP(0);
   const Consts<R>& c = *cp;
   const int tid = threadIdx.x & (kWave - 1);
-  const bool rate_wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >= kWave;   // wave-uniform
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x) / kWave;   // wave-uniform
+  const bool rate_wave = wave == 1;
   const long long n0 = (long long)blockIdx.x * v.tpb;
   const long long n = n0 + tid;
   const int nact = (int)((v.N - n0) < v.tpb ? (v.N - n0) : v.tpb);
   const bool active = tid < nact;
   const long long nn = active ? n : 0;   // inactive lanes compute on drone 0 and store nothing
+
+  if (IO && wave == 2) {
+    // ------------------------------------------------------------ wave 2: history columns
+    // Element g of the block's nact*L history elements (L = ring_len; a float4 per element for
+    // RPM, a float for ONE_D_RPM) is row i = g / L, history column k = g % L: ring slot
+    // head+1+k (oldest first, BaseRLAviary.py:307-319) for k < L-1, the current action for
+    // k = L-1.  LDS-DMA gathers them into tile[g] (issued behind the first hand-off, so the
+    // burst stays out of the state loads' way); after the second-to-last hand-off the wave
+    // streams them to the rows' history columns (coalesced: consecutive lanes, consecutive
+    // columns) and appends the action to the ring.  The element tile stays for the terminal
+    // rows of envs that finish, known after the final barrier.
+    const int L = v.ring_len;
+    const int total = nact * L;
+    const int nsub = c.nsub;
+    const int hd = active ? v.ctr[n].y : 0;      // ring head of drone tid
+    lds_barrier();                                // hand-off 0
+    for (int g0 = 0; g0 < total; g0 += kWave) {
+      const int g = g0 + tid;
+      const int i = g / L, k = g - i * L;
+      const int hi = __shfl(hd, i < kWave ? i : 0);
+      if (g < total) {
+        const long long ni = n0 + i;
+        int slot = hi + 1 + k;
+        slot -= slot >= L ? L : 0;
+        const float* src = k == L - 1 ? io.actions + ni * A : v.ring + ridx(ni, slot, L, A);
+        if (A == 4) __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tile4 + g0), 16, 0, 0);
+        else __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tilef + g0), 4, 0, 0);
+      }
+    }
+    for (int k = 1; k < nsub; ++k) {
+      lds_barrier();                              // hand-off k
+    }
+    // the loads have had the substeps to land; the pose wave's last substep and its epilogue
+    // follow, so the stores below run beside them (the DMA wrote this wave's own tile region:
+    // its data is readable once this wave's vmcnt drains)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int NC = A == 4 ? 3 + L : v.W;          // row stride in elements
+    const int c0 = A == 4 ? 3 : 12;               // first history column
+    const bool wt = v.wt & 1;
+    float* const dst0 = io.obs + n0 * v.W;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(dst0, 0, nact * v.W * 4, 0x00020000);
+    for (int g = tid; g < total; g += kWave) {
+      const int i = g / L, k = g - i * L;
+      const int e = i * NC + c0 + k;
+      if (A == 4) {
+        const float4 val = tile4[g];
+        if (wt) store_wt(rsrc, e * 16, val);
+        else reinterpret_cast<float4*>(dst0)[e] = val;
+      } else {
+        const float val = tilef[g];
+        if (wt) store_wt(rsrc, e * 4, val);
+        else dst0[e] = val;
+      }
+    }
+    if (active) {      // deque.append of the current action; the DMA never read slot `head`
+      float* ring_cur = v.ring + ridx(n, hd, L, A);
+      if (A == 4) *reinterpret_cast<float4*>(ring_cur) = tile4[tid * L + L - 1];
+      else ring_cur[0] = tilef[tid * L + L - 1];
+    }
+    lds_barrier();     // final: sdone published by the pose wave
+    const unsigned long long dr = sdone;
+    if (dr) {
+      float* const tdst = io.terminal_obs + n0 * v.W;
+      for (int g = tid; g < total; g += kWave) {
+        const int i = g / L, k = g - i * L;
+        if ((dr >> i) & 1ull) {
+          const int e = i * NC + c0 + k;
+          if (A == 4) reinterpret_cast<float4*>(tdst)[e] = tile4[g];
+          else tdst[e] = tilef[g];
+        }
+      }
+    }
+    return;
+  }
 
   float a[A];
   if (A == 4) {
@@ -658,6 +738,10 @@ __global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ sta
       for (int j = 0; j < 5; ++j) shand[k & 1][j][tid] = h[j];
       if (k == nsub - 1) { sw[0][tid] = wx; sw[1][tid] = wy; sw[2][tid] = wz; }
       lds_barrier();   // hand-off k published
+    }
+    if (IO) {          // the io wave owns the history columns and the ring append
+      lds_barrier();   // final
+      return;
     }
     // history ring -> obs tile (LDS-DMA): issued once the last hand-off is out, it lands while
     // the pose wave finishes its last substep, the final readback and the task hooks.  The
@@ -810,20 +894,46 @@ __global__ __launch_bounds__(2 * kWave) void step_kernel_duo(R* __restrict__ sta
     for (int k = 6; k < 12; ++k) row12[k] = 0.0f;
   }
   const unsigned long long done_rows = __ballot(do_reset && active && io.terminal_obs != nullptr);
-  if (A == 4) {
-    tile4[0 * kPad + tid] = make_float4(row12[0], row12[1], row12[2], row12[3]);
-    tile4[1 * kPad + tid] = make_float4(row12[4], row12[5], row12[6], row12[7]);
-    tile4[2 * kPad + tid] = make_float4(row12[8], row12[9], row12[10], row12[11]);
-  } else {
+  if (IO) {
+    // the row's 12 state columns straight from registers; the io wave writes the rest
+    if (active) {
+      if (A == 4) {
+        const float4 r0 = make_float4(row12[0], row12[1], row12[2], row12[3]);
+        const float4 r1 = make_float4(row12[4], row12[5], row12[6], row12[7]);
+        const float4 r2 = make_float4(row12[8], row12[9], row12[10], row12[11]);
+        if (v.wt & 1) {
+          const __amdgpu_buffer_rsrc_t r =
+              __builtin_amdgcn_make_buffer_rsrc(io.obs + n0 * v.W, 0, nact * v.W * 4, 0x00020000);
+          const int o = tid * v.W * 4;
+          store_wt(r, o, r0); store_wt(r, o + 16, r1); store_wt(r, o + 32, r2);
+        } else {
+          float4* o4 = reinterpret_cast<float4*>(io.obs + n * v.W);
+          o4[0] = r0; o4[1] = r1; o4[2] = r2;
+        }
+      } else {
+        float* orow = io.obs + n * v.W;
 #pragma unroll
-    for (int k = 0; k < 12; ++k) tilef[k * kPad + tid] = row12[k];
+        for (int k = 0; k < 12; ++k) orow[k] = row12[k];
+      }
+    }
+    if (tid == 0) sdone = done_rows;
+    lds_barrier();   // final: sdone published (the io wave writes the terminal rows' history)
+  } else {
+    if (A == 4) {
+      tile4[0 * kPad + tid] = make_float4(row12[0], row12[1], row12[2], row12[3]);
+      tile4[1 * kPad + tid] = make_float4(row12[4], row12[5], row12[6], row12[7]);
+      tile4[2 * kPad + tid] = make_float4(row12[8], row12[9], row12[10], row12[11]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) tilef[k * kPad + tid] = row12[k];
+    }
+    if (tid == 0) sdone = done_rows;
+    GPD_STAMP(5);
+    lds_barrier();     // tile complete, sdone published
+    GPD_STAMP(6);
+    tile_copy_out<A, 2 * kWave, 3>(tile4, tilef, threadIdx.x, nact, NC, v.nc_magic, v.wt, done_rows, io.obs,
+                                io.terminal_obs, n0);
   }
-  if (tid == 0) sdone = done_rows;
-  GPD_STAMP(5);
-  lds_barrier();     // tile complete, sdone published
-  GPD_STAMP(6);
-  tile_copy_out<A, 2 * kWave, 3>(tile4, tilef, threadIdx.x, nact, NC, v.nc_magic, v.wt, done_rows, io.obs,
-                              io.terminal_obs, n0);
   GPD_STAMP(7);
   GPD_RSTAMP(12);
   if (!active) return;

@@ -100,7 +100,7 @@ class BatchedAviarySim:
     def __init__(self, n_envs, drones_per_env=1, drone_model=DroneModel.CF2X, urdf_path=None,
                  pyb_freq=240, ctrl_freq=30, act=ActionType.RPM, task="hover",
                  physics=Physics.DYN, aero=(), precision="f64", autoreset=True, episode_len_sec=8,
-                 initial_xyzs=None, initial_rpys=None, device=None):
+                 initial_xyzs=None, initial_rpys=None, device=None, tuning=None):
         self._lib = _lib.load()
         if not torch.cuda.is_available():
             raise _lib.GpdLibraryError("BatchedAviarySim needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -127,6 +127,11 @@ class BatchedAviarySim:
         cfg.precision = _lib.GPD_F32 if precision == "f32" else _lib.GPD_F64
         cfg.autoreset = 1 if autoreset else 0
         cfg.episode_len_sec = float(episode_len_sec)
+        # launch tuning (gpd_config: drones_per_block, step_waves, store_policy; 0 = automatic)
+        for name, val in (tuning or {}).items():
+            if name not in ("drones_per_block", "step_waves", "store_policy"):
+                raise ValueError(f"unknown tuning field {name!r}")
+            setattr(cfg, name, int(val))
         keep = []
         for name, arr in (("init_xyzs_host", initial_xyzs), ("init_rpys_host", initial_rpys)):
             if arr is not None:

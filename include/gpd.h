@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define GPD_ABI_VERSION 3
+#define GPD_ABI_VERSION 4
 
 /* return codes */
 #define GPD_OK 0
@@ -115,6 +115,13 @@ typedef struct gpd_config {
   double episode_len_sec;    /* EPISODE_LEN_SEC (8 for both tasks) */
   const double* init_xyzs_host; /* [D][3] INIT_XYZS shared by all envs, NULL = default (:194-197) */
   const double* init_rpys_host; /* [D][3] INIT_RPYS, NULL = zeros */
+  /* Launch tuning: 0 = automatic (the measured defaults).  Explicit values exist for A/B
+   * experiments and tests; they change launch geometry and store policy, never results
+   * beyond the rounding noted in DESIGN.md section 4. */
+  int drones_per_block;      /* drones per step block (rounded to whole envs, <= 64) */
+  int step_waves;            /* plain-DYN single-drone RPM path: 1 single-wave kernel,
+                              * 2 pose+rate waves, 3 pose+rate+io waves */
+  int store_policy;          /* 1 + write-through mask: bit 0 obs/terminal rows, bit 1 state */
 } gpd_config;
 
 /* Derived constants, BaseAviary.py:117-128 (read-only view for tests/facades). */
@@ -124,7 +131,7 @@ typedef struct gpd_constants {
   int pyb_steps_per_ctrl, action_buffer_size, obs_width, act_width, n_drones;
   int trunc_step_counter;    /* smallest step_counter with step_counter/PYB_FREQ > EPISODE_LEN_SEC */
   int drones_per_block;      /* drones per block of the step kernel (launch geometry) */
-  int lanes_per_block;       /* step kernel block size: 64, or 128 for the two-wave kernel */
+  int lanes_per_block;       /* step kernel block size: 64, 128 (two waves) or 192 (three) */
 } gpd_constants;
 
 /* DSLPIDControl coefficients and constants (control/DSLPIDControl.py:37-60; GRAVITY and KF

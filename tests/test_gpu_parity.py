@@ -143,14 +143,17 @@ def test_downwash_multi_parity(prec):
     sim.close()
 
 
-@pytest.mark.parametrize("kernel", ["duo", "single"])
+WAVES = {"io": 3, "duo": 2, "single": 1}
+
+
+@pytest.mark.parametrize("kernel", ["io", "duo", "single"])
 @pytest.mark.parametrize("prec", ["f64", "f32"])
 @pytest.mark.parametrize("act", ["rpm", "one_d_rpm"])
-def test_step_parity_hover(prec, act, kernel, monkeypatch):
+def test_step_parity_hover(prec, act, kernel):
     """HoverAviary step(): obs / reward / terminated / truncated with SB3 auto-reset, through the
-    two-wave step kernel (the default up to 64K drones) and the single-wave one (larger N)."""
+    three-wave step kernel (pose + rate + io waves, the default up to 64K drones), the two-wave
+    one and the single-wave one (larger N)."""
     from gym_pybullet_drones_routing_amd.enums import ActionType
-    monkeypatch.setenv("GPD_DUO", "1" if kernel == "duo" else "0")
     rng = np.random.default_rng(4)
     E, T = 16, 80
     A = 4 if act == "rpm" else 1
@@ -160,8 +163,8 @@ def test_step_parity_hover(prec, act, kernel, monkeypatch):
     if A == 1:
         acts[:, 4:6] = 1.0   # full collective thrust: climbs through z > 2 -> truncation + reset
     obs_r, rew_r, te_r, tr_r, tobs_r = run_vec(acts, E, act=act)
-    sim = _sim(n_envs=E, task="hover", precision=prec, act=ActionType(act))
-    assert sim.constants.lanes_per_block == (128 if kernel == "duo" else 64)
+    sim = _sim(n_envs=E, task="hover", precision=prec, act=ActionType(act), tuning={"step_waves": WAVES[kernel]})
+    assert sim.constants.lanes_per_block == 64 * WAVES[kernel]
     obs0 = sim.obs.cpu().numpy()
     assert obs0.shape == (E, 1, 12 + 15 * A)
     n_done = 0
@@ -186,14 +189,16 @@ def test_step_parity_hover(prec, act, kernel, monkeypatch):
     sim.close()
 
 
+@pytest.mark.parametrize("dpb", [0, 4, 8, 64])
 @pytest.mark.parametrize("prec", ["f64", "f32"])
 @pytest.mark.parametrize("act", ["rpm", "one_d_rpm"])
-def test_duo_kernel_matches_single_wave(prec, act, monkeypatch):
+def test_duo_kernel_matches_single_wave(prec, act, dpb):
     """The two-wave step kernel runs dyn_substep's operations split over two waves: the same
     obs, reward, done flags and state as the single-wave kernel up to rounding (hipcc contracts
-    a few multiply-adds differently in the two code shapes: measured 1 ulp in f64).  Ragged env
-    count (the last block is partial), full-range actions (resets, tumbling drones past the
-    small-angle series), 60 steps."""
+    a few multiply-adds differently in the two code shapes: measured 1 ulp in f64); the
+    three-wave kernel (io wave for the history columns) is bit-identical to the two-wave one.
+    Ragged env count (the last block is partial), full-range actions (resets, tumbling drones
+    past the small-angle series), 60 steps, automatic and pinned block sizes."""
     from gym_pybullet_drones_routing_amd.enums import ActionType
     rng = np.random.default_rng(21)
     E, T = 100, 60
@@ -201,10 +206,11 @@ def test_duo_kernel_matches_single_wave(prec, act, monkeypatch):
     acts = rng.uniform(-1, 1, (T, E, 1, A)).astype(np.float32)
     acts[:, :50] *= np.float32(0.1)
     out = {}
-    for kernel in ("duo", "single"):
-        monkeypatch.setenv("GPD_DUO", "1" if kernel == "duo" else "0")
-        sim = _sim(n_envs=E, task="hover", precision=prec, act=ActionType(act))
-        assert sim.constants.lanes_per_block == (128 if kernel == "duo" else 64)
+    for kernel in ("io", "duo", "single"):
+        sim = _sim(n_envs=E, task="hover", precision=prec, act=ActionType(act),
+                   tuning={"step_waves": WAVES[kernel], "drones_per_block": dpb})
+        assert sim.constants.lanes_per_block == 64 * WAVES[kernel]
+        assert dpb == 0 or sim.constants.drones_per_block == dpb
         rec = []
         for t in range(T):
             o, r, te, tr = sim.step(torch.from_numpy(acts[t]).cuda())
@@ -212,7 +218,12 @@ def test_duo_kernel_matches_single_wave(prec, act, monkeypatch):
                         tr.cpu().numpy().copy(), sim.terminal_obs.cpu().numpy().copy()))
         out[kernel] = (rec, sim.state20().cpu().numpy())
         sim.close()
-    (ra, sa), (rb, sb) = out["duo"], out["single"]
+    # the io and two-wave kernels run the same pose/rate code: bit-identical
+    (ri, si), (ra, sa), (rb, sb) = out["io"], out["duo"], out["single"]
+    for t in range(T):
+        for x, y in zip(ri[t], ra[t]):
+            np.testing.assert_array_equal(x, y, err_msg=f"io vs duo, step {t}")
+    np.testing.assert_array_equal(si, sa)
     tol = 1e-12 if prec == "f64" else 1e-4
     for t in range(T):
         (oa, rwa, tea, tra, ta), (ob, rwb, teb, trb, tb) = ra[t], rb[t]

@@ -39,7 +39,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 def test_host_only_entry_points(lib):
     from gym_pybullet_drones_routing_amd import _lib
-    assert lib.gpd_abi_version() == _lib.GPD_ABI_VERSION == 3
+    assert lib.gpd_abi_version() == _lib.GPD_ABI_VERSION == 4
     q = _lib.PidParams()
     assert lib.gpd_default_pid_params(ctypes.byref(q)) == _lib.GPD_OK
     assert list(q.p_coeff_tor) == [70000., 70000., 60000.] and q.pwm2rpm_const == 4070.3
@@ -58,11 +58,32 @@ def test_host_only_entry_points(lib):
 def test_struct_sizes_match_header():
     """ctypes mirrors of gpd_drone_params / gpd_config / gpd_constants have the C layout."""
     from gym_pybullet_drones_routing_amd import _lib
-    # int + 19 doubles (8-aligned after the int) + 12 doubles
-    assert ctypes.sizeof(_lib.DroneParams) == 8 + 19 * 8 + 12 * 8
-    assert ctypes.sizeof(_lib.Config) == 9 * 4 + 4 + 8 + 8 + 8
-    assert ctypes.sizeof(_lib.Constants) == 9 * 8 + 7 * 4 + 4   # 7 ints + tail padding to 8
-    assert ctypes.sizeof(_lib.PidParams) == (6 * 3 + 4 + 12 + 2) * 8
+    # the C compiler's view of include/gpd.h (sizes and a few field offsets)
+    import subprocess
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = r"""
+#include <stdio.h>
+#include <stddef.h>
+typedef void* hipStream_t;
+#include "gpd.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(gpd_drone_params), sizeof(gpd_config), sizeof(gpd_constants),
+         sizeof(gpd_pid_params), offsetof(gpd_config, episode_len_sec), offsetof(gpd_config, drones_per_block),
+         offsetof(gpd_config, store_policy));
+  return 0;
+}
+"""
+    with tempfile.TemporaryDirectory() as d:
+        open(os.path.join(d, "t.c"), "w").write(src)
+        subprocess.run(["gcc", "-I", os.path.join(root, "include"), "-o", os.path.join(d, "t"), os.path.join(d, "t.c")],
+                       check=True)
+        got = [int(x) for x in subprocess.run([os.path.join(d, "t")], capture_output=True, text=True,
+                                              check=True).stdout.split()]
+    assert got[:4] == [ctypes.sizeof(_lib.DroneParams), ctypes.sizeof(_lib.Config), ctypes.sizeof(_lib.Constants),
+                       ctypes.sizeof(_lib.PidParams)]
+    assert got[4:] == [_lib.Config.episode_len_sec.offset, _lib.Config.drones_per_block.offset,
+                       _lib.Config.store_policy.offset]
 
 
 def test_abi_version_consistent():
