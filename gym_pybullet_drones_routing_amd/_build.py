@@ -29,12 +29,15 @@ def needs_build():
     return any(src.stat().st_mtime > t for src in SOURCES)
 
 
-def build(force=False, verbose=False, stamps=False):
+def build(force=False, verbose=False, stamps=False, variant=None, defines=()):
     """Compile csrc/gpd.hip into libgpd.so for gfx950 (code object v5, loadable by the
     HIP runtime that ships inside the torch wheel).  stamps=True builds the diagnostic
-    libgpd_stamps.so (phase timestamps, never loaded unless GPD_LIB points at it)."""
+    libgpd_stamps.so (phase timestamps, never loaded unless GPD_LIB points at it);
+    variant="x" with -D `defines` builds libgpd_x.so for A/B experiments (scripts/ab_geom.sh)."""
     out = PKG_DIR / "libgpd_stamps.so" if stamps else LIB_PATH
-    if not force and not stamps and not needs_build():
+    if variant:
+        out = PKG_DIR / f"libgpd_{variant}.so"
+    if not force and not stamps and not variant and not needs_build():
         return LIB_PATH
     tmp = out.with_suffix(".so.tmp")
     # kernarg preloading: the step kernel's leading scalar arguments arrive in SGPRs.
@@ -43,7 +46,7 @@ def build(force=False, verbose=False, stamps=False):
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-mcode-object-version=5", "-O3", "-std=c++17",
            "-mllvm", "-amdgpu-kernarg-preload-count=12", "-mllvm", "-amdgpu-sched-strategy=max-ilp",
            "-fPIC", "-shared", "-Wall", "-Wno-unused-result", f"-I{INCLUDE}", "-o", str(tmp),
-           str(CSRC / "gpd.hip")] + (["-DGPD_STAMPS"] if stamps else [])
+           str(CSRC / "gpd.hip")] + (["-DGPD_STAMPS"] if stamps else []) + [f"-D{d}" for d in defines]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError("hipcc failed:\n" + " ".join(cmd) + "\n" + res.stdout + res.stderr)

@@ -497,11 +497,13 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     // (scripts/geom_probe.py): 4096 envs 6.28 -> 5.71 us/step, 16384 envs 7.48 -> 6.49,
     // 65536 envs 10.45 -> 10.31, but 262144 envs 35.8 -> 38.1 (bandwidth-bound: the second
     // wave only adds occupancy pressure).  Its 128-lane copy-out needs t / NC for t <= 128.
-    // A third (io) wave takes the history columns off the critical path (step_waves = 3).
+    // A third (io) wave takes the history columns off the pose wave (step_waves = 3): measured
+    // (scripts/ab_geom.sh, profiles/r2) 4096 envs 5.42 -> 5.32 us/step, but slower from 16384
+    // envs on (6.24 -> 7.04), where the blocks are full and the copy-out overlaps anyway.
     // gpd_config::step_waves overrides (1, 2 or 3).
     const bool duo_ok = s->D == 1 && C.physics_flags == 0 &&
                         (C.act_type == GPD_ACT_RPM || C.act_type == GPD_ACT_ONE_D_RPM);
-    int waves = duo_ok && s->N <= 65536 ? 3 : 1;
+    int waves = !duo_ok || s->N > 65536 ? 1 : (s->N <= 8192 ? 3 : 2);
     if (C.step_waves > 0) waves = duo_ok ? std::min(3, C.step_waves) : 1;
     for (int t = 0; t <= 2 * kWave && waves == 2; ++t)
       if ((t * s->nc_magic) >> 16 != t / NC) waves = 1;

@@ -53,7 +53,9 @@ enum : int { TASK_NONE = 0, TASK_HOVER = 1, TASK_MULTIHOVER = 2 };
 // shader clock at phase boundaries of step_kernel into g_stamps[block][phase].  The shipped
 // library executes no stamp.
 #ifdef GPD_STAMPS
-constexpr int kStampPhases = 14;   // 0..10 shader clocks; 11 / 12: s_memrealtime (100 MHz) at entry / end
+constexpr int kStampPhases = 24;   // 0..10 shader clocks; 11 / 12: s_memrealtime (100 MHz) at entry / end;
+                                   // 13: rate / io wave end (realtime); 14..16: HW_ID of waves 0..2;
+                                   // 17..23: io wave phases (shader clocks)
 __device__ unsigned long long g_stamps[65536 * kStampPhases];
 #define GPD_STAMP(k)                                                                      \
   do {                                                                                    \
@@ -71,7 +73,15 @@ __device__ unsigned long long g_stamps[65536 * kStampPhases];
     if (threadIdx.x == 0 && blockIdx.x < 65536) g_stamps[blockIdx.x * kStampPhases + (k)] = t_; \
     __builtin_amdgcn_sched_barrier(0);                                                    \
   } while (0)
+#define GPD_IOSTAMP(k)                                                                    \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                           \
+    if (tid == 0 && blockIdx.x < 65536) g_stamps[blockIdx.x * kStampPhases + 17 + (k)] = t_; \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+  } while (0)
 #else
+#define GPD_IOSTAMP(k) do {} while (0)
 #define GPD_STAMP(k) do {} while (0)
 #define GPD_RSTAMP(k) do {} while (0)
 #endif
@@ -633,78 +643,124 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
   const int nact = (int)((v.N - n0) < v.tpb ? (v.N - n0) : v.tpb);
   const bool active = tid < nact;
   const long long nn = active ? n : 0;   // inactive lanes compute on drone 0 and store nothing
+#ifdef GPD_STAMPS
+  {   // diagnostic: which SIMD / CU each wave of the block runs on (HW_ID: SIMD_ID bits 5:4)
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    if (tid == 0 && blockIdx.x < 65536) g_stamps[blockIdx.x * kStampPhases + 14 + wave] = hw;
+  }
+#endif
 
   if (IO && wave == 2) {
     // ------------------------------------------------------------ wave 2: history columns
-    // Element g of the block's nact*L history elements (L = ring_len; a float4 per element for
-    // RPM, a float for ONE_D_RPM) is row i = g / L, history column k = g % L: ring slot
-    // head+1+k (oldest first, BaseRLAviary.py:307-319) for k < L-1, the current action for
-    // k = L-1.  LDS-DMA gathers them into tile[g] (issued behind the first hand-off, so the
-    // burst stays out of the state loads' way); after the second-to-last hand-off the wave
-    // streams them to the rows' history columns (coalesced: consecutive lanes, consecutive
-    // columns) and appends the action to the ring.  The element tile stays for the terminal
-    // rows of envs that finish, known after the final barrier.
+    // The history columns of a row are ring slots head+1 .. head+L-1 (oldest first,
+    // BaseRLAviary.py:307-319) and the current action.  The wave appends the action to the
+    // ring and the tile, follows the pose/rate waves' hand-off barriers, then DMAs the ring
+    // slots into the tile and streams the tile, transposed (conflict-free thanks to the column
+    // pad), into the rows' history columns with coalesced stores - beside the pose wave's last
+    // substep and epilogue, which then stores only the 12 state columns.  The tile stays for
+    // the terminal rows of envs that finish, known after the final barrier.
     const int L = v.ring_len;
-    const int total = nact * L;
     const int nsub = c.nsub;
-    const int hd = active ? v.ctr[n].y : 0;      // ring head of drone tid
-    lds_barrier();                                // hand-off 0
-    for (int g0 = 0; g0 < total; g0 += kWave) {
-      const int g = g0 + tid;
-      const int i = g / L, k = g - i * L;
-      const int hi = __shfl(hd, i < kWave ? i : 0);
-      if (g < total) {
-        const long long ni = n0 + i;
-        int slot = hi + 1 + k;
-        slot -= slot >= L ? L : 0;
-        const float* src = k == L - 1 ? io.actions + ni * A : v.ring + ridx(ni, slot, L, A);
-        if (A == 4) __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tile4 + g0), 16, 0, 0);
-        else __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tilef + g0), 4, 0, 0);
+    const int2 cv = v.ctr[nn];
+    const int hd = cv.y;                          // ring slot receiving this step's action
+    float a[A];
+    if (A == 4) {
+      const float4 a4 = *reinterpret_cast<const float4*>(io.actions + nn * 4);
+      a[0] = a4.x; a[1] = a4.y; a[2] = a4.z; a[3] = a4.w;
+    } else {
+      a[0] = io.actions[nn];
+    }
+    // The current action goes into its tile column BEFORE the DMA is issued: a ds_write after
+    // an LDS-DMA in flight makes the compiler wait for the whole DMA (vmcnt(0)) first.
+    if (A == 4) tile4[(L - 1) * kPad + tid] = make_float4(a[0], a[1], a[2], a[3]);
+    else tilef[(L - 1) * kPad + tid] = a[0];
+    if (active) {      // deque.append of the current action; the DMA never reads slot `head`
+      float* ring_cur = v.ring + ridx(n, hd, L, A);
+      if (A == 4) *reinterpret_cast<float4*>(ring_cur) = make_float4(a[0], a[1], a[2], a[3]);
+      else ring_cur[0] = a[0];
+    }
+    // This wave publishes nothing to the others, so its barriers skip lds_barrier's
+    // lgkmcnt(0) wait: an LDS-DMA in flight holds that counter until it lands.
+    GPD_IOSTAMP(0);
+    asm volatile("s_barrier" ::: "memory");       // hand-off 0
+    GPD_IOSTAMP(1);
+    for (int k = 1; k < nsub; ++k) asm volatile("s_barrier" ::: "memory");   // hand-offs 1 .. nsub-1
+    // history ring -> tile (LDS-DMA) behind the last hand-off: an LDS-DMA in flight while the
+    // pose / rate waves still exchange hand-offs slowed their substeps by ~850 cycles per launch
+    // (phase stamps, 4096 envs), issued here it lands beside the pose wave's last substep and
+    // epilogue.  Slot head+1+m of every drone of the block -> tile column m (one coalesced
+    // 64-drone run per slot, lane-contiguous in LDS).
+    {
+      const float* rb = v.ring + ridx(nn, 0, L, A);
+      int slot = hd + 1 == L ? 0 : hd + 1;
+      for (int m = 0; m < L - 1; ++m) {
+        const float* src = rb + slot * (64 * A);
+        if (A == 4) __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tile4 + m * kPad), 16, 0, 0);
+        else __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tilef + m * kPad), 4, 0, 0);
+        slot = slot + 1 == L ? 0 : slot + 1;
       }
     }
-    for (int k = 1; k < nsub; ++k) {
-      lds_barrier();                              // hand-off k
-    }
-    // the loads have had the substeps to land; the pose wave's last substep and its epilogue
-    // follow, so the stores below run beside them (the DMA wrote this wave's own tile region:
-    // its data is readable once this wave's vmcnt drains)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    GPD_IOSTAMP(2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA has landed in its tile
+    GPD_IOSTAMP(3);
+    const int total = nact * L;
     const int NC = A == 4 ? 3 + L : v.W;          // row stride in elements
     const int c0 = A == 4 ? 3 : 12;               // first history column
-    const bool wt = v.wt & 1;
+    const float rL = 1.0f / (float)L;             // (g + 0.5) / L: exact row index for g < 2^12
     float* const dst0 = io.obs + n0 * v.W;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(dst0, 0, nact * v.W * 4, 0x00020000);
-    for (int g = tid; g < total; g += kWave) {
-      const int i = g / L, k = g - i * L;
-      const int e = i * NC + c0 + k;
-      if (A == 4) {
-        const float4 val = tile4[g];
-        if (wt) store_wt(rsrc, e * 16, val);
-        else reinterpret_cast<float4*>(dst0)[e] = val;
-      } else {
-        const float val = tilef[g];
-        if (wt) store_wt(rsrc, e * 4, val);
-        else dst0[e] = val;
+    // four elements per lane in flight per pass (LDS reads, then stores); an element past the
+    // end gets an offset past num_records, so the buffer unit drops its store
+    constexpr int U = 4;
+    for (int g0 = tid; g0 < total; g0 += U * kWave) {
+      int off[U];
+      float4 v4[U];
+      float v1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int g = g0 + u * kWave;
+        const bool ok = g < total;
+        const int gg = ok ? g : total - 1;
+        const int i = (int)(((float)gg + 0.5f) * rL), k = gg - i * L;
+        const int e = i * NC + c0 + k;
+        off[u] = ok ? e * (A == 4 ? 16 : 4) : nact * v.W * 4;
+        if (A == 4) v4[u] = tile4[__umul24(k, kPad) + i];
+        else v1[u] = tilef[__umul24(k, kPad) + i];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (v.wt & 1) {
+          if (A == 4) store_wt(rsrc, off[u], v4[u]);
+          else store_wt(rsrc, off[u], v1[u]);
+        } else {
+          if (A == 4) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gpd_v4i, v4[u]), rsrc, off[u], 0, 0);
+          else __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v1[u]), rsrc, off[u], 0, 0);
+        }
       }
     }
-    if (active) {      // deque.append of the current action; the DMA never read slot `head`
-      float* ring_cur = v.ring + ridx(n, hd, L, A);
-      if (A == 4) *reinterpret_cast<float4*>(ring_cur) = tile4[tid * L + L - 1];
-      else ring_cur[0] = tilef[tid * L + L - 1];
-    }
+    GPD_IOSTAMP(4);
     lds_barrier();     // final: sdone published by the pose wave
+    GPD_IOSTAMP(5);
     const unsigned long long dr = sdone;
     if (dr) {
       float* const tdst = io.terminal_obs + n0 * v.W;
       for (int g = tid; g < total; g += kWave) {
-        const int i = g / L, k = g - i * L;
+        const int i = (int)(((float)g + 0.5f) * rL), k = g - i * L;
         if ((dr >> i) & 1ull) {
           const int e = i * NC + c0 + k;
-          if (A == 4) reinterpret_cast<float4*>(tdst)[e] = tile4[g];
-          else tdst[e] = tilef[g];
+          if (A == 4) reinterpret_cast<float4*>(tdst)[e] = tile4[__umul24(k, kPad) + i];
+          else tdst[e] = tilef[__umul24(k, kPad) + i];
         }
       }
     }
+#ifdef GPD_STAMPS
+    {   // diagnostic: the io wave's end (realtime) into phase 13
+      __builtin_amdgcn_sched_barrier(0);
+      unsigned long long t_;
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+      if (tid == 0 && blockIdx.x < 65536) g_stamps[blockIdx.x * kStampPhases + 13] = t_;
+    }
+#endif
     return;
   }
 
@@ -896,6 +952,7 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
   const unsigned long long done_rows = __ballot(do_reset && active && io.terminal_obs != nullptr);
   if (IO) {
     // the row's 12 state columns straight from registers; the io wave writes the rest
+    GPD_STAMP(5);
     if (active) {
       if (A == 4) {
         const float4 r0 = make_float4(row12[0], row12[1], row12[2], row12[3]);
@@ -918,6 +975,9 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
     }
     if (tid == 0) sdone = done_rows;
     lds_barrier();   // final: sdone published (the io wave writes the terminal rows' history)
+    GPD_STAMP(6);
+    GPD_STAMP(8);
+    GPD_STAMP(9);
   } else {
     if (A == 4) {
       tile4[0 * kPad + tid] = make_float4(row12[0], row12[1], row12[2], row12[3]);
