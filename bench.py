@@ -287,6 +287,31 @@ def time_graph(sim, pool, steps, warmup, per_graph=256):
     return wall, steps, 1000.0 * ev0.elapsed_time(ev1) / steps
 
 
+def time_native(sim, pool, steps, warmup):
+    """Timed region as ONE gpd_step_seq call: `steps` env.step() launches issued back to back from
+    native code (step k reads action slot k % P), no graph.  Its fixed cost per timed region
+    (first launch + the closing synchronize) is about half a graph replay's (scripts/timing_probe.py),
+    which matters at small --steps.  A HIP event pair on the launch stream brackets the launches.
+    Returns (wall seconds, steps run, kernel us)."""
+    steps = max(1, int(steps))
+    sim.step_seq(pool, max(1, int(warmup)))
+    stream = torch.cuda.current_stream(sim.device)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(sim.device)
+    if torch.distributed.is_initialized():
+        torch.distributed.barrier()
+    torch.cuda.synchronize(sim.device)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    sim.step_seq(pool, steps)
+    ev1.record(stream)
+    torch.cuda.synchronize(sim.device)
+    wall = time.perf_counter() - t0
+    if torch.distributed.is_initialized():
+        torch.distributed.barrier()
+    return wall, steps, 1000.0 * ev0.elapsed_time(ev1) / steps
+
+
 def time_steps(sim, pool, steps, warmup):
     """Eager launches (one BatchedAviarySim.step() call per env.step, as an SB3-style caller
     makes them): the wall time of `steps` back-to-back calls, then a second pass with a HIP event
@@ -408,7 +433,9 @@ def parse_args(argv=None):
                     help="processes of the all-core CPU baseline (0 = the CPUs this job may use)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
-    ap.add_argument("--eager", action="store_true", help="time eager launches instead of hipGraph replays")
+    ap.add_argument("--mode", default="native", choices=["native", "graph", "eager"],
+                    help="timed region: native launch loop (gpd_step_seq, default), hipGraph replays, or "
+                         "one Python step() call per env.step")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the real multi-GPU path); gloo only to rehearse several ranks on one GPU")
     return ap.parse_args(argv)
@@ -491,10 +518,15 @@ def run(args):
     eager_wall, eager_kern_us = time_steps(sim, pool, args.steps, args.warmup)
     # (2) timed pass: the same steps replayed from a hipGraph (no host launch overhead); the
     #     roofline's kernel duration comes from the events around these replays
-    if args.eager:
+    if args.mode == "eager":
         wall, steps_run, kern_us = eager_wall, args.steps, eager_kern_us
-    else:
+    elif args.mode == "graph":
         wall, steps_run, kern_us = time_graph(sim, pool, args.steps, args.warmup)
+    else:
+        wall, steps_run, kern_us = time_native(sim, pool, args.steps, args.warmup)
+        g_wall, g_steps, g_kern = time_graph(sim, pool, args.steps, args.warmup)
+        graph_leg = {"ms_per_step": 1000.0 * g_wall / g_steps, "value": E * nsub * g_steps / g_wall,
+                     "kernel_us_per_launch_events": g_kern}
     wall = max_over_ranks(wall, device)
     eager_wall = max_over_ranks(eager_wall, device)
     drone_dt = world * E * nsub * steps_run
@@ -508,7 +540,9 @@ def run(args):
         "value": value, "unit": "drone*dt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f32" if args.precision == "f32" else "f64", "data": "synthetic",
-        "mode": "eager launches" if args.eager else "hipGraph replay, 16 env.step launches per graph (+ one graph of the remainder)",
+        "mode": {"eager": "one Python BatchedAviarySim.step() call per env.step",
+                 "graph": "hipGraph replay, up to 256 env.step launches per graph (+ one graph of the remainder)",
+                 "native": "one gpd_step_seq call: K env.step launches back to back from native code"}[args.mode],
         "config": {"workload": f"{E} HoverAviary envs per GPU (cf2x, Physics.DYN, ActionType.{args.act.upper()}, "
                                f"240/30 Hz = {nsub} substeps/step, U[-1,1] actions, SB3 auto-reset)",
                    "n_envs_per_gpu": E, "global_envs": E * world, "drones_per_env": 1,
@@ -518,6 +552,7 @@ def run(args):
                   "value": world * E * nsub * args.steps / eager_wall,
                   "kernel_us_per_launch_events": eager_kern_us},
         "ctrl_steps_per_s": world * E * args.steps / wall,
+        "graph": graph_leg if args.mode == "native" else None,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "traffic_unit": "bytes per launch",
                      "kernel": step_kernel_name(sim, rbytes, args.act),

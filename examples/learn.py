@@ -13,6 +13,7 @@ masks as device tensors, so the whole loop (policy, env step, GAE, update) stays
     python examples/learn.py                     # HoverAviary, 4096 envs, ONE_D_RPM, Physics.PYB
     python examples/learn.py --multiagent true   # MultiHoverAviary, 2 drones
     python examples/learn.py --physics dyn       # the explicit DYN integrator instead
+    python examples/learn.py --gpus 8 --n_envs 32768   # envs sharded over 8 GPUs, learner on rank 0
 
 Physics defaults to the env classes' default, Physics.PYB (the reference's learn.py does not
 pass one), i.e. the restated Bullet multibody step.
@@ -85,17 +86,25 @@ def evaluate(policy, multiagent, device, act, physics=Physics.PYB):
     return ret, steps
 
 
+def make_env(multiagent, n_envs, act, physics, device, seed=0, distributed=False):
+    env_cls = MultiHoverAviary if multiagent else HoverAviary
+    kw = dict(obs=DEFAULT_OBS, act=act, physics=Physics(physics))
+    if multiagent:
+        kw["num_drones"] = DEFAULT_AGENTS
+    return make_vec_env(env_cls, env_kwargs=kw, n_envs=n_envs, seed=seed, output="torch", device=device,
+                        distributed=distributed)
+
+
 def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), lr=3e-4, epochs=10,
           minibatch=16384, gamma=0.99, gae_lambda=0.95, clip=0.2, vf_coef=0.5, max_grad_norm=0.5,
           eval_every=2, seed=0, device="cuda:0", act=DEFAULT_ACT, target_reward=None, max_seconds=None,
-          log=print, physics=Physics.PYB):
+          log=print, physics=Physics.PYB, env=None):
+    """PPO on the batched env.  ``env``: an already built torch-output VecEnv (e.g. the
+    multi-GPU ``ShardedAviaryVecEnv``); by default one ``AviaryVecEnv`` on ``device``."""
     torch.manual_seed(seed)
-    env_cls = MultiHoverAviary if multiagent else HoverAviary
     physics = Physics(physics)
-    kw = dict(obs=DEFAULT_OBS, act=act, physics=physics)
-    if multiagent:
-        kw["num_drones"] = DEFAULT_AGENTS
-    env = make_vec_env(env_cls, env_kwargs=kw, n_envs=n_envs, seed=seed, output="torch", device=device)
+    if env is None:
+        env = make_env(multiagent, n_envs, act, physics, device, seed)
     if target_reward is None:   # learn.py:80-83
         if act == ActionType.ONE_D_RPM:
             target_reward = 474.15 if not multiagent else 949.5
@@ -185,24 +194,86 @@ def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), l
     return policy, history, best, target_reward
 
 
-def main():
+def parse_args(argv=None):
     p = argparse.ArgumentParser(description="PPO on batched HoverAviary / MultiHoverAviary (MI355X)")
     p.add_argument("--multiagent", default="false")
-    p.add_argument("--n_envs", type=int, default=4096)
+    p.add_argument("--n_envs", type=int, default=4096, help="envs over all GPUs")
     p.add_argument("--total_timesteps", type=float, default=2e8)
     p.add_argument("--max_seconds", type=float, default=None)
     p.add_argument("--physics", default="pyb", help="Physics value (default: pyb, the env classes' default)")
     p.add_argument("--output", default=None, help="JSON file for the training history")
-    a = p.parse_args()
+    p.add_argument("--gpus", type=int, default=1,
+                   help="GPUs: the envs are sharded over one rank per GPU, the learner runs on rank 0 "
+                        "(without WORLD_SIZE in the env, learn.py starts the ranks itself)")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="nccl (= RCCL over xGMI); gloo only to rehearse several ranks on one GPU")
+    return p.parse_args(argv)
+
+
+def run(a):
+    """One rank: shard of the envs; rank 0 also runs PPO on the gathered batch."""
+    import torch.distributed as dist
     multi = str(a.multiagent).lower() in ("1", "true", "yes")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev_index = local % torch.cuda.device_count() if a.dist_backend == "gloo" else local
+    device = torch.device(f"cuda:{dev_index}")
+    torch.cuda.set_device(device)
+    env = None
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
+        env = make_env(multi, a.n_envs, DEFAULT_ACT, Physics(a.physics), device, distributed=True)
+        if rank != 0:
+            env.serve()
+            dist.destroy_process_group()
+            return
     policy, hist, best, target = train(multiagent=multi, n_envs=a.n_envs, total_timesteps=int(a.total_timesteps),
-                                       max_seconds=a.max_seconds, physics=Physics(a.physics))
-    out = {"multiagent": multi, "physics": a.physics, "n_envs": a.n_envs, "target_reward": target, "best_eval_return": best,
-           "reached": best >= target, "history": hist}
-    print(json.dumps({k: v for k, v in out.items() if k != "history"}))
+                                       max_seconds=a.max_seconds, physics=Physics(a.physics), device=device, env=env)
+    out = {"multiagent": multi, "physics": a.physics, "n_envs": a.n_envs, "gpus": world, "target_reward": target,
+           "best_eval_return": best, "reached": best >= target, "history": hist}
+    print(json.dumps({k: v for k, v in out.items() if k != "history"}), flush=True)
     if a.output:
         with open(a.output, "w") as f:
             json.dump(out, f, indent=1)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _rank_entry(rank, world, port, argv):
+    os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    run(parse_args(argv))
+
+
+def main():
+    a = parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None and int(env_world) != a.gpus:
+        raise SystemExit(f"learn.py: WORLD_SIZE={env_world} but --gpus {a.gpus}")
+    if env_world is not None or a.gpus <= 1:
+        run(a)
+        return
+    # --gpus N without a launcher: N rank processes, started before anything touches the GPU
+    import socket
+    import torch.multiprocessing as mp
+    if a.dist_backend == "nccl" and torch.cuda.device_count() < a.gpus:
+        raise SystemExit(f"learn.py: --gpus {a.gpus} needs {a.gpus} GPUs for RCCL (--dist-backend gloo rehearses)")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_rank_entry, args=(r, a.gpus, port, sys.argv[1:])) for r in range(a.gpus)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join()
+    if any(p.exitcode != 0 for p in procs):
+        raise SystemExit(f"learn.py: rank exit codes {[p.exitcode for p in procs]}")
 
 
 if __name__ == "__main__":

@@ -30,7 +30,7 @@ GPD_F32, GPD_F64 = 0, 1
 
 # Every symbol include/gpd.h declares (checked by tests/test_lib_symbols.py).
 EXPORTED = ("gpd_abi_version", "gpd_last_error", "gpd_default_params", "gpd_create", "gpd_destroy",
-            "gpd_get_constants", "gpd_reset", "gpd_step", "gpd_integrate", "gpd_get_state20",
+            "gpd_get_constants", "gpd_reset", "gpd_step", "gpd_step_seq", "gpd_integrate", "gpd_get_state20",
             "gpd_get_raw_state", "gpd_set_raw_state", "gpd_get_step_counters",
             "gpd_set_step_counters", "gpd_state_bytes", "gpd_save_state", "gpd_load_state",
             "gpd_default_pid_params", "gpd_set_pid_params", "gpd_get_ctrl_state", "gpd_set_ctrl_state")
@@ -104,6 +104,7 @@ def load():
         "gpd_get_constants": (ci, [vp, ctypes.POINTER(Constants)]),
         "gpd_reset": (ci, [vp, vp, vp, vp]),
         "gpd_step": (ci, [vp, vp, vp, vp, vp, vp, vp, vp]),
+        "gpd_step_seq": (ci, [vp, vp, ci, ci, vp, vp, vp, vp, vp, vp]),
         "gpd_integrate": (ci, [vp, vp, i, vp, vp]),
         "gpd_get_state20": (ci, [vp, vp, vp]),
         "gpd_get_raw_state": (ci, [vp, vp, vp]),

@@ -498,12 +498,13 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     // 65536 envs 10.45 -> 10.31, but 262144 envs 35.8 -> 38.1 (bandwidth-bound: the second
     // wave only adds occupancy pressure).  Its 128-lane copy-out needs t / NC for t <= 128.
     // A third (io) wave takes the history columns off the pose wave (step_waves = 3): measured
-    // (scripts/ab_geom.sh, profiles/r2) 4096 envs 5.42 -> 5.32 us/step, but slower from 16384
-    // envs on (6.24 -> 7.04), where the blocks are full and the copy-out overlaps anyway.
+    // (scripts/geom_probe.py, gpurun_out r2n) 2048 envs 5.30 -> 5.24 us/step, 4096 envs 5.40 ->
+    // 5.33, but 8192 envs 5.72 -> 5.90 and 16384 envs 6.23 -> 7.20: with fuller blocks the
+    // two-wave copy-out overlaps other blocks' work anyway.
     // gpd_config::step_waves overrides (1, 2 or 3).
     const bool duo_ok = s->D == 1 && C.physics_flags == 0 &&
                         (C.act_type == GPD_ACT_RPM || C.act_type == GPD_ACT_ONE_D_RPM);
-    int waves = !duo_ok || s->N > 65536 ? 1 : (s->N <= 8192 ? 3 : 2);
+    int waves = !duo_ok || s->N > 65536 ? 1 : (s->N <= 4096 ? 3 : 2);
     if (C.step_waves > 0) waves = duo_ok ? std::min(3, C.step_waves) : 1;
     for (int t = 0; t <= 2 * kWave && waves == 2; ++t)
       if ((t * s->nc_magic) >> 16 != t / NC) waves = 1;
@@ -640,6 +641,26 @@ int gpd_step(gpd_sim* sim, const float* actions, float* obs, float* reward, uint
   return sim->prec == GPD_F64
              ? launch_step<double>(sim, actions, obs, reward, terminated, truncated, terminal_obs, st)
              : launch_step<float>(sim, actions, obs, reward, terminated, truncated, terminal_obs, st);
+}
+
+int gpd_step_seq(gpd_sim* sim, const float* actions, int n_slots, int n_steps, float* obs, float* reward,
+                 uint8_t* terminated, uint8_t* truncated, float* terminal_obs, void* stream) {
+  if (!sim || !actions || !obs || !reward || !terminated || !truncated)
+    return fail(GPD_EINVAL, "gpd_step_seq: NULL argument");
+  if (n_slots < 1 || n_steps < 0) return fail(GPD_EINVAL, "gpd_step_seq: n_slots must be >= 1, n_steps >= 0");
+  if (sim->A == 4 && !aligned16(actions)) return fail(GPD_EINVAL, "gpd_step_seq: actions must be 16-byte aligned");
+  if (sim->A == 4 && (!aligned16(obs) || (terminal_obs && !aligned16(terminal_obs))))
+    return fail(GPD_EINVAL, "gpd_step_seq: obs buffers must be 16-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  const size_t slot = (size_t)sim->N * sim->A;
+  for (int t = 0; t < n_steps; ++t) {
+    const float* a = actions + (size_t)(t % n_slots) * slot;
+    const int rc = sim->prec == GPD_F64
+                       ? launch_step<double>(sim, a, obs, reward, terminated, truncated, terminal_obs, st)
+                       : launch_step<float>(sim, a, obs, reward, terminated, truncated, terminal_obs, st);
+    if (rc != GPD_OK) return rc;
+  }
+  return GPD_OK;
 }
 
 int gpd_integrate(gpd_sim* sim, const void* rpm, int n_sub, void* traj, void* stream) {

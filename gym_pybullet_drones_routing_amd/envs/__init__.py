@@ -2,7 +2,7 @@
 from .BaseRLAviary import BaseRLAviary  # noqa: F401
 from .HoverAviary import HoverAviary  # noqa: F401
 from .MultiHoverAviary import MultiHoverAviary  # noqa: F401
-from .vec_env import AviaryVecEnv, make_vec_env  # noqa: F401
+from .vec_env import AviaryVecEnv, ShardedAviaryVecEnv, make_vec_env  # noqa: F401
 
 try:  # register the reference's gymnasium ids when gymnasium is present (__init__.py:1-21)
     from gymnasium.envs.registration import register, registry

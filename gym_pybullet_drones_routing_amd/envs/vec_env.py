@@ -115,9 +115,11 @@ class AviaryVecEnv(_VecEnvBase):
         return list(indices)
 
 
-def make_vec_env(env_cls, n_envs=1, seed=None, env_kwargs=None, **vec_kwargs):
+def make_vec_env(env_cls, n_envs=1, seed=None, env_kwargs=None, distributed=False, **vec_kwargs):
     """``stable_baselines3.common.env_util.make_vec_env`` stand-in for the two RL aviaries:
-    builds ONE batched ``AviaryVecEnv`` instead of ``n_envs`` Python env objects."""
+    builds ONE batched ``AviaryVecEnv`` instead of ``n_envs`` Python env objects; with
+    ``distributed=True`` (inside an initialised torch.distributed group) a
+    ``ShardedAviaryVecEnv`` whose envs are split over the group's ranks."""
     from .HoverAviary import HoverAviary
     from .MultiHoverAviary import MultiHoverAviary
     kw = dict(env_kwargs or {})
@@ -130,4 +132,84 @@ def make_vec_env(env_cls, n_envs=1, seed=None, env_kwargs=None, **vec_kwargs):
     for k in ("gui", "record", "neighbourhood_radius"):
         kw.pop(k, None)
     kw.setdefault("physics", Physics.PYB)   # the env classes' default (HoverAviary.py:20, MultiHoverAviary.py:22)
+    if distributed:
+        return ShardedAviaryVecEnv(n_envs, task=task, num_drones=nd, **kw, **vec_kwargs)
     return AviaryVecEnv(n_envs, task=task, num_drones=nd, **kw, **vec_kwargs)
+
+
+class ShardedAviaryVecEnv:
+    """``AviaryVecEnv`` (torch output) over env shards on every rank of a ``torch.distributed``
+    group: BASELINE config 5 / SURVEY §8(e), the multi-GPU form of the reference's
+    ``make_vec_env(HoverAviary, n_envs=...)`` + PPO loop (``examples/learn.py:52-94``).
+
+    Rank r owns envs ``[r*E/G, (r+1)*E/G)`` (``shard.env_shard``) in its own ``BatchedAviarySim``.
+    The learner (rank 0) uses this object exactly like ``AviaryVecEnv(output="torch")``:
+    ``reset()``, ``step(actions [E, D, A])`` -> (obs [E, D, W], reward [E], done [E], infos) with
+    SB3's ``terminal_observation`` / ``TimeLimit.truncated``.  Each call broadcasts a one-word
+    command, then ``shard.LearnerHandoff`` scatters the actions and all-gathers the shards'
+    output packs.  Every other rank runs ``serve()``, which answers commands until ``close()``.
+    """
+    STEP, RESET, STOP = 0, 1, 2
+
+    def __init__(self, num_envs, **kw):
+        import torch.distributed as dist
+
+        from ..shard import LearnerHandoff, env_shard
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        _, count = env_shard(num_envs, self.rank, self.world)
+        kw = dict(kw)
+        kw["output"] = "torch"
+        self.local = AviaryVecEnv(count, **kw)
+        self.sim = self.local.sim
+        self.handoff = LearnerHandoff(self.sim, num_envs)
+        self.num_envs = int(num_envs)
+        self.num_drones = self.local.num_drones
+        self.action_space = self.local.action_space
+        self.observation_space = self.local.observation_space
+        self.output = "torch"
+        gloo = dist.is_initialized() and dist.get_backend() == "gloo"
+        self._cmd = torch.zeros((1,), dtype=torch.int32, device="cpu" if gloo else self.sim.device)
+        self._actions = torch.zeros((num_envs, self.num_drones, self.sim.act_width), dtype=torch.float32,
+                                    device=self.sim.device)
+        self._open = True
+
+    def _send(self, cmd):
+        if self.world > 1:
+            import torch.distributed as dist
+            self._cmd.fill_(cmd)
+            dist.broadcast(self._cmd, src=0)
+
+    def reset(self):
+        self._send(self.RESET)
+        return self.handoff.reset().clone()
+
+    def step(self, actions):
+        self._actions.copy_(torch.as_tensor(actions, dtype=torch.float32).reshape(self._actions.shape))
+        self._send(self.STEP)
+        obs, rew, te, tr, tobs = self.handoff.step(self._actions)
+        done = (te | tr).bool()
+        infos = {"terminal_observation": tobs, "TimeLimit.truncated": (tr.bool() & ~te.bool()), "done_mask": done}
+        return obs, rew, done, infos
+
+    def serve(self):
+        """Non-learner ranks: step / reset this rank's shard on the learner's command."""
+        import torch.distributed as dist
+        while True:
+            dist.broadcast(self._cmd, src=0)
+            cmd = int(self._cmd.item())
+            if cmd == self.STOP:
+                break
+            if cmd == self.RESET:
+                self.handoff.reset()
+            else:
+                self.handoff.step(None)
+        self.local.close()
+        self._open = False
+
+    def close(self):
+        if self._open:
+            if self.rank == 0:
+                self._send(self.STOP)
+            self.local.close()
+            self._open = False

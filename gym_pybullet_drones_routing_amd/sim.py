@@ -224,6 +224,21 @@ class BatchedAviarySim:
             _lib.check("gpd_step", rc)
         return self.obs, self.reward, self.terminated, self.truncated
 
+    def step_seq(self, action_slots, n_steps, terminal_obs=True):
+        """``n_steps`` consecutive :meth:`step` calls issued from native code (``gpd_step_seq``):
+        step t reads ``action_slots[t % P]`` of ``action_slots`` [P, E, D, A] (float32, on the
+        device); the output tensors hold the last step's results."""
+        a = action_slots
+        if not (isinstance(a, torch.Tensor) and a.device == self.device and a.dtype == torch.float32
+                and a.is_contiguous() and a.numel() % (self.n_drones * self.act_width) == 0):
+            raise ValueError("step_seq needs contiguous float32 action slots [P, E, D, A] on the sim's device")
+        P = a.numel() // (self.n_drones * self.act_width)
+        tptr = self._tobs_ptr if terminal_obs else None
+        with torch.cuda.device(self.device):
+            self._call("gpd_step_seq", ctypes.c_void_p(a.data_ptr()), int(P), int(n_steps), *self._out_ptrs, tptr,
+                       _stream(self.device))
+        return self.obs, self.reward, self.terminated, self.truncated
+
     def capture_graph(self, actions_seq, terminal_obs=True):
         """Record ``len(actions_seq)`` consecutive :meth:`step` launches into one HIP graph
         (``torch.cuda.CUDAGraph``).  Each ``replay()`` advances every env by that many steps,

@@ -175,6 +175,14 @@ int gpd_reset(gpd_sim* sim, const uint8_t* env_mask, float* obs, void* stream);
 int gpd_step(gpd_sim* sim, const float* actions, float* obs, float* reward,
              uint8_t* terminated, uint8_t* truncated, float* terminal_obs, void* stream);
 
+/* n_steps consecutive gpd_step calls issued from native code (open-loop action sequences:
+ * playback, benchmarks): step t reads action slot t % n_slots of actions
+ * [n_slots][E][D][act_width]; every step writes the same output buffers (as n_steps gpd_step
+ * calls would), so they hold the last step's outputs.  One kernel launch per step, no host
+ * round trip in between. */
+int gpd_step_seq(gpd_sim* sim, const float* actions, int n_slots, int n_steps, float* obs, float* reward,
+                 uint8_t* terminated, uint8_t* truncated, float* terminal_obs, void* stream);
+
 /* Raw DYN integrator: n_sub substeps, row t of rpm [n_sub][N][4] (real) drives substep t of
  * every drone; each substep is followed by the readback (PYB_STEPS_PER_CTRL = 1 cadence).
  * traj (nullable) receives the 20-float state after every substep, [n_sub][N][20] real. */

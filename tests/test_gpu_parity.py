@@ -320,6 +320,31 @@ def test_graph_replay_matches_eager():
     b.close()
 
 
+@pytest.mark.parametrize("act", ["rpm", "one_d_rpm"])
+def test_step_seq_matches_steps(act):
+    """gpd_step_seq(P slots, T steps) == T gpd_step calls on slots t % P, bit for bit (outputs,
+    terminal rows, state, counters, action ring via the next observation), past auto-resets."""
+    from gym_pybullet_drones_routing_amd.enums import ActionType
+    rng = np.random.default_rng(9)
+    E, P, T = 96, 7, 40
+    A = 4 if act == "rpm" else 1
+    pool = torch.from_numpy(rng.uniform(-1, 1, (P, E, 1, A)).astype(np.float32)).cuda()
+    a = _sim(n_envs=E, task="hover", precision="f64", act=ActionType(act))
+    b = _sim(n_envs=E, task="hover", precision="f64", act=ActionType(act))
+    for t in range(T):
+        a.step(pool[t % P])
+    b.step_seq(pool, T)
+    torch.cuda.synchronize()
+    for x, y in ((a.obs, b.obs), (a.reward, b.reward), (a.terminated, b.terminated), (a.truncated, b.truncated),
+                 (a.terminal_obs, b.terminal_obs), (a.raw_state(), b.raw_state()), (a.step_counters(), b.step_counters())):
+        assert torch.equal(x, y)
+    a.step(pool[0])
+    b.step(pool[0])
+    assert torch.equal(a.obs, b.obs)
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("prec", ["f64", "f32"])
 def test_gpu_kat_hover_and_symmetric_thrust(prec):
     """KAT-1 on the GPU (hover from rest stays put) and the symmetry the reference has exactly:

@@ -24,3 +24,54 @@ def test_ppo_two_iterations(multi):
     for h in hist:
         assert math.isfinite(h["mean_step_reward"]) and h["eval_len"] >= 1
     assert any("Observation space" in l for l in logs if isinstance(l, str))
+
+
+def _sharded_worker(rank, world, port, q):
+    import datetime
+
+    import torch
+    import torch.distributed as dist
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    try:
+        import learn
+        from gym_pybullet_drones_routing_amd.enums import Physics
+        env = learn.make_env(False, 128, learn.DEFAULT_ACT, Physics.PYB, "cuda:0", distributed=True)
+        assert env.sim.n_envs == 64
+        if rank == 0:
+            _, hist, _, _ = learn.train(n_envs=128, n_steps=8, total_timesteps=2 * 128 * 8, minibatch=512, epochs=2,
+                                        eval_every=1, log=lambda *a: None, device=torch.device("cuda:0"), env=env)
+            env.close()
+            q.put(hist)
+        else:
+            env.serve()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ppo_sharded_two_ranks_matches_single_process():
+    """examples/learn.py --gpus 2 (config 5 plumbing): the learner on rank 0 drives two env shards
+    through ShardedAviaryVecEnv (command broadcast, action scatter, output-pack all-gather; gloo,
+    both ranks on this GPU).  The training history equals one process stepping all 128 envs:
+    the gathered batch is bit-identical, so the seeded PPO run is too."""
+    import socket
+
+    import torch.multiprocessing as mp
+    import learn
+    from tests.test_gpu_dist import _collect
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    hist2 = _collect(q, procs)
+    _, hist1, _, _ = learn.train(n_envs=128, n_steps=8, total_timesteps=2 * 128 * 8, minibatch=512, epochs=2,
+                                 eval_every=1, log=lambda *a: None)
+    assert len(hist1) == len(hist2) == 2
+    for a, b in zip(hist1, hist2):
+        assert a["timesteps"] == b["timesteps"]
+        assert math.isclose(a["mean_step_reward"], b["mean_step_reward"], rel_tol=1e-6)
+        assert math.isclose(a["eval_return"], b["eval_return"], rel_tol=1e-5) and a["eval_len"] == b["eval_len"]
