@@ -166,6 +166,20 @@ Consts<R> make_consts(const gpd_sim* s) {
   c.ang_damp = (R)0.04;      // btMultiBody() m_angularDamping
   c.max_vel = (R)100.0;      // btMultiBody() m_maxCoordinateVelocity
   c.ang_thr2 = (R)((0.125 * M_PI) * (0.125 * M_PI));   // (ANGULAR_MOTION_THRESHOLD / 2)^2
+  // ground-plane contact (plane_contact; constants restated in oracle/bullet_mb.py)
+  c.cyl_r = (R)P.collision_r;
+  c.cyl_hh = (R)(P.collision_h / 2);
+  c.cyl_zoff = (R)P.collision_z_offset;
+  {
+    const double r = P.collision_r + 0.001, h = P.collision_h / 2 + 0.001;   // + URDF shape margin
+    c.brk = (R)(0.02 * std::sqrt(r * r + r * r + h * h));                   // 0.02 x motion disc
+  }
+  c.slop = (R)1e-5;          // m_linearSlop (pybullet)
+  c.erp = (R)0.08;           // m_erp2 (pybullet contactERP)
+  c.mu = (R)(0.5 * 1.0);     // drone default friction x plane.urdf lateral_friction
+  c.plane_half = (R)15.0;    // plane.urdf collision box 30 x 30
+  c.resid = (R)1e-7;         // m_leastSquaresResidualThreshold (pybullet)
+  c.iters = 50;              // m_numIterations (pybullet numSolverIterations)
   c.nsub = s->nsub;
   const gpd_pid_params& Q = s->pid;
   PidConsts<R>& k = c.pid;
@@ -421,7 +435,7 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   if (C.task == GPD_TASK_HOVER && C.drones_per_env != 1)
     return fail(GPD_EINVAL, "gpd_create: HoverAviary is single-drone (drones_per_env must be 1)");
   if (C.precision != GPD_F32 && C.precision != GPD_F64) return fail(GPD_EINVAL, "gpd_create: bad precision");
-  if (C.physics_flags & ~(GPD_F_GND | GPD_F_DRAG | GPD_F_DW | GPD_F_GEOM_WRENCH | GPD_F_BULLET))
+  if (C.physics_flags & ~(GPD_F_GND | GPD_F_DRAG | GPD_F_DW | GPD_F_GEOM_WRENCH | GPD_F_BULLET | GPD_F_NO_PLANE))
     return fail(GPD_EINVAL, "gpd_create: unknown physics flag");
   if (params->model < GPD_MODEL_CF2X || params->model > GPD_MODEL_RACE)
     return fail(GPD_EINVAL, "gpd_create: unknown drone model");

@@ -77,7 +77,7 @@ template <> struct PiC<double> { static constexpr double pi = 3.1415926535897932
 
 // ---------------------------------------------------------------- model constants (device memory)
 enum : int { MODEL_CF2X = 0, MODEL_CF2P = 1, MODEL_RACE = 2 };
-enum : int { F_GND = 1, F_DRAG = 2, F_DW = 4, F_GEOM = 8, F_BULLET = 16 };
+enum : int { F_GND = 1, F_DRAG = 2, F_DW = 4, F_GEOM = 8, F_BULLET = 16, F_NO_PLANE = 32 };
 // PF, the physics flags a kernel is compiled for: 0 = plain DYN (the FAST path), a flag set =
 // those terms compiled in (no flag tests, one basic block per substep), kPfRuntime = the terms
 // selected at run time from Consts::flags (every other combination).
@@ -118,6 +118,11 @@ struct Consts {
   R lin_damp, ang_damp;    // btMultiBody m_linearDamping / m_angularDamping defaults (F_BULLET)
   R max_vel;               // btMultiBody m_maxCoordinateVelocity (F_BULLET)
   R ang_thr2;              // (ANGULAR_MOTION_THRESHOLD/2)^2: the clamped half angle, squared
+  // ground-plane contact of the PYB* modes (plane_contact; oracle/bullet_mb.py plane_contact)
+  R cyl_r, cyl_hh, cyl_zoff;   // collision cylinder (cf2x.urdf:31-35): radius, half length, z offset
+  R brk;                       // contact breaking threshold (0.02 x the cylinder's motion disc)
+  R slop, erp, mu, plane_half, resid;   // m_linearSlop, m_erp2, combined friction, plane box, residual
+  int iters;                   // m_numIterations
   R init0[10];             // reset template of drone 0 (pos, stored quat, rpy): single-drone envs
   R target0[3];            // task target of drone 0 (single-drone envs: no dependent global load)
                            // read it with scalar loads instead of a dependent per-lane load
@@ -510,6 +515,158 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
   tz_out = W[3];
 }
 
+// ---------------------------------------------------------------- ground-plane contact (PYB*)
+// The drone's collision cylinder (cf2x.urdf:31-35) against plane.urdf (BaseAviary.py:484; the
+// collision filter at :500-503 is commented out), solved the way btMultiBodyConstraintSolver
+// does inside p.stepSimulation(): after the unconstrained velocity update, before
+// integrateTransforms, on the pose at the start of the step.  Restatement and its constants:
+// oracle/bullet_mb.py plane_contact (parity unpinned: pybullet is absent).
+//   * candidates: the rim points at body azimuth 0/90/180/270 deg of the cap facing down; a
+//     point joins when its height is below the breaking threshold and it lies over the plane
+//     box's top face;
+//   * rows per point, in base-frame coordinates (M^-1 = diag(1/m, 1/I)): normal = world +z, two
+//     friction directions (0,-1,0), (1,0,0) solved as a pair on the implicit cone;
+//   * projected Gauss-Seidel: every normal row, then every friction pair, per iteration; stop
+//     when the largest squared residual <= resid or after `iters` iterations.
+// Inactive points carry rhs = jdi = 0, so their rows solve to a zero impulse without a branch.
+// The caller gates the call on a wave ballot: a wave without a low drone never enters.
+template <typename R>
+__device__ __forceinline__ R pc_dot(R ax, R ay, R az, R bx, R by, R bz) { return (ax * bx + ay * by) + az * bz; }
+
+template <typename R>
+__device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const Consts<R>& c, const DynK<R>& k) {
+  // the rows live in LDS (one column per lane of the block's single wave): in registers they
+  // would raise the whole kernel's VGPR count for a path that only landing drones take
+  enum { kRhs = 0, kJdi = 3, kJdn = 6, kLam = 7, kPer = 10 };
+  __shared__ R pc[4 * kPer][64];
+  const int ln = threadIdx.x;
+  const R nx = Rm[6], ny = Rm[7], nz = Rm[8];          // base-frame world +z
+  const R ux = -Rm[3], uy = -Rm[4], uz = -Rm[5];       // (0,-1,0)
+  const R ex = Rm[0], ey = Rm[1], ez = Rm[2];          // (1,0,0)
+  const R zc = (-Rm[8] < R(0) ? -c.cyl_hh : c.cyl_hh) + c.cyl_zoff;
+  const R cr = c.cyl_r;
+  bool any = false;
+  {
+    // base-frame velocities
+    const R vbx = pc_dot(Rm[0], Rm[3], Rm[6], s.vx, s.vy, s.vz);
+    const R vby = pc_dot(Rm[1], Rm[4], Rm[7], s.vx, s.vy, s.vz);
+    const R vbz = pc_dot(Rm[2], Rm[5], Rm[8], s.vx, s.vy, s.vz);
+    const R wbx = pc_dot(Rm[0], Rm[3], Rm[6], s.wx, s.wy, s.wz);
+    const R wby = pc_dot(Rm[1], Rm[4], Rm[7], s.wx, s.wy, s.wz);
+    const R wbz = pc_dot(Rm[2], Rm[5], Rm[8], s.wx, s.wy, s.wz);
+#pragma unroll 1
+    for (int p = 0; p < 4; ++p) {
+      const R rx = p == 0 ? cr : (p == 2 ? -cr : R(0)), ry = p == 1 ? cr : (p == 3 ? -cr : R(0));
+      const R dist = s.pz + pc_dot(nx, ny, nz, rx, ry, zc);
+      const R wxp = s.px + pc_dot(Rm[0], Rm[1], Rm[2], rx, ry, zc);
+      const R wyp = s.py + pc_dot(Rm[3], Rm[4], Rm[5], rx, ry, zc);
+      const bool act = dist < c.brk && g_abs(wxp) <= c.plane_half && g_abs(wyp) <= c.plane_half;
+      any = any || act;
+      const R dx[3] = {nx, ux, ex}, dy[3] = {ny, uy, ey}, dz[3] = {nz, uz, ez};
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const R ax = ry * dz[j] - zc * dy[j], ay = zc * dx[j] - rx * dz[j], az = rx * dy[j] - ry * dx[j];
+        const R jd = k.inv_m + ((ax * (ax * k.ijx) + ay * (ay * k.ijy)) + az * (az * k.ijz));
+        const R inv = R(1) / jd;
+        const R rel = pc_dot(dx[j], dy[j], dz[j], vbx, vby, vbz) + pc_dot(ax, ay, az, wbx, wby, wbz);
+        R r;
+        if (j == 0) {
+          const R pen = dist + c.slop;
+          r = pen > R(0) ? (-rel - pen / k.dt) * inv : (-pen * c.erp / k.dt - rel) * inv;
+          pc[p * kPer + kJdn][ln] = act ? jd : R(0);
+        } else {
+          r = -rel * inv;
+        }
+        pc[p * kPer + kJdi + j][ln] = act ? inv : R(0);
+        pc[p * kPer + kRhs + j][ln] = act ? r : R(0);
+        pc[p * kPer + kLam + j][ln] = R(0);
+      }
+    }
+  }
+  const R nx_ = nx, ny_ = ny, nz_ = nz, ux_ = ux, uy_ = uy, uz_ = uz, ex_ = ex, ey_ = ey, ez_ = ez;
+  const R zc_ = zc, cr_ = cr;
+  R dl0 = R(0), dl1 = R(0), dl2 = R(0), da0 = R(0), da1 = R(0), da2 = R(0);
+  bool done = !any;
+  for (int it = 0; it < c.iters; ++it) {
+    if (__ballot(!done) == 0ull) break;
+    if (!done) {
+      // opaque per iteration, and the point loops kept rolled: keeps the compiler from hoisting
+      // the 24 loop-invariant row Jacobians (and their M^-1 products) into registers, which
+      // would raise the whole kernel's VGPR count
+      const R nx = vpin(nx_), ny = vpin(ny_), nz = vpin(nz_), ux = vpin(ux_), uy = vpin(uy_), uz = vpin(uz_);
+      const R ex = vpin(ex_), ey = vpin(ey_), ez = vpin(ez_), zc = vpin(zc_);
+      const R cr = vpin(cr_);
+      R res = R(0);
+#pragma unroll 1
+      for (int p = 0; p < 4; ++p) {                  // normal rows
+        const R rx = p == 0 ? cr : (p == 2 ? -cr : R(0)), ry = p == 1 ? cr : (p == 3 ? -cr : R(0));
+        const R ax = ry * nz - zc * ny, ay = zc * nx - rx * nz, az = rx * ny - ry * nx;
+        const R jv = pc_dot(nx, ny, nz, dl0, dl1, dl2) + pc_dot(ax, ay, az, da0, da1, da2);
+        const R lam = pc[p * kPer + kLam][ln];
+        R delta = pc[p * kPer + kRhs][ln] - pc[p * kPer + kJdi][ln] * jv;
+        const R sum = lam + delta;
+        const bool neg = sum < R(0);
+        delta = neg ? -lam : delta;
+        pc[p * kPer + kLam][ln] = neg ? R(0) : sum;
+        const R dm = k.inv_m * delta;
+        dl0 = dl0 + nx * dm; dl1 = dl1 + ny * dm; dl2 = dl2 + nz * dm;
+        da0 = da0 + (ax * k.ijx) * delta; da1 = da1 + (ay * k.ijy) * delta; da2 = da2 + (az * k.ijz) * delta;
+        const R rr = delta * pc[p * kPer + kJdn][ln];
+        res = rr * rr > res ? rr * rr : res;
+      }
+#pragma unroll 1
+      for (int p = 0; p < 4; ++p) {                  // friction pairs on the cone
+        const R rx = p == 0 ? cr : (p == 2 ? -cr : R(0)), ry = p == 1 ? cr : (p == 3 ? -cr : R(0));
+        const R bx = ry * uz - zc * uy, by = zc * ux - rx * uz, bz = rx * uy - ry * ux;
+        const R cx = ry * ez - zc * ey, cy = zc * ex - rx * ez, cz = rx * ey - ry * ex;
+        const R lnrm = pc[p * kPer + kLam][ln];
+        const bool on = lnrm > R(0);
+        const R lim = c.mu * lnrm;
+        const R l1 = pc[p * kPer + kLam + 1][ln], l2 = pc[p * kPer + kLam + 2][ln];
+        const R j1 = pc_dot(ux, uy, uz, dl0, dl1, dl2) + pc_dot(bx, by, bz, da0, da1, da2);
+        const R j2 = pc_dot(ex, ey, ez, dl0, dl1, dl2) + pc_dot(cx, cy, cz, da0, da1, da2);
+        R s1 = l1 + (pc[p * kPer + kRhs + 1][ln] - pc[p * kPer + kJdi + 1][ln] * j1);
+        R s2 = l2 + (pc[p * kPer + kRhs + 2][ln] - pc[p * kPer + kJdi + 2][ln] * j2);
+        const R m2 = s1 * s1 + s2 * s2;
+        if (m2 > lim * lim) {
+          const R f = lim / g_sqrt(m2);
+          s1 = s1 * f;
+          s2 = s2 * f;
+        }
+        const R d1 = on ? s1 - l1 : R(0);
+        const R d2 = on ? s2 - l2 : R(0);
+        pc[p * kPer + kLam + 1][ln] = on ? s1 : l1;
+        pc[p * kPer + kLam + 2][ln] = on ? s2 : l2;
+        const R m1 = k.inv_m * d1, m2v = k.inv_m * d2;
+        dl0 = dl0 + ux * m1; dl1 = dl1 + uy * m1; dl2 = dl2 + uz * m1;
+        da0 = da0 + (bx * k.ijx) * d1; da1 = da1 + (by * k.ijy) * d1; da2 = da2 + (bz * k.ijz) * d1;
+        dl0 = dl0 + ex * m2v; dl1 = dl1 + ey * m2v; dl2 = dl2 + ez * m2v;
+        da0 = da0 + (cx * k.ijx) * d2; da1 = da1 + (cy * k.ijy) * d2; da2 = da2 + (cz * k.ijz) * d2;
+        const R rr = (d1 + d2) * (d1 + d2);
+        res = rr > res ? rr : res;
+      }
+      done = res <= c.resid;
+    }
+  }
+  // back to world coordinates (rows of Rm: world = Rm . base); lanes without an active point
+  // keep their velocities bit for bit, signed zeros included
+  s.vx = any ? s.vx + pc_dot(Rm[0], Rm[1], Rm[2], dl0, dl1, dl2) : s.vx;
+  s.vy = any ? s.vy + pc_dot(Rm[3], Rm[4], Rm[5], dl0, dl1, dl2) : s.vy;
+  s.vz = any ? s.vz + pc_dot(Rm[6], Rm[7], Rm[8], dl0, dl1, dl2) : s.vz;
+  s.wx = any ? s.wx + pc_dot(Rm[0], Rm[1], Rm[2], da0, da1, da2) : s.wx;
+  s.wy = any ? s.wy + pc_dot(Rm[3], Rm[4], Rm[5], da0, da1, da2) : s.wy;
+  s.wz = any ? s.wz + pc_dot(Rm[6], Rm[7], Rm[8], da0, da1, da2) : s.wz;
+}
+
+// Lowest height of the contact candidates (the cap facing down, rim at 0/90/180/270 deg): the
+// wave gate of plane_contact.
+template <typename R>
+__device__ __forceinline__ R contact_low(const Drone<R>& s, const R Rm[9], const Consts<R>& c) {
+  const R zc = (-Rm[8] < R(0) ? -c.cyl_hh : c.cyl_hh) + c.cyl_zoff;
+  const R h = g_abs(Rm[6]) > g_abs(Rm[7]) ? g_abs(Rm[6]) : g_abs(Rm[7]);
+  return (s.pz + Rm[8] * zc) - c.cyl_r * h;
+}
+
 // ---------------------------------------------------------------- one Bullet (PYB*) substep
 // Physics.PYB* (SURVEY.md §8 f3): the forces of _physics / _groundEffect / _drag / _downwash
 // (BaseAviary.py:679-811) on the links of the URDF multibody, then ONE p.stepSimulation()
@@ -571,6 +728,12 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, const R rpm[4], cons
   s.vx = clampv(s.vx + k.dt * (Fx * k.inv_m - kv * s.vx));
   s.vy = clampv(s.vy + k.dt * (Fy * k.inv_m - kv * s.vy));
   s.vz = clampv(s.vz + k.dt * (Fz * k.inv_m - kv * s.vz));
+  // ground-plane contact (solveConstraints, before integrateTransforms); the margin keeps the
+  // gate conservative against the candidates' own rounding
+  if (!pf_on<PF>(k.flags, F_NO_PLANE)) {
+    const bool low = contact_low(s, Rm, c) < c.brk + R(1e-6);
+    if (GPD_RARE(__ballot(low) != 0ull)) plane_contact<R>(s, Rm, c, k);
+  }
   s.px = s.px + k.dt * s.vx;
   s.py = s.py + k.dt * s.vy;
   s.pz = s.pz + k.dt * s.vz;

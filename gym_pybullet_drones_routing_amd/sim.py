@@ -21,7 +21,7 @@ _ACTS = {ActionType.RPM: _lib.GPD_ACT_RPM, ActionType.ONE_D_RPM: _lib.GPD_ACT_ON
 PID_ACTS = (ActionType.PID, ActionType.VEL, ActionType.ONE_D_PID)
 _TASKS = {"none": _lib.GPD_TASK_NONE, "hover": _lib.GPD_TASK_HOVER, "multihover": _lib.GPD_TASK_MULTIHOVER}
 _AERO = {"gnd": _lib.GPD_F_GND, "drag": _lib.GPD_F_DRAG, "dw": _lib.GPD_F_DW, "geom": _lib.GPD_F_GEOM_WRENCH,
-         "bullet": _lib.GPD_F_BULLET}
+         "bullet": _lib.GPD_F_BULLET, "no_plane": _lib.GPD_F_NO_PLANE}
 _PHYSICS = {
     Physics.DYN: (),
     Physics.PYB: ("bullet",),
@@ -30,7 +30,13 @@ _PHYSICS = {
     Physics.PYB_DW: ("bullet", "dw"),
     Physics.PYB_GND_DRAG_DW: ("bullet", "gnd", "drag", "dw"),
 }
-_warned_pyb = False
+_warned = set()
+
+
+def _warn_once(key, msg):
+    if key not in _warned:
+        _warned.add(key)
+        warnings.warn(msg, stacklevel=3)
 
 
 def physics_flags(physics=Physics.DYN, aero=()):
@@ -39,21 +45,20 @@ def physics_flags(physics=Physics.DYN, aero=()):
     DYN is the reference's explicit integrator (BaseAviary.py:352-353).  The PYB* values apply
     the reference's forces (``_physics`` / ``_groundEffect`` / ``_drag`` / ``_downwash``,
     :679-811) to a restated Bullet3 multibody base step (``p.stepSimulation``, :369-370; SURVEY
-    §8 f3): default damping, world-frame angular velocity, exponential-map orientation.  Bullet's
-    contacts (ground plane, drone-drone) are not reproduced, which is reported once with a
-    warning.  ``aero`` adds terms by name (``gnd``, ``drag``, ``dw``, ``geom``, ``bullet``), e.g.
-    the aero terms on the DYN integrator (BASELINE config 3).
+    §8 f3): default damping, world-frame angular velocity, exponential-map orientation, and the
+    collision cylinder's contact with the ground plane (``plane.urdf``, BaseAviary.py:484).
+    Drone <-> drone collisions are not reproduced, which multi-drone envs report once with a
+    warning.  ``aero`` adds terms by name (``gnd``, ``drag``, ``dw``, ``geom``, ``bullet``,
+    ``no_plane``), e.g. the aero terms on the DYN integrator (BASELINE config 3), or
+    ``no_plane`` for the reference's commented-out plane collision filter (:500-503).
     """
-    global _warned_pyb
     physics = Physics(physics)
     terms = set(_PHYSICS[physics]) | set(aero)
     unknown = terms - set(_AERO)
     if unknown:
         raise ValueError(f"unknown aero terms {sorted(unknown)}; expected a subset of {sorted(_AERO)}")
-    if "bullet" in terms and not _warned_pyb:
-        warnings.warn(f"{physics}: Bullet3 multibody step restated without contacts (a drone below the ground "
-                      "plane keeps falling; drones do not collide)", stacklevel=3)
-        _warned_pyb = True
+    if "no_plane" in terms and "bullet" not in terms:
+        raise ValueError("'no_plane' applies to the Physics.PYB* modes only (Physics.DYN has no contacts)")
     flags = 0
     for t in terms:
         flags |= _AERO[t]
@@ -108,6 +113,10 @@ class BatchedAviarySim:
         act = ActionType(act)
         if precision not in ("f32", "f64"):
             raise ValueError("precision must be 'f32' or 'f64'")
+        if precision == "f32":
+            _warn_once("f32", "precision='f32' does not meet the 1e-5 state-parity gate over 5 s (open-loop "
+                       "attitude dynamics amplify float32 rounding to 1e-5..2e-4; DESIGN.md §5); f64 is the "
+                       "reference's precision and costs about the same on MI355X")
         self.drone_model = DroneModel(drone_model)
         self.params = parse_urdf(urdf_path, self.drone_model) if urdf_path else default_params(self.drone_model)
         self.params.model = model_id(self.drone_model)
@@ -124,6 +133,9 @@ class BatchedAviarySim:
         cfg.act_type = _ACTS[act]
         cfg.task = _TASKS[task]
         cfg.physics_flags = physics_flags(physics, aero)
+        if cfg.physics_flags & _lib.GPD_F_BULLET and self.drones_per_env > 1:
+            _warn_once("pyb_multi", f"{Physics(physics)}: drone <-> drone collisions are not restated "
+                       "(the ground-plane contact is)")
         cfg.precision = _lib.GPD_F32 if precision == "f32" else _lib.GPD_F64
         cfg.autoreset = 1 if autoreset else 0
         cfg.episode_len_sec = float(episode_len_sec)

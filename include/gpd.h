@@ -85,7 +85,10 @@ extern "C" {
 #define GPD_F_BULLET 16       /* Physics.PYB*: the forces go through a restated Bullet3 btMultiBody
                                  base step (p.stepSimulation, :369-370; default damping 0.04,
                                  world-frame angular velocity, exponential-map orientation, velocity
-                                 clamp 100; no contacts) instead of _dynamics; implies GEOM_WRENCH */
+                                 clamp 100, ground-plane contact of the collision cylinder) instead
+                                 of _dynamics; implies GEOM_WRENCH */
+#define GPD_F_NO_PLANE 32     /* with GPD_F_BULLET: no drone <-> plane contact (the reference's
+                                 commented-out setCollisionFilterPair, BaseAviary.py:500-503) */
 
 /* precision */
 #define GPD_F32 0

@@ -38,11 +38,14 @@ the reference tree):
   the orientation ``m_baseQuat.inverse()`` through a ``btTransform`` basis (the same round trip
   as on the DYN path), world linear and angular velocity.
 
-Not restated: contacts.  The collision cylinder (``cf2x.urdf:31-35``) against ``plane.urdf`` and
-against other drones is Bullet's constraint solver (PGS, ERP, friction), which this path does
-not model: a body below the plane keeps falling.  Bit-level rounding of Bullet's own operation
-order (the world <-> base round trips of the link forces, the 6x6 inverse of the articulated
-inertia) is not reproduced either; the restatement is exact in exact arithmetic.
+Ground-plane contact (``p.loadURDF("plane.urdf")``, ``:484``; the drone <-> plane collision filter
+at ``:500-503`` is commented out, so the pair collides) is restated as ``plane_contact`` below:
+Bullet's multibody contact constraints solved by projected Gauss-Seidel inside
+``btMultiBodyConstraintSolver`` between the velocity update and ``integrateTransforms``.  The
+contact set is this restatement's own (see ``plane_contact``); drone <-> drone collisions
+(cylinder vs cylinder, MultiHoverAviary) are not restated.  Bit-level rounding of Bullet's own
+operation order (the world <-> base round trips of the link forces, the 6x6 inverse of the
+articulated inertia) is not reproduced either; the restatement is exact in exact arithmetic.
 
 Parity status: **parity unpinned** - restated from Bullet3 knowledge; pybullet cannot be run
 in this pipeline.  Pinned by the analytic checks in ``tests/test_oracle_bullet.py`` (hover
@@ -102,12 +105,13 @@ def base_quat_update(q_wb, omega_w, dt):
 
 
 def multibody_step(pos, q_s, vel_w, omega_w, f_base, t_base, f_world, m, inertia, dt,
-                   lin_damp=LIN_DAMP, ang_damp=ANG_DAMP, max_vel=MAX_COORD_VEL):
-    """One ``stepSimulation`` of a free base with no contacts.
+                   lin_damp=LIN_DAMP, ang_damp=ANG_DAMP, max_vel=MAX_COORD_VEL, cylinder=None):
+    """One ``stepSimulation`` of a free base.
 
     ``f_base`` / ``t_base``: force and torque in the base frame (the link forces moved to the
-    base COM); ``f_world``: world-frame base force (gravity).  Returns the new
-    (pos, q_s, vel_w, omega_w)."""
+    base COM); ``f_world``: world-frame base force (gravity).  ``cylinder`` = (radius,
+    half_height, z_offset) of the collision cylinder turns on the ground-plane contact
+    (``plane_contact``); None = free flight.  Returns the new (pos, q_s, vel_w, omega_w)."""
     inertia = np.asarray(inertia, dtype=np.float64)
     q_wb = qconj(q_s)                                        # m_baseQuat
     rot = quat_to_mat(q_wb)                                  # rot_from_parent[0]: world -> base
@@ -126,6 +130,152 @@ def multibody_step(pos, q_s, vel_w, omega_w, f_base, t_base, f_world, m, inertia
     vdot = rot.T @ (acc_lin + np.cross(w, v))
     omega_new = np.clip(np.asarray(omega_w, dtype=np.float64) + wdot * dt, -max_vel, max_vel)
     vel_new = np.clip(np.asarray(vel_w, dtype=np.float64) + vdot * dt, -max_vel, max_vel)
+    if cylinder is not None:                                 # solveConstraints, before integrateTransforms
+        vel_new, omega_new = plane_contact(pos, rot.T, vel_new, omega_new, m, inertia, dt, *cylinder)
     pos_new = np.asarray(pos, dtype=np.float64) + dt * vel_new
     q_s_new = qconj(base_quat_update(q_wb, omega_new, dt))
     return pos_new, q_s_new, vel_new, omega_new
+
+
+# ---------------------------------------------------------------------------- ground-plane contact
+# pybullet's world settings (PhysicsServerCommandProcessor::createEmptyDynamicsWorld) and Bullet3
+# defaults the contact restatement uses; third-party values restated from Bullet3 knowledge
+# (parity unpinned, see the module doc).
+CONTACT_ERP = 0.08          # btContactSolverInfo::m_erp2 as pybullet sets it (contactERP)
+LINEAR_SLOP = 1e-5          # m_linearSlop as pybullet sets it
+SOLVER_ITERS = 50           # m_numIterations as pybullet sets it (numSolverIterations)
+RESIDUAL_THRESHOLD = 1e-7   # m_leastSquaresResidualThreshold as pybullet sets it
+FRICTION = 0.5 * 1.0        # combined friction = drone (btCollisionObject default 0.5, the URDFs
+                            # carry no <contact>) x plane.urdf lateral_friction 1; restitution 0
+URDF_MARGIN = 0.001         # gUrdfDefaultCollisionMargin (collision-shape margin of URDF shapes)
+BREAKING_FACTOR = 0.02      # gContactBreakingThreshold, relative to the shape's angular-motion disc
+PLANE_HALF = 15.0           # plane.urdf collision box 30 x 30 x 10 at z = -5: top face z = 0
+
+
+def breaking_threshold(radius, half_height):
+    """btCollisionDispatcher (CD_USE_RELATIVE_CONTACT_BREAKING_THRESHOLD) takes the smaller of the
+    two shapes' getContactBreakingThreshold(0.02) = 0.02 * getAngularMotionDisc(); the drone's
+    cylinder is the smaller: disc = |AABB half extents| incl. margin, centred at the origin."""
+    r, h = radius + URDF_MARGIN, half_height + URDF_MARGIN
+    return BREAKING_FACTOR * math.sqrt(r * r + r * r + h * h)
+
+
+def contact_points(radius, half_height, z_offset, rot_bw):
+    """Body-frame contact candidates: the four rim points at body azimuth 0, 90, 180, 270 deg of
+    the cap whose outward normal points down (btCylinderShapeZ's support rule: ``v.z < 0`` ->
+    the -z cap, with v = R^T (0, 0, -1)).  Bullet's own manifold holds <= 4 points refreshed
+    from GJK/EPA and its contact cache; this fixed four-point set is the restatement's
+    deterministic stand-in for a resting / landing cylinder."""
+    zc = -half_height if -rot_bw[2, 2] < 0.0 else half_height
+    zc = zc + z_offset
+    return [np.array([radius, 0.0, zc]), np.array([0.0, radius, zc]),
+            np.array([-radius, 0.0, zc]), np.array([0.0, -radius, zc])]
+
+
+def plane_contact(pos, rot_bw, vel_w, omega_w, m, inertia, dt, radius, half_height, z_offset):
+    """Contact of the collision cylinder with the ground plane for one ``stepSimulation``.
+
+    Follows btMultiBodyConstraintSolver for a free base against a static body:
+    * contact geometry from the pose at the start of the step (collision detection runs before
+      the solve), velocities after the unconstrained update (solveExternalForces);
+    * a candidate point joins when its signed distance to the plane is below the breaking
+      threshold and it lies over the plane box's top face;
+    * rows per point: the normal (+z) and two friction directions (btPlaneSpace1(+z) =
+      (0,-1,0), (1,0,0); SOLVER_USE_2_FRICTION_DIRECTIONS with the implicit friction cone);
+      Jacobians in the base frame, M^-1 = diag(1/m, 1/I);
+    * normal rhs: separated points (penetration = distance + slop > 0) are speculative,
+      velocityError = -v_n - penetration/dt; penetrating points add the ERP position error
+      -penetration * erp / dt; restitution 0, cfm 0; impulse >= 0;
+    * friction rhs: -v_t; the pair (t1, t2) is projected onto the cone |lambda_t| <=
+      mu * lambda_n, and solved only while the point's normal impulse is positive;
+    * each iteration solves every normal row, then every friction pair; the solver stops when
+      the largest squared row residual (normal: delta * jacDiag, friction pair: delta1 + delta2)
+      is <= the threshold, or after the iteration cap;
+    * no warm start (the restatement keeps no manifold between steps).
+    Returns the new world (vel, omega)."""
+    rot_bw = np.asarray(rot_bw, dtype=np.float64)
+    pos = np.asarray(pos, dtype=np.float64)
+    brk = breaking_threshold(radius, half_height)
+    n_b = rot_bw[2, :].copy()                 # base-frame directions of world +z, (0,-1,0), (1,0,0)
+    t1_b = -rot_bw[1, :]
+    t2_b = rot_bw[0, :].copy()
+    pts = []
+    for r in contact_points(radius, half_height, z_offset, rot_bw):
+        dist = pos[2] + n_b @ r
+        wx = pos[0] + rot_bw[0, :] @ r
+        wy = pos[1] + rot_bw[1, :] @ r
+        if dist < brk and abs(wx) <= PLANE_HALF and abs(wy) <= PLANE_HALF:
+            pts.append((r, dist))
+    if not pts:
+        return vel_w, omega_w
+    inertia = np.asarray(inertia, dtype=np.float64)
+    inv_m = 1.0 / m
+    inv_i = 1.0 / inertia
+    v_b = rot_bw.T @ np.asarray(vel_w, dtype=np.float64)
+    w_b = rot_bw.T @ np.asarray(omega_w, dtype=np.float64)
+
+    def row(r, d):
+        a = np.array([r[1] * d[2] - r[2] * d[1], r[2] * d[0] - r[0] * d[2], r[0] * d[1] - r[1] * d[0]])
+        jd = inv_m + ((a[0] * (a[0] * inv_i[0]) + a[1] * (a[1] * inv_i[1])) + a[2] * (a[2] * inv_i[2]))
+        rel = ((d[0] * v_b[0] + d[1] * v_b[1]) + d[2] * v_b[2]) + ((a[0] * w_b[0] + a[1] * w_b[1]) + a[2] * w_b[2])
+        return a, jd, 1.0 / jd, rel
+
+    rows = []
+    for r, dist in pts:
+        a_n, jd_n, jdi_n, rel_n = row(r, n_b)
+        pen = dist + LINEAR_SLOP
+        if pen > 0:
+            rhs_n = (-rel_n - pen / dt) * jdi_n
+        else:
+            rhs_n = (-pen * CONTACT_ERP / dt - rel_n) * jdi_n
+        a_1, _, jdi_1, rel_1 = row(r, t1_b)
+        a_2, _, jdi_2, rel_2 = row(r, t2_b)
+        rows.append(dict(a=(a_n, a_1, a_2), jd_n=jd_n, jdi=(jdi_n, jdi_1, jdi_2),
+                         rhs=(rhs_n, -rel_1 * jdi_1, -rel_2 * jdi_2), lam=[0.0, 0.0, 0.0]))
+    dvl = np.zeros(3)
+    dva = np.zeros(3)
+
+    def jdv(d, a):
+        return ((d[0] * dvl[0] + d[1] * dvl[1]) + d[2] * dvl[2]) + ((a[0] * dva[0] + a[1] * dva[1]) + a[2] * dva[2])
+
+    def apply(d, a, delta):
+        for j in range(3):
+            dvl[j] = dvl[j] + d[j] * (inv_m * delta)
+            dva[j] = dva[j] + (a[j] * inv_i[j]) * delta
+
+    for _ in range(SOLVER_ITERS):
+        res = 0.0
+        for c in rows:                                        # normal rows
+            delta = c["rhs"][0] - c["jdi"][0] * jdv(n_b, c["a"][0])
+            s = c["lam"][0] + delta
+            if s < 0.0:
+                delta = -c["lam"][0]
+                s = 0.0
+            c["lam"][0] = s
+            apply(n_b, c["a"][0], delta)
+            res = max(res, (delta * c["jd_n"]) ** 2)
+        for c in rows:                                        # friction pairs (implicit cone)
+            ln = c["lam"][0]
+            if not ln > 0.0:
+                continue
+            lim = FRICTION * ln
+            d1 = c["rhs"][1] - c["jdi"][1] * jdv(t1_b, c["a"][1])
+            d2 = c["rhs"][2] - c["jdi"][2] * jdv(t2_b, c["a"][2])
+            s1 = c["lam"][1] + d1
+            s2 = c["lam"][2] + d2
+            m2 = s1 * s1 + s2 * s2
+            if m2 > lim * lim:
+                f = lim / math.sqrt(m2)
+                s1 = s1 * f
+                s2 = s2 * f
+            d1 = s1 - c["lam"][1]
+            d2 = s2 - c["lam"][2]
+            c["lam"][1] = s1
+            c["lam"][2] = s2
+            apply(t1_b, c["a"][1], d1)
+            apply(t2_b, c["a"][2], d2)
+            res = max(res, (d1 + d2) ** 2)
+        if res <= RESIDUAL_THRESHOLD:
+            break
+    return (np.asarray(vel_w, dtype=np.float64) + rot_bw @ dvl,
+            np.asarray(omega_w, dtype=np.float64) + rot_bw @ dva)

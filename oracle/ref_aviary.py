@@ -243,7 +243,9 @@ class RefAviary:
         pos, q_s, vel, omega = multibody_step(self._b_pos[i], self._b_quat[i], self._b_vel[i], self._b_angv[i],
                                               f_base, np.array([tx, ty, z_torque]),
                                               np.array([0.0, 0.0, -p["G"]]) * self.M, self.M,
-                                              np.array([p["ixx"], p["iyy"], p["izz"]]), self.PYB_TIMESTEP)
+                                              np.array([p["ixx"], p["iyy"], p["izz"]]), self.PYB_TIMESTEP,
+                                              cylinder=None if "no_plane" in self.AERO else
+                                              (p["collision_r"], p["collision_h"] / 2, p["collision_z_offset"]))
         self._b_pos[i], self._b_quat[i], self._b_vel[i], self._b_angv[i] = pos, q_s, vel, omega
         self.rpy_rates[i, :] = omega
 

@@ -9,6 +9,16 @@ import numpy as np
 from oracle.ref_aviary import RefAviary
 
 
+# f64 gate for Physics.PYB* runs whose drones touch the ground plane.  Contact events are
+# discontinuous in the state (a speculative row enters the solve at the breaking threshold with
+# a nonzero impulse; the solver stops on a residual threshold), so a rounding-level difference
+# can be amplified: the oracle itself turns a 1e-15 perturbation of integrate_pyb_gnd_drag's
+# start state into 1.1e-9 on one drone within 2.5 s (tests/test_golden.py
+# test_oracle_contact_self_sensitivity_within_gate).  Max over drones and samples <= 1e-7; the
+# median stays at the 1e-10 gate of the contact-free paths.
+TOL_CONTACT = 1e-7
+
+
 def state_rel_err(a, b):
     """Per-drone relative L2 error of the state (SURVEY §8(d) gate): pos, quat, rpy, vel, ang_v -
     columns 0..15 of the 20-float state vector.  q and -q are the same orientation, so the
@@ -68,3 +78,31 @@ def assert_obs_match(gpu, ref, rtol=1e-5, atol=1e-6, err_msg=""):
     assert gpu.shape == ref.shape, (gpu.shape, ref.shape)
     np.testing.assert_array_equal(gpu[..., 12:], ref[..., 12:], err_msg=f"action history {err_msg}")
     np.testing.assert_allclose(gpu[..., :12], ref[..., :12], rtol=rtol, atol=atol, err_msg=err_msg)
+
+
+def oracle_raw(env):
+    """The oracle's physics-client state as a raw [N, 20] array (gpd_get_raw_state layout):
+    pos, stored quat, vel, integrated rate (world rate on the Bullet path), ang_v, last action."""
+    n = env.NUM_DRONES
+    raw = np.zeros((n, 20))
+    raw[:, 0:3] = env._b_pos
+    raw[:, 3:7] = env._b_quat
+    raw[:, 7:10] = env._b_vel
+    raw[:, 10:13] = env._b_angv if env.INTEGRATOR == "bullet" else env.rpy_rates
+    raw[:, 13:16] = env._b_angv
+    raw[:, 16:20] = env.last_clipped_action
+    return raw
+
+
+def resynced_substep_errors(sim, env, rpms):
+    """Local parity of chaotic runs (drones crashing into the plane): before every substep the
+    GPU sim is set to the oracle's state, both take ONE substep on the same RPMs, and the
+    per-drone relative state error of that substep is recorded.  Rounding differences cannot
+    compound, so an identical algorithm agrees to rounding at every substep.  Returns [T, N]."""
+    errs = []
+    for t in range(rpms.shape[0]):
+        sim.set_raw_state(oracle_raw(env))
+        g = sim.integrate(rpms[t:t + 1], record=True).cpu().numpy()
+        r = env.integrate(rpms[t:t + 1])
+        errs.append(state_rel_err(g, r)[0])
+    return np.array(errs)

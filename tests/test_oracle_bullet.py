@@ -3,7 +3,9 @@
 pybullet cannot run in this pipeline, so the restated btMultiBody base step is pinned by closed
 forms: hover equilibrium, damped free fall (recurrence and terminal velocity), the coordinate
 velocity clamp, a damped spin about a principal axis, the exponential map against scipy, the
-prop-placement roll sign, and the world-frame form the GPU kernel evaluates.
+prop-placement roll sign, and the world-frame form the GPU kernel evaluates.  The ground-plane
+contact restatement (``plane_contact``) is pinned by rest / no-force / sliding-friction / tilted
+landing checks.
 """
 import math
 
@@ -12,7 +14,8 @@ import pytest
 from scipy.spatial.transform import Rotation
 
 from oracle.bullet_math import quat_to_mat
-from oracle.bullet_mb import ANG_DAMP, LIN_DAMP, MAX_COORD_VEL, base_quat_update, multibody_step, qconj
+from oracle.bullet_mb import (ANG_DAMP, FRICTION, LIN_DAMP, LINEAR_SLOP, MAX_COORD_VEL, base_quat_update,
+                              breaking_threshold, multibody_step, plane_contact, qconj)
 from oracle.params import derived
 from oracle.ref_aviary import RefAviary
 
@@ -36,8 +39,8 @@ def test_hover_equilibrium():
 def test_damped_free_fall_recurrence_and_terminal_velocity():
     """rpm = 0: vz' = vz + dt (-G - k (1 + |vz|) vz), z' = z + dt vz' (damping K1 = K2 = 0.04)."""
     T = 2400
-    traj = _env().integrate(np.zeros((T, 1, 4)))
-    vz, z = 0.0, 0.1125
+    traj = _env(initial_xyzs=[[0.0, 0.0, 500.0]]).integrate(np.zeros((T, 1, 4)))
+    vz, z = 0.0, 500.0
     ref_v, ref_z = [], []
     for _ in range(T):
         vz = vz + DT * (-P["G"] - LIN_DAMP * (1 + abs(vz)) * vz)
@@ -145,3 +148,76 @@ def test_spatial_form_equals_world_form():
         np.testing.assert_allclose(out[2], v2, rtol=0, atol=1e-13)
         np.testing.assert_allclose(out[3], w2, rtol=0, atol=1e-12)
         np.testing.assert_allclose(out[0], p2, rtol=0, atol=1e-15)
+
+
+# ---------------------------------------------------------------------------- ground-plane contact
+HH = P["collision_h"] / 2
+
+
+def test_contact_zero_rpm_drop_comes_to_rest_on_the_plane():
+    """KAT: zero RPM from the reference's start height (0.1125 m, BaseAviary.py:196) lands and
+    rests with the cylinder's bottom on z = 0 (to the linear slop), level and at rest."""
+    T = 480
+    traj = _env().integrate(np.zeros((T, 1, 4)))
+    z = traj[:, 0, 2]
+    assert z.min() > HH - 2e-3                                 # no tunnelling through the plane
+    assert z[-1] == pytest.approx(HH - LINEAR_SLOP, abs=1e-6)
+    assert np.abs(traj[-1, 0, 10:16]).max() < 1e-5             # at rest (vel, ang_v; PGS leaves ~1e-6 yaw)
+    assert np.abs(traj[-1, 0, 7:9]).max() < 1e-5               # level (roll, pitch)
+
+
+def test_contact_no_force_above_the_plane():
+    """Above the breaking threshold the contact adds nothing: hover / free fall / tumbling flight
+    from 0.5 m are bit-identical with and without the plane for 0.25 s."""
+    rng = np.random.default_rng(5)
+    rpms = HOVER * (1 + 0.05 * rng.uniform(-1, 1, (60, 1, 4)))
+    xyz = [[0.1, -0.2, 0.5]]
+    a = _env(initial_xyzs=xyz).integrate(rpms)
+    b = _env(initial_xyzs=xyz, aero=("no_plane",)).integrate(rpms)
+    np.testing.assert_array_equal(a, b)
+    assert a[:, 0, 2].min() > 0.3
+
+
+def test_contact_breaking_threshold_value():
+    r, h = P["collision_r"] + 0.001, HH + 0.001
+    assert breaking_threshold(P["collision_r"], HH) == pytest.approx(0.02 * math.sqrt(2 * r * r + h * h), rel=1e-15)
+
+
+def test_contact_sliding_friction_stops_the_drone():
+    """A drone resting on the plane with a horizontal velocity slides under Coulomb friction:
+    deceleration mu*G (plus the small multibody damping), stopping distance ~ v^2 / (2 mu G)."""
+    v0 = 0.5
+    env = _env(initial_xyzs=[[0.0, 0.0, HH - LINEAR_SLOP]])
+    env._b_vel[0] = [v0, 0.0, 0.0]
+    traj = env.integrate(np.zeros((120, 1, 4)))
+    x_stop = traj[-1, 0, 0]
+    d_ref = v0 * v0 / (2 * FRICTION * P["G"])
+    assert abs(traj[-1, 0, 10]) < 1e-6
+    assert x_stop == pytest.approx(d_ref, rel=0.1)
+    assert abs(traj[-1, 0, 1]) < 1e-6                        # no sideways drift
+    assert traj[:, 0, 2].min() > HH - 1e-3
+
+
+def test_contact_tilted_landing_settles_flat():
+    """Dropped from 0.1125 m with 0.3 rad roll, the cylinder lands on its rim and settles on its
+    bottom cap (level, at rest, bottom on the plane)."""
+    traj = _env(initial_rpys=[[0.3, 0.0, 0.0]]).integrate(np.zeros((720, 1, 4)))
+    assert abs(traj[-1, 0, 7]) < 1e-4 and abs(traj[-1, 0, 8]) < 1e-4
+    assert traj[-1, 0, 2] == pytest.approx(HH - LINEAR_SLOP, abs=1e-5)
+    assert np.abs(traj[-1, 0, 10:16]).max() < 1e-4
+
+
+def test_contact_velocity_level_constraints_hold():
+    """After one contact solve on a penetrating resting drone, every active point's normal
+    velocity matches its ERP target (residual threshold) and its normal impulse is >= 0."""
+    rot = quat_to_mat(np.array([0.0, 0.0, 0.0, 1.0]))
+    pos = np.array([0.0, 0.0, HH - 1e-3])                      # 1 mm into the plane
+    v, w = plane_contact(pos, rot, np.array([0.0, 0.0, -0.3]), np.zeros(3), M, INERTIA, DT,
+                         P["collision_r"], HH, 0.0)
+    target = (1e-3 - LINEAR_SLOP) * 0.08 / DT                   # -penetration * erp / dt
+    # every point's normal velocity at its target, to the solver's stopping residual
+    # (sqrt(1e-7) ~ 3e-4 in velocity units)
+    for rx, ry in ((0.06, 0), (0, 0.06), (-0.06, 0), (0, -0.06)):
+        vn = v[2] + (w[0] * ry - w[1] * rx)
+        assert vn == pytest.approx(target, abs=1e-3)
+    assert np.abs(v[:2]).max() < 1e-4
