@@ -533,10 +533,16 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
 template <typename R>
 __device__ __forceinline__ R pc_dot(R ax, R ay, R az, R bx, R by, R bz) { return (ax * bx + ay * by) + az * bz; }
 
+#ifdef GPD_CONTACT_STATS
+// diagnostic build only: per solving wave, the iterations run [0..50] and the active lanes [51..115]
+__device__ unsigned long long g_pc_hist[128];
+#endif
 template <typename R>
 __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const Consts<R>& c, const DynK<R>& k) {
-  // the rows live in LDS (one column per lane of the block's single wave): in registers they
-  // would raise the whole kernel's VGPR count for a path that only landing drones take
+  // The rows' constants (rhs, 1/jacDiag, jacDiag) live in LDS, one column per lane of the
+  // block's single wave; the impulses stay in registers.  Kept in registers with the point loops
+  // unrolled, the 12 rows' Jacobians would be hoisted out of the iteration loop and raise the
+  // whole kernel's VGPR count for a path that only grounded drones take.
   enum { kRhs = 0, kJdi = 3, kJdn = 6, kLam = 7, kPer = 10 };
   __shared__ R pc[4 * kPer][64];
   const int ln = threadIdx.x;
@@ -587,23 +593,27 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
   const R zc_ = zc, cr_ = cr;
   R dl0 = R(0), dl1 = R(0), dl2 = R(0), da0 = R(0), da1 = R(0), da2 = R(0);
   bool done = !any;
+#ifdef GPD_CONTACT_STATS
+  int it_used = 0;
+  const unsigned long long nact = __ballot(any);
+#endif
   for (int it = 0; it < c.iters; ++it) {
     if (__ballot(!done) == 0ull) break;
+#ifdef GPD_CONTACT_STATS
+    it_used = it + 1;
+#endif
     if (!done) {
-      // opaque per iteration, and the point loops kept rolled: keeps the compiler from hoisting
-      // the 24 loop-invariant row Jacobians (and their M^-1 products) into registers, which
-      // would raise the whole kernel's VGPR count
+      // opaque per iteration: the row Jacobians are recomputed, not hoisted (see above)
       const R nx = vpin(nx_), ny = vpin(ny_), nz = vpin(nz_), ux = vpin(ux_), uy = vpin(uy_), uz = vpin(uz_);
-      const R ex = vpin(ex_), ey = vpin(ey_), ez = vpin(ez_), zc = vpin(zc_);
-      const R cr = vpin(cr_);
+      const R ex = vpin(ex_), ey = vpin(ey_), ez = vpin(ez_), zc = vpin(zc_), cr = vpin(cr_);
       R res = R(0);
-#pragma unroll 1
+#pragma unroll
       for (int p = 0; p < 4; ++p) {                  // normal rows
         const R rx = p == 0 ? cr : (p == 2 ? -cr : R(0)), ry = p == 1 ? cr : (p == 3 ? -cr : R(0));
         const R ax = ry * nz - zc * ny, ay = zc * nx - rx * nz, az = rx * ny - ry * nx;
         const R jv = pc_dot(nx, ny, nz, dl0, dl1, dl2) + pc_dot(ax, ay, az, da0, da1, da2);
-        const R lam = pc[p * kPer + kLam][ln];
         R delta = pc[p * kPer + kRhs][ln] - pc[p * kPer + kJdi][ln] * jv;
+        const R lam = pc[p * kPer + kLam][ln];
         const R sum = lam + delta;
         const bool neg = sum < R(0);
         delta = neg ? -lam : delta;
@@ -614,7 +624,7 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
         const R rr = delta * pc[p * kPer + kJdn][ln];
         res = rr * rr > res ? rr * rr : res;
       }
-#pragma unroll 1
+#pragma unroll
       for (int p = 0; p < 4; ++p) {                  // friction pairs on the cone
         const R rx = p == 0 ? cr : (p == 2 ? -cr : R(0)), ry = p == 1 ? cr : (p == 3 ? -cr : R(0));
         const R bx = ry * uz - zc * uy, by = zc * ux - rx * uz, bz = rx * uy - ry * ux;
@@ -648,6 +658,12 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
       done = res <= c.resid;
     }
   }
+#ifdef GPD_CONTACT_STATS
+  if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) {
+    atomicAdd(&g_pc_hist[it_used], 1ull);
+    atomicAdd(&g_pc_hist[51 + __popcll(nact)], 1ull);
+  }
+#endif
   // back to world coordinates (rows of Rm: world = Rm . base); lanes without an active point
   // keep their velocities bit for bit, signed zeros included
   s.vx = any ? s.vx + pc_dot(Rm[0], Rm[1], Rm[2], dl0, dl1, dl2) : s.vx;

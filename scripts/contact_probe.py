@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Step time of the Physics.PYB kernels with and without ground contact (4096 HoverAviary envs, f64).
+
+Cases: 'crash' = U[-1,1] RPM actions (many drones end up on the plane, as in bench.py's PYB row),
+'rest' = zero actions of thrust 0.8 hover (every drone resting on the plane after ~0.3 s),
+'fly' = hover actions (no contact), 'noplane' = U[-1,1] with the plane off.  Prints one line
+per case: mean us/step over a timed region of replayed steps and the fraction of low drones.
+Select the library with GPD_LIB (A/B builds)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gym_pybullet_drones_routing_amd.enums import ActionType, Physics  # noqa: E402
+from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim  # noqa: E402
+
+
+def run(case, E=4096, warm=60, steps=200):
+    aero = ("no_plane",) if case == "noplane" else ()
+    sim = BatchedAviarySim(n_envs=E, act=ActionType.RPM, physics=Physics.PYB, aero=aero, device="cuda:0")
+    g = torch.Generator(device="cuda:0").manual_seed(0)
+    n = warm + steps
+    if case in ("crash", "noplane"):
+        acts = torch.rand((n, E, 1, 4), generator=g, device="cuda:0", dtype=torch.float32) * 2 - 1
+    elif case == "rest":
+        acts = torch.full((n, E, 1, 4), -1.0, device="cuda:0")      # 0.95 hover RPM: sinks and rests
+    else:
+        acts = torch.zeros((n, E, 1, 4), device="cuda:0")
+    for t in range(warm):
+        sim.step(acts[t])
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for t in range(warm, n):
+        sim.step(acts[t])
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1000 / steps
+    z = sim.state20()[:, 2]
+    lowf = float((z < 0.02).double().mean())
+    print(f"{case:8s} {us:9.2f} us/step  low drones {lowf:.3f}", flush=True)
+    lib = sim._lib
+    if hasattr(lib, "gpd_debug_contact_hist"):       # -DGPD_CONTACT_STATS build
+        h = (ctypes.c_ulonglong * 128)()
+        lib.gpd_debug_contact_hist(h)
+        it = np.array(h[:51])
+        la = np.array(h[51:116])
+        if it.sum():
+            print(f"   solves {it.sum()}  iterations: mean {np.dot(np.arange(51), it) / it.sum():.2f} "
+                  f"hist {dict((i, int(v)) for i, v in enumerate(it) if v)}  active lanes mean "
+                  f"{np.dot(np.arange(65), la) / la.sum():.1f}", flush=True)
+    sim.close()
+
+
+if __name__ == "__main__":
+    for case in (sys.argv[1:] or ["fly", "noplane", "crash", "rest"]):
+        run(case)
