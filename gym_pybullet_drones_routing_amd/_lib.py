@@ -22,7 +22,7 @@ GPD_EUNSUPPORTED = -4
 
 GPD_MODEL_CF2X, GPD_MODEL_CF2P, GPD_MODEL_RACE = 0, 1, 2
 GPD_ACT_RPM, GPD_ACT_ONE_D_RPM, GPD_ACT_PID, GPD_ACT_VEL, GPD_ACT_ONE_D_PID = 0, 1, 2, 3, 4
-GPD_ABI_VERSION = 4
+GPD_ABI_VERSION = 5
 CTRL_COMPS = 9  # integral_pos_e(3) integral_rpy_e(3) last_rpy(3)
 GPD_TASK_NONE, GPD_TASK_HOVER, GPD_TASK_MULTIHOVER = 0, 1, 2
 GPD_F_GND, GPD_F_DRAG, GPD_F_DW, GPD_F_GEOM_WRENCH, GPD_F_BULLET, GPD_F_NO_PLANE = 1, 2, 4, 8, 16, 32
@@ -33,7 +33,8 @@ EXPORTED = ("gpd_abi_version", "gpd_last_error", "gpd_default_params", "gpd_crea
             "gpd_get_constants", "gpd_reset", "gpd_step", "gpd_step_seq", "gpd_integrate", "gpd_get_state20",
             "gpd_get_raw_state", "gpd_set_raw_state", "gpd_get_step_counters",
             "gpd_set_step_counters", "gpd_state_bytes", "gpd_save_state", "gpd_load_state",
-            "gpd_default_pid_params", "gpd_set_pid_params", "gpd_get_ctrl_state", "gpd_set_ctrl_state")
+            "gpd_default_pid_params", "gpd_set_pid_params", "gpd_get_ctrl_state", "gpd_set_ctrl_state",
+            "gpd_nonfinite")
 
 
 class GpdLibraryError(RuntimeError):
@@ -118,6 +119,7 @@ def load():
         "gpd_set_pid_params": (ci, [vp, ctypes.POINTER(PidParams)]),
         "gpd_get_ctrl_state": (ci, [vp, vp, vp]),
         "gpd_set_ctrl_state": (ci, [vp, vp, vp]),
+        "gpd_nonfinite": (ci, [vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name) and os.environ.get("GPD_ALLOW_ABI_MISMATCH"):

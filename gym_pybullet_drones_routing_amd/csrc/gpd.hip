@@ -352,6 +352,15 @@ int launch_state20(gpd_sim* s, void* out, int raw, hipStream_t st) {
 }
 
 template <typename R>
+int launch_nonfinite(gpd_sim* s, uint8_t* flags, hipStream_t st) {
+  const SimView<R> v = make_view<R>(s);
+  HIP_TRY(hipMemsetAsync(flags, 0, (size_t)s->E, st));
+  hipLaunchKernelGGL((nonfinite_kernel<R>), dim3(grid_for(s->N, 256)), dim3(256), 0, st, v, flags);
+  HIP_TRY(hipGetLastError());
+  return GPD_OK;
+}
+
+template <typename R>
 int launch_set_raw(gpd_sim* s, const void* in, hipStream_t st) {
   const SimView<R> v = make_view<R>(s);
   hipLaunchKernelGGL((set_raw_kernel<R>), dim3(grid_for(s->N, 256)), dim3(256), 0, st, v, (const R*)in);
@@ -696,6 +705,12 @@ int gpd_get_raw_state(gpd_sim* sim, void* out, void* stream) {
   if (!sim || !out) return fail(GPD_EINVAL, "gpd_get_raw_state: NULL argument");
   hipStream_t st = (hipStream_t)stream;
   return sim->prec == GPD_F64 ? launch_state20<double>(sim, out, 1, st) : launch_state20<float>(sim, out, 1, st);
+}
+
+int gpd_nonfinite(gpd_sim* sim, uint8_t* env_flags, void* stream) {
+  if (!sim || !env_flags) return fail(GPD_EINVAL, "gpd_nonfinite: NULL argument");
+  hipStream_t st = (hipStream_t)stream;
+  return sim->prec == GPD_F64 ? launch_nonfinite<double>(sim, env_flags, st) : launch_nonfinite<float>(sim, env_flags, st);
 }
 
 int gpd_set_raw_state(gpd_sim* sim, const void* in, void* stream) {

@@ -1132,6 +1132,20 @@ __global__ __launch_bounds__(256) void state20_kernel(SimView<R> v, R* __restric
   o[16] = last[0]; o[17] = last[1]; o[18] = last[2]; o[19] = last[3];
 }
 
+// Per-env non-finite guard: flag[e] = 1 when any drone of env e holds a
+// non-finite integrated state component (pos, stored quat, vel, rates, ang_v), e.g. after the
+// downwash quotient's beta = 0 edge (BaseAviary.py:802-804).  flag is zeroed by the caller;
+// several drones of one env may store the same 1.
+template <typename R>
+__global__ __launch_bounds__(256) void nonfinite_kernel(SimView<R> v, uint8_t* __restrict__ flag) {
+  const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= v.N) return;
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) bad = bad || !isfinite(v.state[tidx(n, k, kStateComps)]);
+  if (bad) flag[n / v.D] = 1;
+}
+
 template <typename R>
 __global__ __launch_bounds__(256) void set_raw_kernel(SimView<R> v, const R* __restrict__ in) {
   const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;

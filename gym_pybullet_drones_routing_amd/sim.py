@@ -288,6 +288,14 @@ class BatchedAviarySim:
             self._call("gpd_get_state20", _ptr(out), _stream(self.device))
         return out
 
+    def nonfinite(self):
+        """Per-env non-finite guard (the reference has none): bool [E] on the device,
+        True where any drone of the env holds a non-finite state component."""
+        out = torch.empty((self.n_envs,), dtype=torch.uint8, device=self.device)
+        with torch.cuda.device(self.device):
+            self._call("gpd_nonfinite", _ptr(out), _stream(self.device))
+        return out.bool()
+
     def raw_state(self):
         out = torch.empty((self.n_drones, 20), dtype=self.real_dtype, device=self.device)
         with torch.cuda.device(self.device):

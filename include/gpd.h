@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define GPD_ABI_VERSION 4
+#define GPD_ABI_VERSION 5
 
 /* return codes */
 #define GPD_OK 0
@@ -199,6 +199,11 @@ int gpd_get_state20(gpd_sim* sim, void* out, void* stream);
  * seed arbitrary initial conditions. */
 int gpd_get_raw_state(gpd_sim* sim, void* out, void* stream);
 int gpd_set_raw_state(gpd_sim* sim, const void* in, void* stream);
+/* Per-env non-finite guard (new, the reference has none): env_flags [E] uint8
+ * (device memory) = 1 where any drone of the env holds a non-finite pos / quat / vel / rate /
+ * ang_v component (e.g. the downwash quotient at beta = 0, BaseAviary.py:802-804), else 0.
+ * Asynchronous on `stream`; the step path itself never tests for it. */
+int gpd_nonfinite(gpd_sim* sim, uint8_t* env_flags, void* stream);
 /* PID action types: replace the controller coefficients of every drone (setPIDCoefficients).
  * Synchronous (uploads the constant block). */
 int gpd_set_pid_params(gpd_sim* sim, const gpd_pid_params* params);

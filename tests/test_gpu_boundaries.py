@@ -132,3 +132,29 @@ def test_downwash_cull_at_10(dxy, active):
         assert abs(vz) < 1e-12, vz
     assert state_rel_err(traj, rtraj).max() <= 1e-10
     sim.close()
+
+
+def test_nonfinite_guard_flags_only_the_poisoned_env():
+    """gpd_nonfinite: a NaN seeded into one drone of env 2 (as the downwash quotient
+    at beta = 0 would produce, BaseAviary.py:802-804) flags env 2 only, before and after a step;
+    the other envs step on unaffected."""
+    from gym_pybullet_drones_routing_amd.enums import ActionType
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+    E, D = 6, 2
+    sim = BatchedAviarySim(n_envs=E, drones_per_env=D, task="multihover", act=ActionType.RPM, device="cuda:0")
+    assert not sim.nonfinite().any()
+    raw = sim.raw_state().cpu().numpy()
+    raw[2 * D + 1, 8] = np.nan
+    sim.set_raw_state(raw)
+    assert sim.nonfinite().cpu().numpy().tolist() == [False, False, True, False, False, False]
+    ref = BatchedAviarySim(n_envs=E, drones_per_env=D, task="multihover", act=ActionType.RPM, device="cuda:0")
+    acts = torch.zeros((E, D, 4), device="cuda:0")
+    sim.step(acts)
+    ref.step(acts)
+    assert sim.nonfinite().cpu().numpy().tolist() == [False, False, True, False, False, False]
+    a, b = sim.state20().cpu().numpy(), ref.state20().cpu().numpy()
+    keep = np.ones(E * D, bool)
+    keep[2 * D:3 * D] = False
+    np.testing.assert_array_equal(a[keep], b[keep])
+    sim.close()
+    ref.close()

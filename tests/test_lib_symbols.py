@@ -39,7 +39,8 @@ def test_every_declared_symbol_is_exported(lib):
 
 def test_host_only_entry_points(lib):
     from gym_pybullet_drones_routing_amd import _lib
-    assert lib.gpd_abi_version() == _lib.GPD_ABI_VERSION == 4
+    assert lib.gpd_abi_version() == _lib.GPD_ABI_VERSION == 5
+    assert lib.gpd_nonfinite(None, None, None) == _lib.GPD_EINVAL
     q = _lib.PidParams()
     assert lib.gpd_default_pid_params(ctypes.byref(q)) == _lib.GPD_OK
     assert list(q.p_coeff_tor) == [70000., 70000., 60000.] and q.pwm2rpm_const == 4070.3
