@@ -117,6 +117,7 @@ struct gpd_sim {
   int wt = 0;                     // SimView::wt (write-through store policy)
   int nc_magic = 0;               // SimView::nc_magic
   bool duo = false;               // step launches step_kernel_duo (two or three waves per block)
+  bool wide = false;              // D > 64: step_kernel_wide / integrate_kernel_wide, one env per workgroup
   int step_waves = 1;             // waves per step block (1, 2, or 3 with the io wave)
   DwPairs dw_pairs{0, 0};         // SimView::dw_pairs
   double bound_xy;
@@ -293,6 +294,21 @@ inline unsigned grid_for(long long n, int tpb) { return (unsigned)((n + tpb - 1)
 inline size_t real_size(const gpd_sim* s) { return s->prec == GPD_F64 ? sizeof(double) : sizeof(float); }
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+template <typename R, int MAXT>
+const void* step_wide_fn(int act) {
+  switch (act) {
+    case GPD_ACT_RPM: return (const void*)step_kernel_wide<R, ACT_RPM, MAXT>;
+    case GPD_ACT_ONE_D_RPM: return (const void*)step_kernel_wide<R, ACT_ONE_D_RPM, MAXT>;
+    case GPD_ACT_PID: return (const void*)step_kernel_wide<R, ACT_PID, MAXT>;
+    case GPD_ACT_VEL: return (const void*)step_kernel_wide<R, ACT_VEL, MAXT>;
+    default: return (const void*)step_kernel_wide<R, ACT_ONE_D_PID, MAXT>;
+  }
+}
+template <typename R, int MAXT>
+const void* integrate_wide_fn(bool traj) {
+  return traj ? (const void*)integrate_kernel_wide<R, true, MAXT> : (const void*)integrate_kernel_wide<R, false, MAXT>;
+}
+
 template <typename R>
 int launch_step(gpd_sim* s, const float* actions, float* obs, float* reward, uint8_t* term, uint8_t* trunc,
                 float* terminal_obs, hipStream_t st) {
@@ -301,6 +317,13 @@ int launch_step(gpd_sim* s, const float* actions, float* obs, float* reward, uin
   io.terminal_obs = terminal_obs;
   const SimView<R> v = make_view<R>(s);
   const Consts<R>* c = (const Consts<R>*)s->d_consts;
+  if (s->wide) {
+    const void* f = s->D <= 256 ? step_wide_fn<R, 256>(s->cfg.act_type)
+                    : (s->D <= 512 ? step_wide_fn<R, 512>(s->cfg.act_type) : step_wide_fn<R, 1024>(s->cfg.act_type));
+    void* args[] = {(void*)&v, (void*)&io, (void*)&c};
+    HIP_TRY(hipLaunchKernel(f, dim3(s->E), dim3((s->D + kWave - 1) / kWave * kWave), args, 0, st));
+    return GPD_OK;
+  }
   const unsigned grid = grid_for(s->N, s->tpb);
   const size_t lds = (size_t)s->tile_bytes;
   typedef void (*StepFn)(R*, const float*, int2*, const Consts<R>*, long long, int, int, SimView<R>, StepIO<R>);
@@ -320,6 +343,13 @@ int launch_integrate(gpd_sim* s, const void* rpm, int n_sub, void* traj, hipStre
   const bool plain = s->cfg.physics_flags == 0;
   const R* r = (const R*)rpm;
   R* tr = (R*)traj;
+  if (s->wide) {
+    const void* fw = s->D <= 256 ? integrate_wide_fn<R, 256>(tr != nullptr)
+                     : (s->D <= 512 ? integrate_wide_fn<R, 512>(tr != nullptr) : integrate_wide_fn<R, 1024>(tr != nullptr));
+    void* args[] = {(void*)&v, (void*)&c, (void*)&r, (void*)&n_sub, (void*)&tr};
+    HIP_TRY(hipLaunchKernel(fw, dim3(s->E), dim3((s->D + kWave - 1) / kWave * kWave), args, 0, st));
+    return GPD_OK;
+  }
   const void* f;
   if (tr) {
     f = s->D > 1 ? (const void*)integrate_kernel<R, true, kPfRuntime, true>
@@ -428,8 +458,8 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   *out = nullptr;
   const gpd_config& C = *cfg;
   if (C.n_envs < 1) return fail(GPD_EINVAL, "gpd_create: n_envs must be >= 1");
-  if (C.drones_per_env < 1 || C.drones_per_env > kWave)
-    return fail(GPD_EINVAL, "gpd_create: drones_per_env must be in [1, 64]");
+  if (C.drones_per_env < 1 || C.drones_per_env > kWideMax)
+    return fail(GPD_EINVAL, "gpd_create: drones_per_env must be in [1, 1024]");
   if (C.pyb_freq < 1 || C.ctrl_freq < 1) return fail(GPD_EINVAL, "gpd_create: frequencies must be >= 1");
   if (C.pyb_freq % C.ctrl_freq != 0)
     return fail(GPD_EINVAL, "[ERROR] in BaseAviary.__init__(), pyb_freq is not divisible by env_freq.");
@@ -483,6 +513,9 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     want = std::max(s->D, (want / s->D) * s->D);
     if (C.drones_per_block > 0) want = std::max(s->D, std::min(full, (C.drones_per_block / s->D) * s->D));
     s->tpb = want;
+    // envs of more than 64 drones: one env per multi-wave workgroup (step_kernel_wide)
+    s->wide = s->D > kWave;
+    if (s->wide) s->tpb = s->D;
   }
   s->npad = ((long long)s->N + 63) / 64 * 64;
   {

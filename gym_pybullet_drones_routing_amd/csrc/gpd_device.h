@@ -545,7 +545,7 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
   // whole kernel's VGPR count for a path that only grounded drones take.
   enum { kRhs = 0, kJdi = 3, kJdn = 6, kLam = 7, kPer = 10 };
   __shared__ R pc[4 * kPer][64];
-  const int ln = threadIdx.x;
+  const int ln = threadIdx.x & 63;
   const R nx = Rm[6], ny = Rm[7], nz = Rm[8];          // base-frame world +z
   const R ux = -Rm[3], uy = -Rm[4], uz = -Rm[5];       // (0,-1,0)
   const R ex = Rm[0], ey = Rm[1], ez = Rm[2];          // (1,0,0)
@@ -701,7 +701,7 @@ __device__ __forceinline__ R contact_low(const Drone<R>& s, const R Rm[9], const
 // The exponential map's half angle is clamped at pi/8 < 0.5, so the cos / sinc series always
 // applies (a select, no branch; below Bullet's f < 0.001 Taylor switch the series agrees with
 // Bullet's two-term expansion to ~1e-30).
-template <typename R, int PF, bool ANGV>
+template <typename R, int PF, bool ANGV, int CW = 1>
 __device__ __forceinline__ void bullet_substep(Drone<R>& s, const R rpm[4], const R W[4], const R last[4], R dwsum,
                                                R q0[4], R d, const Consts<R>& c, const DynK<R>& k) {
   R inv, Rm[9];
@@ -748,7 +748,17 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, const R rpm[4], cons
   // gate conservative against the candidates' own rounding
   if (!pf_on<PF>(k.flags, F_NO_PLANE)) {
     const bool low = contact_low(s, Rm, c) < c.brk + R(1e-6);
-    if (GPD_RARE(__ballot(low) != 0ull)) plane_contact<R>(s, Rm, c, k);
+    if (CW == 1) {
+      if (GPD_RARE(__ballot(low) != 0ull)) plane_contact<R>(s, Rm, c, k);
+    } else {
+      // multi-wave workgroups (envs of more than 64 drones, step_kernel_wide): the LDS rows hold
+      // one wave's lanes, so the waves take turns (the whole workgroup runs this code)
+      const int wv = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+      for (int w = 0; w < nw; ++w) {
+        if (wv == w && __ballot(low) != 0ull) plane_contact<R>(s, Rm, c, k);
+        __syncthreads();
+      }
+    }
   }
   s.px = s.px + k.dt * s.vx;
   s.py = s.py + k.dt * s.vy;
@@ -788,7 +798,7 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, const R rpm[4], cons
 // written before the readback and the two dependency chains interleave.  Lanes with
 // |theta| >= 0.5 (|omega| >= 240 rad/s at 240 Hz: library sin/cos) are redone in a
 // wave-uniform branch at the end.
-template <typename R, int PF, bool ANGV = true>
+template <typename R, int PF, bool ANGV = true, int CW = 1>
 __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R W[4], const R last[4], R dwsum,
                                             const Consts<R>& c, const DynK<R>& k) {
   R q0[4] = {s.qx, s.qy, s.qz, s.qw};
@@ -808,7 +818,7 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R
     }
   }
   if (pf_on<PF>(k.flags, F_BULLET)) {
-    bullet_substep<R, PF, ANGV>(s, rpm, W, last, dwsum, q0, d, c, k);
+    bullet_substep<R, PF, ANGV, CW>(s, rpm, W, last, dwsum, q0, d, c, k);
     return;
   }
   R inv, Rm[9];

@@ -1006,6 +1006,209 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
 }
 
 // ---------------------------------------------------------------------------------------
+// Envs of more than 64 drones (MultiHoverAviary(num_drones=D), D <= kWideMax): one env per
+// workgroup of ceil(D/64) waves.  The per-substep position exchange of _downwash
+// (BaseAviary.py:785-811, O(D^2)) and the env's reward / done reductions go through LDS with
+// workgroup barriers; lanes d >= D compute on drone 0 of the env and store nothing.  Physics
+// flags are tested at run time; observation rows are stored straight from registers (history
+// columns read from the ring), without the LDS tile of the one-wave kernels.  Same operations
+// and order as step_kernel / integrate_kernel (tests/test_gpu_wide.py).
+constexpr int kWideMax = 1024;
+
+template <typename R>
+__device__ __forceinline__ R wide_downwash(const Drone<R>& s, R* sx, R* sy, R* sz, int d, int D,
+                                           const Consts<R>& c, int flags) {
+  R dw = R(0);
+  if (flags & F_DW) {
+    __syncthreads();                       // previous readers of sx/sy/sz are done
+    if (d < D) { sx[d] = s.px; sy[d] = s.py; sz[d] = s.pz; }
+    __syncthreads();
+    dw = downwash_sum(s.px, s.py, s.pz, sx, sy, sz, 0, D, c);
+  }
+  return dw;
+}
+
+// MAXT: the workgroup size bound the instantiation is compiled for (256 / 512 / 1024 threads:
+// the register budget per lane halves with each doubling, 1024 spills to scratch).
+template <typename R, int ACT, int MAXT>
+__global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R> io, const Consts<R>* __restrict__ cp) {
+  constexpr int A = act_width(ACT);
+  __shared__ R sx[MAXT], sy[MAXT], sz[MAXT];
+  __shared__ int sflag[MAXT];
+  const Consts<R>& c = *cp;
+  const int D = v.D;
+  const int d = threadIdx.x;
+  const bool active = d < D;
+  const long long e = blockIdx.x;
+  const long long n = e * D + (active ? d : 0);
+  const bool drag = (c.flags & F_DRAG) != 0;
+  Drone<R> s;
+  R last[4];
+  load_drone(v, n, s, last, drag);
+  const int2 cv = v.ctr[e];
+  const int sc = cv.x, head = cv.y;
+  float a[A];
+#pragma unroll
+  for (int j = 0; j < A; ++j) a[j] = io.actions[n * A + j];
+  const DynK<R> dk = dyn_consts(c);
+  R rpm[4];
+  R cs[9];
+  if (!act_is_pid(ACT)) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) rpm[k] = (R)action_to_rpm(dk.hover_f32, a[A == 4 ? k : 0]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) cs[k] = v.ctrl[tidx(n, k, 9)];
+    R qn[4], Rm[9], rpy[3];
+    readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
+    quat_to_euler(qn, rpy[0], rpy[1], rpy[2]);
+    const R pos[3] = {s.px, s.py, s.pz}, vel[3] = {s.vx, s.vy, s.vz};
+    R tpos[3], tvel[3], tyaw;
+    pid_targets<R, ACT>(c.pid, a, pos, rpy, tpos, tyaw, tvel);
+    dsl_pid<R, ACT != ACT_VEL>(c.pid, pos, Rm, rpy, vel, tpos, tyaw, tvel, cs, rpm);
+  }
+  R W[4];
+  rpm_wrench<R, kPfRuntime>(rpm, dk, c, W);
+  const int nw = (D + kWave - 1) / kWave;
+  for (int it = 0; it < dk.nsub; ++it) {
+    const R dw = wide_downwash(s, sx, sy, sz, d, D, c, dk.flags);
+    if (nw > 1) dyn_substep<R, kPfRuntime, true, 16>(s, rpm, W, last, dw, c, dk);
+    else dyn_substep<R, kPfRuntime, true, 1>(s, rpm, W, last, dw, c, dk);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
+  }
+  // final readback (:374) -> obs / reward / done
+  R qn[4], Rm[9];
+  readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
+  const AttitudeArgs<R> att = attitude_args(qn);
+  float roll, pitch, yaw;
+  obs_euler_f32(qn, att, roll, pitch, yaw);
+  float reward = -1.0f;
+  bool term = false, trunc = false;
+  if (v.task != TASK_NONE) {
+    const R* tg = v.target + (active ? d : 0) * 3;
+    const R tx = tg[0] - s.px, ty = tg[1] - s.py, tz = tg[2] - s.pz;
+    const R d2 = tx * tx + ty * ty + tz * tz;
+    const R dist = g_sqrt(d2);
+    R r = R(2) - d2 * d2;
+    r = r > R(0) ? r : R(0);
+    const bool oob = g_abs(s.px) > v.bound_xy || g_abs(s.py) > v.bound_xy || s.pz > R(2) ||
+                     tilted_beyond(att, R(0.38941834230865049), R(0.42279321873816178));  // sin/tan(0.4)
+    __syncthreads();
+    if (active) { sx[d] = r; sy[d] = dist; sflag[d] = oob ? 1 : 0; }
+    __syncthreads();
+    if (d == 0) {   // MultiHoverAviary: the summed reward / distance in the reference's order
+      R rs = R(0), ds = R(0);
+      int anyo = 0;
+      for (int j = 0; j < D; ++j) { rs += sx[j]; ds += sy[j]; anyo |= sflag[j]; }
+      sflag[0] = (ds < R(1e-4) ? 1 : 0) | ((anyo != 0 || sc >= v.trunc_sc) ? 2 : 0);
+      sx[0] = rs;
+    }
+    __syncthreads();
+    const int fl = sflag[0];
+    term = fl & 1;
+    trunc = (fl >> 1) & 1;
+    reward = (float)sx[0];
+  }
+  const bool done = term || trunc;
+  const bool do_reset = done && v.autoreset;
+  float row12[12] = {(float)s.px, (float)s.py, (float)s.pz, roll, pitch, yaw,
+                     (float)s.vx, (float)s.vy, (float)s.vz, (float)s.ax, (float)s.ay, (float)s.az};
+  if (!active) return;
+  const int L = v.ring_len, Wd = v.W;
+  // history columns: ring slots head+1 .. head+L-1 (oldest first), then the current action
+  // (BaseRLAviary.py:307-319); the same for the terminal row and the (reset) observation
+  float* orow = io.obs + n * Wd;
+  float* trow = (do_reset && io.terminal_obs) ? io.terminal_obs + n * Wd : nullptr;
+  for (int k = 0; k < L - 1; ++k) {
+    int slot = head + 1 + k;
+    slot -= slot >= L ? L : 0;
+    const float* src = v.ring + ridx(n, slot, L, A);
+    for (int j = 0; j < A; ++j) {
+      const float x = src[j];
+      orow[12 + k * A + j] = x;
+      if (trow) trow[12 + k * A + j] = x;
+    }
+  }
+  for (int j = 0; j < A; ++j) {
+    orow[12 + (L - 1) * A + j] = a[j];
+    if (trow) trow[12 + (L - 1) * A + j] = a[j];
+  }
+  float* ring_cur = v.ring + ridx(n, head, L, A);     // deque.append (slot head is not read above)
+  for (int j = 0; j < A; ++j) ring_cur[j] = a[j];
+  if (do_reset) {
+    if (trow)
+      for (int k = 0; k < 12; ++k) trow[k] = row12[k];
+    const R* ini = v.init + d * 10;
+    s.px = ini[0]; s.py = ini[1]; s.pz = ini[2];
+    s.qx = ini[3]; s.qy = ini[4]; s.qz = ini[5]; s.qw = ini[6];
+    s.vx = s.vy = s.vz = R(0);
+    s.wx = s.wy = s.wz = R(0);
+    s.ax = s.ay = s.az = R(0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) last[k] = R(0);
+    row12[0] = (float)ini[0]; row12[1] = (float)ini[1]; row12[2] = (float)ini[2];
+    row12[3] = (float)ini[7]; row12[4] = (float)ini[8]; row12[5] = (float)ini[9];
+    for (int k = 6; k < 12; ++k) row12[k] = 0.0f;
+  }
+  for (int k = 0; k < 12; ++k) orow[k] = row12[k];
+  store_drone(v, n, s, last);
+  if (act_is_pid(ACT)) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) v.ctrl[tidx(n, k, 9)] = cs[k];
+  }
+  if (d == 0) {
+    io.reward[e] = reward;
+    io.term[e] = term ? 1 : 0;
+    io.trunc[e] = trunc ? 1 : 0;
+    v.ctr[e] = make_int2(do_reset ? 0 : sc + dk.nsub, head + 1 == L ? 0 : head + 1);
+  }
+}
+
+// gpd_integrate for envs of more than 64 drones (see step_kernel_wide).
+template <typename R, bool TRAJ, int MAXT>
+__global__ __launch_bounds__(MAXT) void integrate_kernel_wide(SimView<R> v, const Consts<R>* __restrict__ cp,
+                                                              const R* __restrict__ rpm_in, int n_sub,
+                                                              R* __restrict__ traj) {
+  __shared__ R sx[MAXT], sy[MAXT], sz[MAXT];
+  const Consts<R>& c = *cp;
+  const int D = v.D;
+  const int d = threadIdx.x;
+  const bool active = d < D;
+  const long long n = (long long)blockIdx.x * D + (active ? d : 0);
+  Drone<R> s;
+  R last[4];
+  load_drone(v, n, s, last, true);
+  const DynK<R> dk = dyn_consts(c);
+  const int nw = (D + kWave - 1) / kWave;
+  const long long N = v.N;
+  for (int t = 0; t < n_sub; ++t) {
+    const R* src = rpm_in + ((long long)t * N + n) * 4;
+    R rpm[4] = {src[0], src[1], src[2], src[3]};
+    R W[4];
+    rpm_wrench<R, kPfRuntime>(rpm, dk, c, W);
+    const R dw = wide_downwash(s, sx, sy, sz, d, D, c, dk.flags);
+    if (nw > 1) dyn_substep<R, kPfRuntime, true, 16>(s, rpm, W, last, dw, c, dk);
+    else dyn_substep<R, kPfRuntime, true, 1>(s, rpm, W, last, dw, c, dk);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) last[k] = rpm[k];
+    if (TRAJ && active) {
+      R qn[4], Rm[9], roll, pitch, yaw;
+      readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
+      quat_to_euler(qn, roll, pitch, yaw);
+      R* o = traj + ((long long)t * N + n) * 20;
+      o[0] = s.px; o[1] = s.py; o[2] = s.pz;
+      o[3] = qn[0]; o[4] = qn[1]; o[5] = qn[2]; o[6] = qn[3];
+      o[7] = roll; o[8] = pitch; o[9] = yaw;
+      o[10] = s.vx; o[11] = s.vy; o[12] = s.vz;
+      o[13] = s.ax; o[14] = s.ay; o[15] = s.az;
+      o[16] = last[0]; o[17] = last[1]; o[18] = last[2]; o[19] = last[3];
+    }
+  }
+  if (active && n_sub > 0) store_drone(v, n, s, last);
+}
+
+// ---------------------------------------------------------------------------------------
 // gpd_integrate: n_sub raw substeps with explicit per-substep RPMs, each followed by a readback.
 // PF as in step_kernel: 0 (plain DYN, the raw-integrator bench) or kPfRuntime; TRAJ: record the
 // [n_sub][N][20] trajectory.

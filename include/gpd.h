@@ -107,7 +107,7 @@ typedef struct gpd_drone_params {
 
 typedef struct gpd_config {
   int n_envs;                /* E >= 1 */
-  int drones_per_env;        /* D in [1, 64] (HoverAviary: 1) */
+  int drones_per_env;        /* D in [1, 1024] (HoverAviary: 1); D > 64 runs one env per multi-wave workgroup */
   int pyb_freq;              /* PYB_FREQ, default 240 */
   int ctrl_freq;             /* CTRL_FREQ, must divide pyb_freq (HoverAviary default 30) */
   int act_type;              /* GPD_ACT_* */

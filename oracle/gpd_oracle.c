@@ -347,7 +347,8 @@ void orc_step(orc_sim* S, const float* actions, float* obs, float* reward, uint8
 #endif
   for (int e = 0; e < S->E; ++e) {
     const int D = S->D, A = S->A;
-    double rpm[64 * 4], scratch[64 * 20];
+    double* rpm = (double*)malloc(sizeof(double) * 4 * (size_t)D);
+    double* scratch = (double*)malloc(sizeof(double) * 20 * (size_t)D);
     double* env = S->raw + (size_t)e * D * 20;
     for (int d = 0; d < D; ++d) {
       size_t n = (size_t)e * D + d;
@@ -391,6 +392,8 @@ void orc_step(orc_sim* S, const float* actions, float* obs, float* reward, uint8
         obs_row(S, e, d, env + (size_t)d * 20, obs + n * S->W);
       }
     }
+    free(rpm);
+    free(scratch);
   }
 }
 
@@ -401,7 +404,7 @@ void orc_integrate(orc_sim* S, const double* rpm, int T, double* traj, int nthre
 #endif
   for (int e = 0; e < S->E; ++e) {
     const int D = S->D;
-    double scratch[64 * 20];
+    double* scratch = (double*)malloc(sizeof(double) * 20 * (size_t)D);
     double* env = S->raw + (size_t)e * D * 20;
     for (int t = 0; t < T; ++t) {
       env_substep(S, env, rpm + ((size_t)t * S->N + (size_t)e * D) * 4, scratch);
@@ -409,5 +412,6 @@ void orc_integrate(orc_sim* S, const double* rpm, int T, double* traj, int nthre
         for (int d = 0; d < D; ++d)
           state20_row(env + (size_t)d * 20, traj + ((size_t)t * S->N + (size_t)e * D + d) * 20);
     }
+    free(scratch);
   }
 }
