@@ -342,6 +342,59 @@ def time_steps(sim, pool, steps, warmup):
     return wall, 1000.0 * float(np.mean(kern_ms))
 
 
+def launch_floor_us(device, launches=64, reps=20):
+    """Per-launch cost of an EMPTY kernel replayed back to back from a hipGraph (torch's spin
+    kernel with a zero count): the dependent kernel-boundary cost every step launch pays."""
+    sleep = getattr(torch.cuda, "_sleep", None)
+    x = torch.zeros(64, device=device)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(launches):
+            if sleep is not None:
+                sleep(0)
+            else:
+                x.add_(1.0)
+    for _ in range(3):
+        g.replay()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(device)
+    ev0.record()
+    for _ in range(reps):
+        g.replay()
+    ev1.record()
+    torch.cuda.synchronize(device)
+    return 1000.0 * ev0.elapsed_time(ev1) / (launches * reps)
+
+
+def latency_model(device, precision, act, E, kern_us, nsub):
+    """Latency roofline of the bench config (the step is latency-bound at 4096 envs, DESIGN.md
+    §7): step kernel time = launch floor + fixed in-kernel work (state/action loads, final
+    readback + hooks, output rows) + nsub x the substep critical path.  The substep slope comes
+    from the same workload at 1 and 16 substeps per control step (pyb_freq 30 / 480 Hz, ctrl
+    30 Hz); the floor from an empty kernel.  'bound_us' = floor + nsub x slope is the time with
+    zero prologue / epilogue; frac = bound / achieved."""
+    from gym_pybullet_drones_routing_amd.enums import ActionType
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+    A = 4 if act == "rpm" else 1
+    k = {}
+    for pyb in (30, 480):
+        sim = BatchedAviarySim(n_envs=E, task="hover", act=ActionType(act), precision=precision,
+                               pyb_freq=pyb, ctrl_freq=30, device=device)
+        pool = make_pool(E, A, device, seed=5, pool=16)
+        k[pyb] = time_graph(sim, pool, 256, 32)[2]
+        sim.close()
+    slope = (k[480] - k[30]) / 15.0
+    floor = launch_floor_us(device)
+    fixed = k[30] - slope - floor
+    model = floor + fixed + nsub * slope
+    bound = floor + nsub * slope
+    return {"launch_floor_us": floor, "per_substep_us": slope, "fixed_in_kernel_us": fixed,
+            "kernel_us_1_substep": k[30], "kernel_us_16_substeps": k[480], "model_us": model,
+            "achieved_us": kern_us, "bound_us": bound, "frac": bound / kern_us,
+            "note": "kernel time = launch floor + fixed in-kernel work + substeps x substep critical path; "
+                    "bound = floor + substeps x critical path (no prologue / epilogue)"}
+
+
 def other_configs(device, precision, act):
     """BASELINE.json configs 3 and 4 and the controller action types, each timed like the main
     line (hipGraph replays of env.step for every env) - reported beside the metric, not as it."""
@@ -598,6 +651,8 @@ def run(args):
                             "action_bytes_per_step": act_b, "gathered_bytes_per_step": pack_b,
                             "pack_bytes_per_rank": handoff.nbytes}
 
+    if rank == 0 and world == 1:
+        result["roofline"]["latency_model"] = latency_model(device, args.precision, args.act, E, kern_us, nsub)
     if rank == 0 and world == 1 and not args.no_sweep:
         sweep = []
         for e_large in (65536, 1 << 20, 1 << 22):
@@ -613,6 +668,8 @@ def run(args):
             torch.cuda.empty_cache()
         result["sweep"] = sweep
 
+    if rank == 0 and world == 1:
+        result["roofline"]["latency_model"] = latency_model(device, args.precision, args.act, E, kern_us, nsub)
     if rank == 0 and world == 1 and not args.no_sweep:
         import warnings
         with warnings.catch_warnings():

@@ -537,6 +537,16 @@ __device__ __forceinline__ R pc_dot(R ax, R ay, R az, R bx, R by, R bz) { return
 // diagnostic build only: per solving wave, the iterations run [0..50] and the active lanes [51..115]
 __device__ unsigned long long g_pc_hist[128];
 #endif
+// r_p x d for the rim point p (p = 0..3: (cr,0,zc), (0,cr,zc), (-cr,0,zc), (0,-cr,zc)), with the
+// zero components dropped (exact: 0*x - y == -y).
+template <int P, typename R>
+__device__ __forceinline__ void pc_arm(R cr, R zc, R dx, R dy, R dz, R& ax, R& ay, R& az) {
+  if (P == 0) { ax = -(zc * dy); ay = zc * dx - cr * dz; az = cr * dy; }
+  if (P == 1) { ax = cr * dz - zc * dy; ay = zc * dx; az = -(cr * dx); }
+  if (P == 2) { ax = -(zc * dy); ay = zc * dx + cr * dz; az = -(cr * dy); }
+  if (P == 3) { ax = -(cr * dz) - zc * dy; ay = zc * dx; az = cr * dx; }
+}
+
 template <typename R>
 __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const Consts<R>& c, const DynK<R>& k) {
   // The rows' constants (rhs, 1/jacDiag, jacDiag) live in LDS, one column per lane of the
@@ -593,11 +603,13 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
   const R zc_ = zc, cr_ = cr;
   R dl0 = R(0), dl1 = R(0), dl2 = R(0), da0 = R(0), da1 = R(0), da2 = R(0);
   bool done = !any;
+  const R mu = vpin(c.mu), resid = vpin(c.resid);      // once, not a constant-block load per iteration
+  const int iters = c.iters;
 #ifdef GPD_CONTACT_STATS
   int it_used = 0;
   const unsigned long long nact = __ballot(any);
 #endif
-  for (int it = 0; it < c.iters; ++it) {
+  for (int it = 0; it < iters; ++it) {
     if (__ballot(!done) == 0ull) break;
 #ifdef GPD_CONTACT_STATS
     it_used = it + 1;
@@ -609,8 +621,11 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
       R res = R(0);
 #pragma unroll
       for (int p = 0; p < 4; ++p) {                  // normal rows
-        const R rx = p == 0 ? cr : (p == 2 ? -cr : R(0)), ry = p == 1 ? cr : (p == 3 ? -cr : R(0));
-        const R ax = ry * nz - zc * ny, ay = zc * nx - rx * nz, az = rx * ny - ry * nx;
+        R ax, ay, az;
+        if (p == 0) pc_arm<0>(cr, zc, nx, ny, nz, ax, ay, az);
+        if (p == 1) pc_arm<1>(cr, zc, nx, ny, nz, ax, ay, az);
+        if (p == 2) pc_arm<2>(cr, zc, nx, ny, nz, ax, ay, az);
+        if (p == 3) pc_arm<3>(cr, zc, nx, ny, nz, ax, ay, az);
         const R jv = pc_dot(nx, ny, nz, dl0, dl1, dl2) + pc_dot(ax, ay, az, da0, da1, da2);
         R delta = pc[p * kPer + kRhs][ln] - pc[p * kPer + kJdi][ln] * jv;
         const R lam = pc[p * kPer + kLam][ln];
@@ -626,23 +641,26 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
       }
 #pragma unroll
       for (int p = 0; p < 4; ++p) {                  // friction pairs on the cone
-        const R rx = p == 0 ? cr : (p == 2 ? -cr : R(0)), ry = p == 1 ? cr : (p == 3 ? -cr : R(0));
-        const R bx = ry * uz - zc * uy, by = zc * ux - rx * uz, bz = rx * uy - ry * ux;
-        const R cx = ry * ez - zc * ey, cy = zc * ex - rx * ez, cz = rx * ey - ry * ex;
+        R bx, by, bz, cx, cy, cz;
+        if (p == 0) { pc_arm<0>(cr, zc, ux, uy, uz, bx, by, bz); pc_arm<0>(cr, zc, ex, ey, ez, cx, cy, cz); }
+        if (p == 1) { pc_arm<1>(cr, zc, ux, uy, uz, bx, by, bz); pc_arm<1>(cr, zc, ex, ey, ez, cx, cy, cz); }
+        if (p == 2) { pc_arm<2>(cr, zc, ux, uy, uz, bx, by, bz); pc_arm<2>(cr, zc, ex, ey, ez, cx, cy, cz); }
+        if (p == 3) { pc_arm<3>(cr, zc, ux, uy, uz, bx, by, bz); pc_arm<3>(cr, zc, ex, ey, ez, cx, cy, cz); }
         const R lnrm = pc[p * kPer + kLam][ln];
         const bool on = lnrm > R(0);
-        const R lim = c.mu * lnrm;
+        const R lim = mu * lnrm;
         const R l1 = pc[p * kPer + kLam + 1][ln], l2 = pc[p * kPer + kLam + 2][ln];
         const R j1 = pc_dot(ux, uy, uz, dl0, dl1, dl2) + pc_dot(bx, by, bz, da0, da1, da2);
         const R j2 = pc_dot(ex, ey, ez, dl0, dl1, dl2) + pc_dot(cx, cy, cz, da0, da1, da2);
         R s1 = l1 + (pc[p * kPer + kRhs + 1][ln] - pc[p * kPer + kJdi + 1][ln] * j1);
         R s2 = l2 + (pc[p * kPer + kRhs + 2][ln] - pc[p * kPer + kJdi + 2][ln] * j2);
+        // onto the cone: (s1, s2) * lim / |s| when |s| > lim (a select: no branch, and the
+        // Newton-refined rsqrt instead of a square root and a divide; within ~2 ulp of them)
         const R m2 = s1 * s1 + s2 * s2;
-        if (m2 > lim * lim) {
-          const R f = lim / g_sqrt(m2);
-          s1 = s1 * f;
-          s2 = s2 * f;
-        }
+        const bool clip = m2 > lim * lim;
+        const R f = clip ? lim * g_rsqrt(clip ? m2 : R(1)) : R(1);
+        s1 = s1 * f;
+        s2 = s2 * f;
         const R d1 = on ? s1 - l1 : R(0);
         const R d2 = on ? s2 - l2 : R(0);
         pc[p * kPer + kLam + 1][ln] = on ? s1 : l1;
@@ -655,7 +673,7 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
         const R rr = (d1 + d2) * (d1 + d2);
         res = rr > res ? rr : res;
       }
-      done = res <= c.resid;
+      done = res <= resid;
     }
   }
 #ifdef GPD_CONTACT_STATS

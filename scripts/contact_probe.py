@@ -7,6 +7,7 @@ Cases: 'crash' = U[-1,1] RPM actions (many drones end up on the plane, as in ben
 per case: mean us/step over a timed region of replayed steps and the fraction of low drones.
 Select the library with GPD_LIB (A/B builds)."""
 import ctypes
+import math
 import os
 import sys
 
@@ -18,17 +19,26 @@ from gym_pybullet_drones_routing_amd.enums import ActionType, Physics  # noqa: E
 from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim  # noqa: E402
 
 
+STAG = [[0.15 * math.cos(2 * math.pi * i / 8), 0.15 * math.sin(2 * math.pi * i / 8), 0.5 + 0.1 * i] for i in range(8)]
+
+
 def run(case, E=4096, warm=60, steps=200):
     aero = ("no_plane",) if case == "noplane" else ()
-    sim = BatchedAviarySim(n_envs=E, act=ActionType.RPM, physics=Physics.PYB, aero=aero, device="cuda:0")
+    if case == "multi":    # bench.py's PYB_GND_DRAG_DW row: 512 MultiHover envs x 8 drones, staggered
+        E, D = 512, 8
+        sim = BatchedAviarySim(n_envs=E, drones_per_env=D, task="multihover", act=ActionType.RPM,
+                               physics=Physics.PYB_GND_DRAG_DW, initial_xyzs=STAG, device="cuda:0")
+    else:
+        D = 1
+        sim = BatchedAviarySim(n_envs=E, act=ActionType.RPM, physics=Physics.PYB, aero=aero, device="cuda:0")
     g = torch.Generator(device="cuda:0").manual_seed(0)
     n = warm + steps
-    if case in ("crash", "noplane"):
-        acts = torch.rand((n, E, 1, 4), generator=g, device="cuda:0", dtype=torch.float32) * 2 - 1
+    if case in ("crash", "noplane", "multi"):
+        acts = torch.rand((n, E, D, 4), generator=g, device="cuda:0", dtype=torch.float32) * 2 - 1
     elif case == "rest":
-        acts = torch.full((n, E, 1, 4), -1.0, device="cuda:0")      # 0.95 hover RPM: sinks and rests
+        acts = torch.full((n, E, D, 4), -1.0, device="cuda:0")      # 0.95 hover RPM: sinks and rests
     else:
-        acts = torch.zeros((n, E, 1, 4), device="cuda:0")
+        acts = torch.zeros((n, E, D, 4), device="cuda:0")
     for t in range(warm):
         sim.step(acts[t])
     torch.cuda.synchronize()
@@ -56,5 +66,5 @@ def run(case, E=4096, warm=60, steps=200):
 
 
 if __name__ == "__main__":
-    for case in (sys.argv[1:] or ["fly", "noplane", "crash", "rest"]):
+    for case in (sys.argv[1:] or ["fly", "noplane", "crash", "rest", "multi"]):
         run(case)
