@@ -486,6 +486,9 @@ def parse_args(argv=None):
                     help="processes of the all-core CPU baseline (0 = the CPUs this job may use)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
+    ap.add_argument("--no-latency-model", action="store_true",
+                    help="skip the latency-model leg (its 1- and 16-substep launches share the bench kernel's "
+                         "name and grid, so a rocprofv3 trace of the bench kernel leaves it out)")
     ap.add_argument("--mode", default="graph", choices=["native", "graph", "eager"],
                     help="timed region: hipGraph replays (default), a native launch loop (gpd_step_seq), or "
                          "one Python step() call per env.step")
@@ -651,7 +654,7 @@ def run(args):
                             "action_bytes_per_step": act_b, "gathered_bytes_per_step": pack_b,
                             "pack_bytes_per_rank": handoff.nbytes}
 
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.no_latency_model:
         result["roofline"]["latency_model"] = latency_model(device, args.precision, args.act, E, kern_us, nsub)
     if rank == 0 and world == 1 and not args.no_sweep:
         sweep = []
@@ -668,7 +671,7 @@ def run(args):
             torch.cuda.empty_cache()
         result["sweep"] = sweep
 
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.no_latency_model:
         result["roofline"]["latency_model"] = latency_model(device, args.precision, args.act, E, kern_us, nsub)
     if rank == 0 and world == 1 and not args.no_sweep:
         import warnings

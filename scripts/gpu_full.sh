@@ -10,7 +10,7 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
 timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit $?
 # kernel trace of the bench command (bench config only, then with the large-N sweep)
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_bench -o bench --output-format csv -- python3 bench.py --no-cpu-baseline --no-sweep > $OUT/prof_bench_stdout.json 2> $OUT/prof_bench.err || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_bench -o bench --output-format csv -- python3 bench.py --no-cpu-baseline --no-sweep --no-latency-model > $OUT/prof_bench_stdout.json 2> $OUT/prof_bench.err || exit $?
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_sweep -o sweep --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/prof_sweep_stdout.json 2> $OUT/prof_sweep.err || exit $?
 # PMC: FETCH_SIZE and WRITE_SIZE in separate passes (TCC slots), kernel-trace only
 for E in 4096 65536 1048576 4194304; do
