@@ -243,15 +243,46 @@ def state_parity(device, precision, E=256, T=150, seed=0):
             "vs": "C fp64 restatement of BaseAviary.step (oracle/gpd_oracle.c); PyBullet is unavailable"}
 
 
+def _timed_region(device, body):
+    """The contract's timed region: barrier + synchronize, `body()` (K env.step launches),
+    synchronize, and the wall time between.  No HIP events inside it: an event record before the
+    first launch holds the queue for ~3-5 us, a fixed cost that is 4-5 % of a 20-step region
+    (scripts/region_probe.py, profiles/r2/latency/region_*.txt)."""
+    torch.cuda.synchronize(device)
+    if torch.distributed.is_initialized():
+        torch.distributed.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    body()
+    torch.cuda.synchronize(device)
+    wall = time.perf_counter() - t0
+    if torch.distributed.is_initialized():
+        torch.distributed.barrier()
+    return wall
+
+
+def _event_region_us(device, body):
+    """The same launches again, right after the timed region, bracketed by a HIP event pair on
+    the launch stream: (event time / launches) is the step kernel's average duration including
+    the in-graph kernel boundary (an upper bound; rocprofv3 reports the kernel alone)."""
+    stream = torch.cuda.current_stream(device)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(device)
+    ev0.record(stream)
+    body()
+    ev1.record(stream)
+    torch.cuda.synchronize(device)
+    return 1000.0 * ev0.elapsed_time(ev1)
+
+
 def time_graph(sim, pool, steps, warmup, per_graph=256):
     """Timed region in hipGraph mode: one graph = `per_graph` consecutive env.step() launches
     reading distinct pre-filled action slots, plus one graph of the remaining steps % per_graph
     launches, so that exactly `steps` steps are timed.  Before the timed region every captured
     graph is replayed at least once (the first replay of a graph pays its upload to the device),
     then `warmup` further untimed steps run, whatever `warmup` is.
-    A HIP event pair on the launch stream brackets the replays, so (event time / launches) is
-    the step kernel's average duration including the in-graph kernel boundary (an upper bound;
-    rocprofv3 reports the kernel alone).  Returns (wall seconds, steps run, kernel us)."""
+    The kernel duration comes from _event_region_us over a second, identical replay.
+    Returns (wall seconds, steps run, kernel us)."""
     P = pool.shape[0]
     steps = max(1, int(steps))
     per_graph = min(per_graph, steps)
@@ -267,49 +298,29 @@ def time_graph(sim, pool, steps, warmup, per_graph=256):
         graph.replay()
     for k in range(wrem):
         sim.step(pool[k % P])
-    stream = torch.cuda.current_stream(sim.device)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize(sim.device)
-    if torch.distributed.is_initialized():
-        torch.distributed.barrier()
-    torch.cuda.synchronize(sim.device)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(reps):
-        graph.replay()
-    if tail is not None:
-        tail.replay()
-    ev1.record(stream)
-    torch.cuda.synchronize(sim.device)
-    wall = time.perf_counter() - t0
-    if torch.distributed.is_initialized():
-        torch.distributed.barrier()
-    return wall, steps, 1000.0 * ev0.elapsed_time(ev1) / steps
+
+    def body():
+        for _ in range(reps):
+            graph.replay()
+        if tail is not None:
+            tail.replay()
+    wall = _timed_region(sim.device, body)
+    return wall, steps, _event_region_us(sim.device, body) / steps
 
 
 def time_native(sim, pool, steps, warmup):
     """Timed region as ONE gpd_step_seq call: `steps` env.step() launches issued back to back from
     native code (step k reads action slot k % P), no graph.  Its per-region fixed cost is a little
     below a graph replay's, but each launch costs the host ~5-6 us (about one kernel), so at large
-    K it can turn host-bound (scripts/timing_probe.py); reported beside the graph timing.  A HIP
-    event pair on the launch stream brackets the launches.  Returns (wall s, steps, kernel us)."""
+    K it can turn host-bound (scripts/timing_probe.py); reported beside the graph timing.  Kernel
+    duration from _event_region_us over a second, identical call.  Returns (wall s, steps, kernel us)."""
     steps = max(1, int(steps))
     sim.step_seq(pool, max(1, int(warmup)))
-    stream = torch.cuda.current_stream(sim.device)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize(sim.device)
-    if torch.distributed.is_initialized():
-        torch.distributed.barrier()
-    torch.cuda.synchronize(sim.device)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    sim.step_seq(pool, steps)
-    ev1.record(stream)
-    torch.cuda.synchronize(sim.device)
-    wall = time.perf_counter() - t0
-    if torch.distributed.is_initialized():
-        torch.distributed.barrier()
-    return wall, steps, 1000.0 * ev0.elapsed_time(ev1) / steps
+
+    def body():
+        sim.step_seq(pool, steps)
+    wall = _timed_region(sim.device, body)
+    return wall, steps, _event_region_us(sim.device, body) / steps
 
 
 def time_steps(sim, pool, steps, warmup):
@@ -671,8 +682,6 @@ def run(args):
             torch.cuda.empty_cache()
         result["sweep"] = sweep
 
-    if rank == 0 and world == 1 and not args.no_latency_model:
-        result["roofline"]["latency_model"] = latency_model(device, args.precision, args.act, E, kern_us, nsub)
     if rank == 0 and world == 1 and not args.no_sweep:
         import warnings
         with warnings.catch_warnings():
