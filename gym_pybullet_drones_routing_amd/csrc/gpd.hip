@@ -109,7 +109,7 @@ struct gpd_sim {
   void* d_state = nullptr;
   void* d_ctrl = nullptr;         // tiled [npad/64][9][64] DSLPIDControl state (PID action types)
   float* d_ring = nullptr;
-  int2* d_ctr = nullptr;          // [E] {step_counter, ring head}
+  int2* d_ctr = nullptr;          // [E] {step_counter, ring head} + [E].x: last action in the ring
   void* d_init = nullptr;
   void* d_target = nullptr;
   void* d_consts = nullptr;       // Consts<real> in device memory
@@ -309,6 +309,22 @@ const void* integrate_wide_fn(bool traj) {
   return traj ? (const void*)integrate_kernel_wide<R, true, MAXT> : (const void*)integrate_kernel_wide<R, false, MAXT>;
 }
 
+// last_clipped_action back from the ring (store_drone_step) before anything reads or replaces
+// state[16..19]; a no-op launch when no step ran since the last settle
+template <typename R>
+int settle_last(gpd_sim* s, hipStream_t st) {
+  if (!(s->wt & 4)) return GPD_OK;
+  const SimView<R> v = make_view<R>(s);
+  const Consts<R>* c = (const Consts<R>*)s->d_consts;
+  hipLaunchKernelGGL((last_from_ring_kernel<R>), dim3(grid_for(s->N, 256)), dim3(256), 0, st, v, c);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemsetAsync(s->d_ctr + s->E, 0, sizeof(int2), st));
+  return GPD_OK;
+}
+inline int settle_last_any(gpd_sim* s, hipStream_t st) {
+  return s->prec == GPD_F64 ? settle_last<double>(s, st) : settle_last<float>(s, st);
+}
+
 template <typename R>
 int launch_step(gpd_sim* s, const float* actions, float* obs, float* reward, uint8_t* term, uint8_t* trunc,
                 float* terminal_obs, hipStream_t st) {
@@ -336,6 +352,8 @@ int launch_step(gpd_sim* s, const float* actions, float* obs, float* reward, uin
 
 template <typename R>
 int launch_integrate(gpd_sim* s, const void* rpm, int n_sub, void* traj, hipStream_t st) {
+  const int rc = settle_last<R>(s, st);   // the raw substeps read and store last_clipped_action
+  if (rc != GPD_OK) return rc;
   const SimView<R> v = make_view<R>(s);
   const Consts<R>* c = (const Consts<R>*)s->d_consts;
   const unsigned grid = grid_for(s->N, s->tpb);
@@ -375,6 +393,8 @@ int launch_reset(gpd_sim* s, const uint8_t* mask, float* obs, hipStream_t st) {
 
 template <typename R>
 int launch_state20(gpd_sim* s, void* out, int raw, hipStream_t st) {
+  const int rc = settle_last<R>(s, st);
+  if (rc != GPD_OK) return rc;
   const SimView<R> v = make_view<R>(s);
   hipLaunchKernelGGL((state20_kernel<R>), dim3(grid_for(s->N, 256)), dim3(256), 0, st, v, (R*)out, raw);
   HIP_TRY(hipGetLastError());
@@ -392,6 +412,7 @@ int launch_nonfinite(gpd_sim* s, uint8_t* flags, hipStream_t st) {
 
 template <typename R>
 int launch_set_raw(gpd_sim* s, const void* in, hipStream_t st) {
+  if (s->wt & 4) HIP_TRY(hipMemsetAsync(s->d_ctr + s->E, 0, sizeof(int2), st));   // all 20 replaced
   const SimView<R> v = make_view<R>(s);
   hipLaunchKernelGGL((set_raw_kernel<R>), dim3(grid_for(s->N, 256)), dim3(256), 0, st, v, (const R*)in);
   HIP_TRY(hipGetLastError());
@@ -536,6 +557,10 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     s->wt = C.store_policy > 0 ? ((C.store_policy - 1) & 3) : 3;
     const size_t state_bytes = (size_t)kStateComps * s->npad * (C.precision == GPD_F64 ? 8 : 4);
     if (state_bytes >= 0x7fffffffULL) s->wt &= ~2;
+    // bit 2: the step kernels leave last_clipped_action in the ring (store_drone_step) where
+    // the step never reads it back: RPM action types (the ring holds the very actions it maps),
+    // no drag (the only reader, on the first substep)
+    if ((C.act_type == GPD_ACT_RPM || C.act_type == GPD_ACT_ONE_D_RPM) && !(C.physics_flags & GPD_F_DRAG)) s->wt |= 4;
   }
   s->bound_xy = C.task == GPD_TASK_MULTIHOVER ? 2.0 : 1.5;
   s->tile_bytes = step_tile_bytes(s->A, s->ring_len);
@@ -640,7 +665,7 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   const size_t rs = real_size(s);
   hipError_t e1 = hipMalloc(&s->d_state, (size_t)kStateComps * s->npad * rs);
   hipError_t e2 = hipMalloc((void**)&s->d_ring, (size_t)s->ring_len * s->npad * s->A * sizeof(float));
-  hipError_t e3 = hipMalloc((void**)&s->d_ctr, (size_t)s->E * sizeof(int2));
+  hipError_t e3 = hipMalloc((void**)&s->d_ctr, (size_t)(s->E + 1) * sizeof(int2));
   hipError_t e4 = hipMalloc(&s->d_init, (size_t)s->D * 10 * rs);
   hipError_t e5 = hipMalloc(&s->d_target, (size_t)s->D * 3 * rs);
   hipError_t e6 = hipMalloc(&s->d_consts, s->prec == GPD_F64 ? sizeof(Consts<double>) : sizeof(Consts<float>));
@@ -655,7 +680,7 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   if (rc != GPD_OK) { free_sim(s); return rc; }
   if (hipMemset(s->d_state, 0, (size_t)kStateComps * s->npad * rs) != hipSuccess ||
       hipMemset(s->d_ring, 0, (size_t)s->ring_len * s->npad * s->A * sizeof(float)) != hipSuccess ||
-      hipMemset(s->d_ctr, 0, (size_t)s->E * sizeof(int2)) != hipSuccess ||
+      hipMemset(s->d_ctr, 0, (size_t)(s->E + 1) * sizeof(int2)) != hipSuccess ||
       (pid && hipMemset(s->d_ctrl, 0, (size_t)kCtrlComps * s->npad * rs) != hipSuccess)) {
     free_sim(s);
     return fail(GPD_EHIP, "gpd_create: hipMemset failed");
@@ -819,6 +844,8 @@ int gpd_get_step_counters(gpd_sim* sim, int32_t* out, void* stream) {
 
 int gpd_set_step_counters(gpd_sim* sim, const int32_t* in, void* stream) {
   if (!sim || !in) return fail(GPD_EINVAL, "gpd_set_step_counters: NULL argument");
+  const int rc = settle_last_any(sim, (hipStream_t)stream);   // the ring-derived value reads them
+  if (rc != GPD_OK) return rc;
   HIP_TRY(hipMemcpy2DAsync(sim->d_ctr, sizeof(int2), in, sizeof(int32_t), sizeof(int32_t), (size_t)sim->E,
                            hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return GPD_OK;
@@ -860,6 +887,8 @@ int gpd_save_state(gpd_sim* sim, void* blob_host, void* stream) {
   int64_t hdr[kBlobHeader / 8];
   blob_header(sim, hdr);
   std::memcpy(b, hdr, kBlobHeader);
+  const int rc = settle_last_any(sim, st);
+  if (rc != GPD_OK) return rc;
   size_t off = kBlobHeader;
   Section sec[4];
   const int ns = sections(sim, sec);
@@ -887,6 +916,7 @@ int gpd_load_state(gpd_sim* sim, const void* blob_host, void* stream) {
     if (sec[i].bytes) HIP_TRY(hipMemcpyAsync(sec[i].dev, b + off, sec[i].bytes, hipMemcpyHostToDevice, st));
     off += sec[i].bytes;
   }
+  if (sim->wt & 4) HIP_TRY(hipMemsetAsync(sim->d_ctr + sim->E, 0, sizeof(int2), st));   // saved settled
   HIP_TRY(hipStreamSynchronize(st));
   return GPD_OK;
 }

@@ -124,7 +124,8 @@ struct SimView {
   long long npad;         // drones rounded up to whole 64-drone tiles
   int N, D, A, W, tpb, ring_len;
   int task, autoreset, trunc_sc;
-  int wt;                 // write-through stores: bit 0 obs/terminal rows, bit 1 state (see store_wt)
+  int wt;                 // write-through stores: bit 0 obs/terminal rows, bit 1 state (see store_wt);
+                          // bit 2: last_clipped_action lives in the ring (store_drone_step)
   int nc_magic;           // floor(t / NC) == (t * nc_magic) >> 16 for 0 <= t < 64 (host-checked)
   DwPairs dw_pairs;       // downwash pair split (n = 0: one lane per drone loops over its env)
   R bound_xy;             // 1.5 (Hover) or 2.0 (MultiHover)
@@ -182,8 +183,10 @@ __device__ __forceinline__ void store_drone_wt(const SimView<R>& v, long long n,
   int o = (int)(tidx(n, 0, kStateComps) * sizeof(R));
   const R vals[20] = {s.px, s.py, s.pz, s.qx, s.qy, s.qz, s.qw, s.vx, s.vy, s.vz,
                       s.wx, s.wy, s.wz, s.ax, s.ay, s.az, last[0], last[1], last[2], last[3]};
+  const bool skip_last = (v.wt & 4) != 0;   // store_drone_step
 #pragma unroll
-  for (int k = 0; k < 20; ++k, o += 64 * (int)sizeof(R)) store_wt(r, o, vals[k]);
+  for (int k = 0; k < 20; ++k, o += 64 * (int)sizeof(R))
+    if (k < 16 || !skip_last) store_wt(r, o, vals[k]);
 }
 
 template <typename R>
@@ -195,6 +198,35 @@ __device__ __forceinline__ void store_drone(const SimView<R>& v, long long n, co
   st[10 * 64] = s.wx; st[11 * 64] = s.wy; st[12 * 64] = s.wz;
   st[13 * 64] = s.ax; st[14 * 64] = s.ay; st[15 * 64] = s.az;
   st[16 * 64] = last[0]; st[17 * 64] = last[1]; st[18 * 64] = last[2]; st[19 * 64] = last[3];
+}
+
+// The step kernels' state store.  With SimView::wt bit 2 (RPM / ONE_D_RPM action types without
+// drag, where nothing in the step reads it) last_clipped_action is not stored: it equals
+// action_to_rpm of the ring's newest slot, or 0 in an env that has not stepped since its reset,
+// and last_from_ring_kernel writes it back before any reader of state[16..19] (32 B per drone
+// and step less HBM traffic in f64).  The kernel marks that with ctr[E].x = 1 (mark_last_in_ring).
+template <typename R>
+__device__ __forceinline__ void store_drone_step(const SimView<R>& v, long long n, const Drone<R>& s,
+                                                 const R last[4]) {
+  if (v.wt & 2) {
+    store_drone_wt(v, n, s, last);
+    return;
+  }
+  R* st = v.state + tidx(n, 0, kStateComps);
+  st[0 * 64] = s.px; st[1 * 64] = s.py; st[2 * 64] = s.pz;
+  st[3 * 64] = s.qx; st[4 * 64] = s.qy; st[5 * 64] = s.qz; st[6 * 64] = s.qw;
+  st[7 * 64] = s.vx; st[8 * 64] = s.vy; st[9 * 64] = s.vz;
+  st[10 * 64] = s.wx; st[11 * 64] = s.wy; st[12 * 64] = s.wz;
+  st[13 * 64] = s.ax; st[14 * 64] = s.ay; st[15 * 64] = s.az;
+  if (!(v.wt & 4)) {
+    st[16 * 64] = last[0]; st[17 * 64] = last[1]; st[18 * 64] = last[2]; st[19 * 64] = last[3];
+  }
+}
+
+// drone 0's lane of a step launch: the state's last_clipped_action columns are stale from here on
+template <typename R>
+__device__ __forceinline__ void mark_last_in_ring(const SimView<R>& v, long long n) {
+  if ((v.wt & 4) && n == 0) v.ctr[v.N / v.D] = make_int2(1, 0);
 }
 
 // Workgroup barrier for LDS exchanges within a block (between its waves, or its lanes): waits for this wave's own
@@ -583,8 +615,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
   GPD_STAMP(7);
   GPD_RSTAMP(12);
   if (!active) return;
-  if (v.wt & 2) store_drone_wt(v, n, s, last);
-  else store_drone(v, n, s, last);
+  store_drone_step(v, n, s, last);
+  mark_last_in_ring(v, n);
   if (act_is_pid(ACT)) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) v.ctrl[tidx(n, k, 9)] = cs[k];
@@ -997,8 +1029,8 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
   GPD_STAMP(7);
   GPD_RSTAMP(12);
   if (!active) return;
-  if (v.wt & 2) store_drone_wt(v, n, s, last);
-  else store_drone(v, n, s, last);
+  store_drone_step(v, n, s, last);
+  mark_last_in_ring(v, n);
   io.reward[n] = reward;
   io.term[n] = term ? 1 : 0;
   io.trunc[n] = trunc ? 1 : 0;
@@ -1152,7 +1184,8 @@ __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R>
     for (int k = 6; k < 12; ++k) row12[k] = 0.0f;
   }
   for (int k = 0; k < 12; ++k) orow[k] = row12[k];
-  store_drone(v, n, s, last);
+  store_drone_step(v, n, s, last);
+  mark_last_in_ring(v, n);
   if (act_is_pid(ACT)) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) v.ctrl[tidx(n, k, 9)] = cs[k];
@@ -1309,6 +1342,27 @@ __global__ __launch_bounds__(256) void reset_kernel(SimView<R> v, const uint8_t*
       for (int j = 0; j < A; ++j) orow[12 + k * A + j] = src[j];
     }
   }
+}
+
+// last_clipped_action back into the state (store_drone_step): when ctr[E].x is set, drone n's
+// state[16..19] = action_to_rpm of its ring's newest slot (head - 1 after the step; the same
+// float32 mapping as the step, _preprocessAction BaseRLAviary.py:191-192), or 0 when its env's
+// step_counter is 0 (_housekeeping zeroes last_clipped_action, BaseAviary.py:466).  The caller
+// clears the mark afterwards (stream order).
+template <typename R>
+__global__ __launch_bounds__(256) void last_from_ring_kernel(SimView<R> v, const Consts<R>* __restrict__ c) {
+  const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= v.N) return;
+  if (v.ctr[v.N / v.D].x == 0) return;
+  const int2 cv = v.ctr[n / v.D];
+  R last[4] = {R(0), R(0), R(0), R(0)};
+  if (cv.x != 0) {
+    const int slot = cv.y == 0 ? v.ring_len - 1 : cv.y - 1;
+    const float* a = v.ring + ridx(n, slot, v.ring_len, v.A);
+    const float hover = c->hover_f32;
+    for (int k = 0; k < 4; ++k) last[k] = (R)action_to_rpm(hover, a[v.A == 4 ? k : 0]);
+  }
+  for (int k = 0; k < 4; ++k) v.state[tidx(n, 16 + k, kStateComps)] = last[k];
 }
 
 // state20 (BaseAviary._getDroneStateVector :541-561, literal Bullet readback) / raw transposes
