@@ -274,8 +274,12 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const
 // Bytes of dynamic LDS the step kernel needs for its observation tile: the row's columns
 // (state, history, current action).  A == 4 keeps float4 columns (state 3, history+action L);
 // A == 1 / 3 keep float columns (state 12, history+action L*A).
+#ifndef GPD_TILE_MIN
+#define GPD_TILE_MIN 0   // diagnostic builds only: minimum LDS per block (occupancy probe)
+#endif
 __host__ __device__ inline int step_tile_bytes(int A, int ring_len) {
-  return A == 4 ? (3 + ring_len) * kPad * 16 : (12 + ring_len * A) * kPad * 4;
+  const int b = A == 4 ? (3 + ring_len) * kPad * 16 : (12 + ring_len * A) * kPad * 4;
+  return b > GPD_TILE_MIN ? b : GPD_TILE_MIN;
 }
 
 // Copy-out of the observation tile: the block's nact rows of NC columns (float4 columns for
