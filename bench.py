@@ -78,7 +78,7 @@ def rocprof_kernel_us(kernel, grid, precision):
             continue
         for row in d.get("kernels", []):
             if row.get("kernel") == kernel and row.get("grid") == grid and "bench" in row.get("trace", ""):
-                best = (row["mean_us"], os.path.relpath(f, ROOT))
+                best = (row["mean_us"], os.path.relpath(f, ROOT), row.get("b2b_median_us"))
     return best
 
 
@@ -633,6 +633,11 @@ def run(args):
     if rp is not None:
         result["roofline"]["kernel_us_rocprof"] = rp[0]
         result["roofline"]["kernel_us_rocprof_source"] = rp[1]
+        if rp[2] is not None:
+            # the profiler leaves most launches isolated (each waits for the host); the ones that
+            # still ran back to back, as in the graph-replayed timed region, are the like-for-like
+            # figure for kernel_us (scripts/prof_summary.py B2B_US)
+            result["roofline"]["kernel_us_rocprof_back_to_back_median"] = rp[2]
     tr = pmc_traffic(grid_lanes, args.precision)
     if tr is not None:
         result["roofline"]["traffic"] = tr[0]

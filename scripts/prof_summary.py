@@ -19,11 +19,23 @@ from collections import defaultdict
 
 
 def kernel_groups(trace_csv, name="step_kernel"):
+    """{(kernel, grid): [(duration us, started within B2B_US of the previous launch's end)]}"""
+    rows = sorted((r for r in csv.DictReader(open(trace_csv)) if name in r["Kernel_Name"]),
+                  key=lambda r: int(r["Start_Timestamp"]))
     g = defaultdict(list)
-    for r in csv.DictReader(open(trace_csv)):
-        if name in r["Kernel_Name"]:
-            g[(r["Kernel_Name"], int(r["Grid_Size_X"]))].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0)
+    prev_end = None
+    for r in rows:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        b2b = prev_end is not None and (s - prev_end) / 1000.0 < B2B_US
+        g[(r["Kernel_Name"], int(r["Grid_Size_X"]))].append(((e - s) / 1000.0, b2b))
+        prev_end = e
     return g
+
+
+# Launches that start within this many us of the previous one's end ran back to back, as in the
+# graph-replayed timed region; the rest ran after an idle queue (the profiler makes most
+# launches isolated: each one waits for the host), which adds a cold start to their duration.
+B2B_US = 3.0
 
 
 def pmc_groups(pmc_csv, counter, name="step_kernel"):
@@ -38,14 +50,20 @@ def main(rdir, out_md):
     lines = [f"# rocprofv3 summary — {os.path.basename(rdir.rstrip('/'))}", ""]
     summary = {"kernels": [], "pmc": [], "precision": os.environ.get("GPD_PROFILE_PRECISION", "f64")}
     for trace in sorted(glob.glob(os.path.join(rdir, "**", "*_kernel_trace.csv"), recursive=True)):
-        lines += [f"## {os.path.relpath(trace, rdir)}", "", "| kernel | grid (lanes) | launches | mean us | median us | min us |",
-                  "|---|---|---|---|---|---|"]
-        for (k, grid), v in sorted(kernel_groups(trace).items(), key=lambda kv: kv[0][1]):
+        lines += [f"## {os.path.relpath(trace, rdir)}", "",
+                  "| kernel | grid (lanes) | launches | mean us | median us | min us | back-to-back launches | their median us |",
+                  "|---|---|---|---|---|---|---|---|"]
+        for (k, grid), dv in sorted(kernel_groups(trace).items(), key=lambda kv: kv[0][1]):
             short = k.split("(")[0].replace("void ", "")
+            v = [d for d, _ in dv]
+            b = [d for d, bb in dv if bb]
             row = {"trace": os.path.relpath(trace, rdir), "kernel": short, "grid": grid, "launches": len(v),
-                   "mean_us": statistics.mean(v), "median_us": statistics.median(v), "min_us": min(v)}
+                   "mean_us": statistics.mean(v), "median_us": statistics.median(v), "min_us": min(v),
+                   "b2b_launches": len(b), "b2b_median_us": statistics.median(b) if b else None}
             summary["kernels"].append(row)
-            lines.append(f"| `{short}` | {grid} | {len(v)} | {row['mean_us']:.2f} | {row['median_us']:.2f} | {row['min_us']:.2f} |")
+            bm = f"{row['b2b_median_us']:.2f}" if b else "-"
+            lines.append(f"| `{short}` | {grid} | {len(v)} | {row['mean_us']:.2f} | {row['median_us']:.2f} | "
+                         f"{row['min_us']:.2f} | {len(b)} | {bm} |")
         lines.append("")
     pmc = {}
     for f in sorted(glob.glob(os.path.join(rdir, "**", "*_counter_collection.csv"), recursive=True)):
