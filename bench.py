@@ -261,18 +261,23 @@ def _timed_region(device, body):
     return wall
 
 
-def _event_region_us(device, body):
-    """The same launches again, right after the timed region, bracketed by a HIP event pair on
-    the launch stream: (event time / launches) is the step kernel's average duration including
-    the in-graph kernel boundary (an upper bound; rocprofv3 reports the kernel alone)."""
+def _event_region_us(device, body, launches, min_launches=256):
+    """The same launches again, right after the timed region, repeated to at least
+    `min_launches` step launches and bracketed by one HIP event pair on the launch stream:
+    returns the step kernel's average duration in us, including the in-graph kernel boundary
+    (an upper bound; rocprofv3 reports the kernel alone).  The repetition keeps the region's
+    own fixed cost (queue start after the first event, the first launch's cold caches: ~10 us,
+    DESIGN.md §7) from inflating the per-launch figure of a short (K = 20) timed region."""
+    reps = max(1, -(-int(min_launches) // max(1, int(launches))))
     stream = torch.cuda.current_stream(device)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(device)
     ev0.record(stream)
-    body()
+    for _ in range(reps):
+        body()
     ev1.record(stream)
     torch.cuda.synchronize(device)
-    return 1000.0 * ev0.elapsed_time(ev1)
+    return 1000.0 * ev0.elapsed_time(ev1) / (reps * launches)
 
 
 def time_graph(sim, pool, steps, warmup, per_graph=256):
@@ -281,7 +286,8 @@ def time_graph(sim, pool, steps, warmup, per_graph=256):
     launches, so that exactly `steps` steps are timed.  Before the timed region every captured
     graph is replayed at least once (the first replay of a graph pays its upload to the device),
     then `warmup` further untimed steps run, whatever `warmup` is.
-    The kernel duration comes from _event_region_us over a second, identical replay.
+    The kernel duration comes from _event_region_us over the same replays right after it (for
+    fewer than 256 steps: over one 256-launch graph of the same kind).
     Returns (wall seconds, steps run, kernel us)."""
     P = pool.shape[0]
     steps = max(1, int(steps))
@@ -305,7 +311,13 @@ def time_graph(sim, pool, steps, warmup, per_graph=256):
         if tail is not None:
             tail.replay()
     wall = _timed_region(sim.device, body)
-    return wall, steps, _event_region_us(sim.device, body) / steps
+    if steps >= 256:
+        return wall, steps, _event_region_us(sim.device, body, steps)
+    # a short timed region: the kernel time from one 256-launch graph of the same steps, so that
+    # neither the region's fixed cost nor per-replay graph boundaries enter the per-launch figure
+    long_graph = sim.capture_graph([pool[k % P] for k in range(256)])
+    long_graph.replay()
+    return wall, steps, _event_region_us(sim.device, long_graph.replay, 256)
 
 
 def time_native(sim, pool, steps, warmup):
@@ -313,14 +325,14 @@ def time_native(sim, pool, steps, warmup):
     native code (step k reads action slot k % P), no graph.  Its per-region fixed cost is a little
     below a graph replay's, but each launch costs the host ~5-6 us (about one kernel), so at large
     K it can turn host-bound (scripts/timing_probe.py); reported beside the graph timing.  Kernel
-    duration from _event_region_us over a second, identical call.  Returns (wall s, steps, kernel us)."""
+    duration from _event_region_us over the same call right after it.  Returns (wall s, steps, kernel us)."""
     steps = max(1, int(steps))
     sim.step_seq(pool, max(1, int(warmup)))
 
     def body():
         sim.step_seq(pool, steps)
     wall = _timed_region(sim.device, body)
-    return wall, steps, _event_region_us(sim.device, body) / steps
+    return wall, steps, _event_region_us(sim.device, body, steps)
 
 
 def time_steps(sim, pool, steps, warmup):
@@ -443,6 +455,24 @@ def other_configs(device, precision, act):
                     "value": E * D * sim.pyb_steps_per_ctrl * n / w, "unit": "drone*dt/s"})
         sim.close()
     return out
+
+
+def hbm_copy_gbps(device, n=1 << 28, reps=5):
+    """Live ceiling beside the 8 TB/s spec: torch copy_ of n float32 (1 GiB, far past the 256 MB
+    Infinity Cache), bytes read + written per second (scripts/ubench/rw_mix.hip measures the
+    step's own read/write shape)."""
+    x = torch.empty(n, device=device)
+    y = torch.empty(n, device=device)
+    y.copy_(x)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        y.copy_(x)
+    torch.cuda.synchronize(device)
+    el = (time.perf_counter() - t0) / reps
+    del x, y
+    torch.cuda.empty_cache()
+    return 2 * n * 4 / el / 1e9
 
 
 def raw_integrator(device, precision, n_drones=1 << 20, n_sub=32):
@@ -685,7 +715,11 @@ def run(args):
             s2.close()
             del p2
             torch.cuda.empty_cache()
+        copy = hbm_copy_gbps(device)
+        for row in sweep:
+            row["frac_of_copy"] = row["achieved_GBps"] / copy
         result["sweep"] = sweep
+        result["hbm_copy_GBps"] = copy
 
     if rank == 0 and world == 1 and not args.no_sweep:
         import warnings
