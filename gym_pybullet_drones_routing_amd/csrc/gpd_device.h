@@ -35,6 +35,8 @@ __device__ __forceinline__ float g_exp(float x) { return expf(x); }
 __device__ __forceinline__ double g_exp(double x) { return exp(x); }
 __device__ __forceinline__ float g_abs(float x) { return fabsf(x); }
 __device__ __forceinline__ double g_abs(double x) { return fabs(x); }
+__device__ __forceinline__ float g_fmax(float a, float b) { return fmaxf(a, b); }
+__device__ __forceinline__ double g_fmax(double a, double b) { return fmax(a, b); }
 
 // 1/sqrt(x) for x > 0: the hardware estimate (v_rsq_*) refined by Newton steps
 // y <- y + y*(1/2 - x*y*y/2); two steps for double (error <= ~2 ulp), one for float.  Replaces
@@ -637,7 +639,7 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
         dl0 = dl0 + nx * dm; dl1 = dl1 + ny * dm; dl2 = dl2 + nz * dm;
         da0 = da0 + (ax * k.ijx) * delta; da1 = da1 + (ay * k.ijy) * delta; da2 = da2 + (az * k.ijz) * delta;
         const R rr = delta * pc[p * kPer + kJdn][ln];
-        res = rr * rr > res ? rr * rr : res;
+        res = g_fmax(res, rr * rr);   // the oracle's max(res, x); x = rr^2 is never -0, NaN keeps res
       }
 #pragma unroll
       for (int p = 0; p < 4; ++p) {                  // friction pairs on the cone
@@ -671,7 +673,7 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
         dl0 = dl0 + ex * m2v; dl1 = dl1 + ey * m2v; dl2 = dl2 + ez * m2v;
         da0 = da0 + (cx * k.ijx) * d2; da1 = da1 + (cy * k.ijy) * d2; da2 = da2 + (cz * k.ijz) * d2;
         const R rr = (d1 + d2) * (d1 + d2);
-        res = rr > res ? rr : res;
+        res = g_fmax(res, rr);
       }
       done = res <= resid;
     }
