@@ -2,6 +2,8 @@
 
 Both are test infrastructure; agreement between two independent codings of the same
 reference lines is what lets the C one stand in for the numpy one at large sizes."""
+import os
+
 import numpy as np
 import pytest
 
@@ -76,3 +78,18 @@ def test_step_c_vs_numpy(act, task, D):
         for e in np.nonzero(te | tr)[0]:
             assert_obs_match(c.terminal_obs[e], tobs_r[(t, e)], 1e-6, 1e-7)
     c.close()
+
+
+def test_oracle_under_asan():
+    """the C restatement under AddressSanitizer + UBSan (oracle/asan_driver.c drives
+    every entry point on single- and 8-drone envs with every force flag); no report, exit 0."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle"), "asan"], capture_output=True, text=True,
+                       timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    assert "OK" in r.stdout and "Sanitizer" not in out and "runtime error" not in out, out[-3000:]
