@@ -650,6 +650,9 @@ def run(args):
                    "n_envs_per_gpu": E, "global_envs": E * world, "drones_per_env": 1,
                    "parallelism": f"env-sharded x{world} (no collective in the step loop)"},
         "kernel_us": kern_us,
+        "timed_region_note": ("a timed region carries a fixed ~18 us HIP round trip (graph launch -> first kernel, "
+                              "completion -> synchronize return), ~0.9 us/step at K = 20; per-step cost without it "
+                              "= kernel_us (DESIGN.md §7.1)") if args.steps < 100 else None,
         "eager": {"ms_per_step": 1000.0 * eager_wall / args.steps,
                   "value": world * E * nsub * args.steps / eager_wall,
                   "kernel_us_per_launch_events": eager_kern_us},
