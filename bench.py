@@ -681,31 +681,33 @@ def run(args):
         result["roofline"]["traffic_source"] = tr[1] + " (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate passes)"
     if world > 1:
         # config 5: the learner hand-off (shard.LearnerHandoff): rank 0 scatters the global action
-        # batch, every rank steps its shard, one all-gather of the output packs (obs, reward,
-        # terminated, truncated, terminal rows) returns the step to the learner
-        handoff = LearnerHandoff(sim, E * world)
+        # batch, every rank steps its shard, the output-pack prefixes (obs, reward, terminated,
+        # truncated) go to the learner ("gather") or to every rank ("all_gather"), and the finished
+        # envs' terminal rows follow, densely packed
         gpool = None
         if rank == 0:
             gpool = make_pool(E * world, A, device, seed=11, pool=8)
         G = max(10, args.steps // 3)
-        for k in range(3):
-            handoff.step(gpool[k % 8] if rank == 0 else None)
-        torch.cuda.synchronize(device)
-        torch.distributed.barrier()
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        for k in range(G):
-            handoff.step(gpool[k % 8] if rank == 0 else None)
-        torch.cuda.synchronize(device)
-        gw = max_over_ranks(time.perf_counter() - t0, device)
         coll = "RCCL" if args.dist_backend == "nccl" else "gloo (rehearsal, through host memory)"
-        act_b, pack_b = handoff.bytes_per_step()
-        result["gather"] = {"mode": f"learner hand-off per step: {coll} scatter of actions from rank 0, eager "
-                                    "shard step, all_gather_into_tensor of the output packs (obs, reward, "
-                                    "terminated, truncated, terminal obs)",
-                            "ms_per_step": 1000 * gw / G, "value": world * E * nsub * G / gw,
-                            "action_bytes_per_step": act_b, "gathered_bytes_per_step": pack_b,
-                            "pack_bytes_per_rank": handoff.nbytes}
+        legs = {}
+        for hmode in ("gather", "all_gather"):
+            handoff = LearnerHandoff(sim, E * world, mode=hmode)
+            for k in range(3):
+                handoff.step(gpool[k % 8] if rank == 0 else None)
+            torch.cuda.synchronize(device)
+            torch.distributed.barrier()
+            torch.cuda.synchronize(device)
+            handoff.terminal_bytes, handoff.steps = 0, 0
+            t0 = time.perf_counter()
+            for k in range(G):
+                handoff.step(gpool[k % 8] if rank == 0 else None)
+            torch.cuda.synchronize(device)
+            gw = max_over_ranks(time.perf_counter() - t0, device)
+            legs[hmode] = dict(handoff.stats(), ms_per_step=1000 * gw / G, value=world * E * nsub * G / gw)
+        result["gather"] = {"mode": f"learner hand-off per step ({coll}): scatter of actions from rank 0, eager "
+                                    "shard step, gather / all_gather_into_tensor of the output-pack prefixes, "
+                                    "terminal rows of finished envs only",
+                            "legs": legs}
 
     if rank == 0 and world == 1 and not args.no_latency_model:
         result["roofline"]["latency_model"] = latency_model(device, args.precision, args.act, E, kern_us, nsub)

@@ -181,8 +181,11 @@ struct Drone {
 
 // ---------------------------------------------------------------- Bullet3 rotation helpers
 // btMatrix3x3::setRotation (pybullet getMatrixFromQuaternion, BaseAviary.py:836): row-major.
+// The literal Bullet helpers (quat_to_mat, mat_to_quat, quat_to_euler) are compiled without FP
+// contraction: Bullet's double-precision build (and numpy) rounds every product and sum.
 template <typename R>
 __device__ __forceinline__ void quat_to_mat(R x, R y, R z, R w, R m[9]) {
+#pragma clang fp contract(off)
   const R d = x * x + y * y + z * z + w * w;
   const R s = R(2) / d;
   const R xs = x * s, ys = y * s, zs = z * s;
@@ -197,6 +200,7 @@ __device__ __forceinline__ void quat_to_mat(R x, R y, R z, R w, R m[9]) {
 // btMatrix3x3::getRotation: basis -> quaternion [x,y,z,w] (w > 0 when trace > 0).
 template <typename R>
 __device__ __forceinline__ void mat_to_quat(const R m[9], R q[4]) {
+#pragma clang fp contract(off)
   const R trace = m[0] + m[4] + m[8];
   if (trace > R(0)) {
     R s = g_sqrt(trace + R(1));
@@ -363,6 +367,7 @@ __device__ __forceinline__ void cos_sinc(float t2, float& c, float& sc) {
 // btQuaternion::getEulerZYX (pybullet getEulerFromQuaternion, BaseAviary.py:518).
 template <typename R>
 __device__ __forceinline__ void quat_to_euler(const R q[4], R& roll, R& pitch, R& yaw) {
+#pragma clang fp contract(off)
   const R x = q[0], y = q[1], z = q[2], w = q[3];
   const R sqx = x * x, sqy = y * y, sqz = z * z, squ = w * w;
   const R sarg = R(-2) * (x * z - w * y);
@@ -415,6 +420,83 @@ __device__ __forceinline__ bool tilted_beyond(const AttitudeArgs<R>& t, R sin_li
 template <typename R>
 __device__ __forceinline__ bool upright(const AttitudeArgs<R>& t) {
   return !t.gimbal && (t.b > R(0) || (t.b == R(0) && t.a == R(0) && !signbit(t.b)));
+}
+
+// ---------------------------------------------------------------- exact attitude decisions (f64)
+// tilted_beyond / upright see the fused readback's quaternion (~1 ulp from Bullet's) and compare
+// against rounded limits, so within a few ulp of a threshold they can disagree with the
+// reference, whose decisions are made on libm atan2 / asin outputs (HoverAviary.py:111,
+// MultiHoverAviary.py:124, BaseAviary.py:742).  attitude_decide re-decides the lanes of that band
+// exactly: the literal Bullet readback of the stored quaternion (quat_to_mat -> mat_to_quat ->
+// getEulerZYX's arguments, no FP contraction), then comparisons that equal "RN(atan2(a, b)) > 0.4",
+// "RN(asin(s)) > 0.4" and "RN(atan2(a, b)) < RN(pi/2)" for correctly rounded atan2 / asin
+// (glibc's, to which pybullet's btAtan2 / btAsin resolve):
+//   RN(x) > 0.4   <=>  x > M  = 0.4 + ulp(0.4)/2           (the rounding midpoint)
+//   asin(s) > M   <=>  s >= kSinLim, the smallest double above sin(M)
+//   atan2(a,b) > M, b > 0  <=>  |a| > tan(M) b             (tan(M) as a double-double)
+//   RN(x) < RN(pi/2) <=> x < Mg = RN(pi/2) - ulp/2;  atan2 < Mg, b > 0  <=>  b > cot(Mg) |a|
+// The constants come from mpmath at 400 bits (tests/test_oracle_kat.py re-derives them and checks
+// the rules against glibc on near-threshold samples).  Each double-double product is compared
+// exactly to ~2^-106 relative (an FMA gives the product's rounding error).
+struct AttK {
+  static constexpr double sin_lim = 0x1.8ec3ae92b676cp-2;                                  // asin > M
+  static constexpr double tan_hi = 0x1.b0f0b49dcdcd9p-2, tan_lo = -0x1.10521c23b5ec7p-56;  // tan(M)
+  static constexpr double cot_hi = 0x1.8d313198a2e03p-53, cot_lo = 0x1.c1cd129024e0ap-107; // cot(Mg)
+  static constexpr double gimbal = 0.99999;
+  static constexpr double band = 1e-12;   // fused vs literal arguments differ by a few 1e-16
+};
+// u > (hi + lo) * v for u, v >= 0
+__device__ __forceinline__ bool dd_above(double u, double hi, double lo, double v) {
+#pragma clang fp contract(off)
+  const double p = hi * v;
+  const double e = fma(hi, v, -p);      // hi*v = p + e exactly
+  return ((u - p) - e) - lo * v > 0.0;  // u - p is exact whenever the sign is in doubt (Sterbenz)
+}
+
+// getEulerZYX's arguments from the literal readback of the stored quaternion (x, y, z, w)
+// (BaseAviary.py:517-518: getBasePositionAndOrientation -> getEulerFromQuaternion)
+template <typename R>
+__device__ __forceinline__ void attitude_literal(R x, R y, R z, R w, AttitudeArgs<R>& t) {
+#pragma clang fp contract(off)
+  R m[9], q[4];
+  quat_to_mat(x, y, z, w, m);
+  mat_to_quat(m, q);
+  const R qx = q[0], qy = q[1], qz = q[2], qw = q[3];
+  t.sarg = R(-2) * (qx * qz - qw * qy);
+  t.a = R(2) * (qy * qz + qw * qx);
+  t.b = ((qw * qw - qx * qx) - qy * qy) + qz * qz;   // squ - sqx - sqy + sqz
+  t.gimbal = t.sarg <= R(-0.99999) || t.sarg >= R(0.99999);
+}
+
+// TILT: tilt = |roll| > 0.4 or |pitch| > 0.4; UP: up = |roll| < pi/2 and |pitch| < pi/2.
+// qs = the stored quaternion the readback starts from; t = attitude_args of the fused readback,
+// replaced by the literal arguments on the lanes that were re-decided (so that the observation's
+// gimbal branch follows the reference too).  Lanes outside the band keep the fused decision,
+// which equals the exact one there.  f32 builds keep the fused predicates.
+template <typename R, bool TILT, bool UP>
+__device__ __forceinline__ void attitude_decide(R qx, R qy, R qz, R qw, AttitudeArgs<R>& t, bool& tilt, bool& up) {
+  if (TILT) tilt = tilted_beyond(t, R(0.38941834230865049), R(0.42279321873816178));   // ~sin/tan(0.4)
+  if (UP) up = upright(t);
+  if constexpr (sizeof(R) == 8) {
+    const double as = fabs(t.sarg);
+    bool near = fabs(as - AttK::gimbal) < AttK::band;
+    if (TILT) near = near || fabs(as - AttK::sin_lim) < AttK::band || fabs(fabs(t.a) - AttK::tan_hi * t.b) < AttK::band;
+    if (UP) near = near || fabs(t.b) < AttK::band;
+    if (GPD_RARE(__ballot(near) != 0ull)) {
+      if (near) {
+        attitude_literal(qx, qy, qz, qw, t);
+        const bool zero_roll = t.a == 0.0 && t.b == 0.0 && !signbit(t.b);   // atan2(+-0, +0) = +-0
+        if (TILT) {
+          const bool roll_out = t.b > 0.0 ? dd_above(fabs(t.a), AttK::tan_hi, AttK::tan_lo, t.b) : !zero_roll;
+          tilt = t.gimbal || fabs(t.sarg) >= AttK::sin_lim || roll_out;
+        }
+        if (UP) {
+          const bool roll_in = t.b > 0.0 ? dd_above(t.b, AttK::cot_hi, AttK::cot_lo, fabs(t.a)) : zero_roll;
+          up = !t.gimbal && roll_in;
+        }
+      }
+    }
+  }
 }
 // float32 Euler angles for the float32 observation (the reference casts its float64 angles to
 // float32, BaseRLAviary.py:315); evaluated in float32 from the double-precision arguments.
@@ -729,7 +811,9 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, const R rpm[4], cons
   bool up = true;
   if (pf_on<PF>(k.flags, F_GND)) {   // |self.rpy[0,1]| < pi/2, :742
     const R qn[4] = {q0[0] * inv, q0[1] * inv, q0[2] * inv, q0[3] * inv};
-    up = upright(attitude_args(qn));
+    AttitudeArgs<R> t = attitude_args(qn);
+    bool tilt_unused;
+    attitude_decide<R, false, true>(s.qx, s.qy, s.qz, s.qw, t, tilt_unused, up);
   }
   R fz, tx, ty, tz;
   body_wrench<R, PF>(s, Rm, up, rpm, W, c, k, fz, tx, ty, tz);
@@ -850,7 +934,9 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R
     readback_unit<R, ANGV || kPoseFirst, false>(q0[0], q0[1], q0[2], q0[3], d, inv, Rm);
     if (pf_on<PF>(k.flags, F_GND)) {   // |self.rpy[0,1]| < pi/2, :742
       const R qn[4] = {q0[0] * inv, q0[1] * inv, q0[2] * inv, q0[3] * inv};
-      up = upright(attitude_args(qn));
+      AttitudeArgs<R> t = attitude_args(qn);
+      bool tilt_unused;
+      attitude_decide<R, false, true>(s.qx, s.qy, s.qz, s.qw, t, tilt_unused, up);
     }
   };
   if (kPoseFirst) readback();

@@ -502,7 +502,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
   // final readback (:374) -> obs / reward / done
   R qn[4], Rm[9];
   readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
-  const AttitudeArgs<R> att = attitude_args(qn);
+  AttitudeArgs<R> att = attitude_args(qn);
+  bool tilted, up_unused;   // |roll| or |pitch| > 0.4, decided exactly near the limit (attitude_decide)
+  attitude_decide<R, true, false>(s.qx, s.qy, s.qz, s.qw, att, tilted, up_unused);
   float roll, pitch, yaw;
   obs_euler_f32(qn, att, roll, pitch, yaw);
 
@@ -518,8 +520,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
     const R dist = g_sqrt(d2);
     R r = R(2) - d2 * d2;
     r = r > R(0) ? r : R(0);
-    const bool oob = g_abs(s.px) > v.bound_xy || g_abs(s.py) > v.bound_xy || s.pz > R(2) ||
-                     tilted_beyond(att, R(0.38941834230865049), R(0.42279321873816178));  // sin/tan(0.4)
+    const bool oob = g_abs(s.px) > v.bound_xy || g_abs(s.py) > v.bound_xy || s.pz > R(2) || tilted;
     if (MULTI) {
       srew[tid] = r;
       sdist[tid] = dist;
@@ -936,7 +937,9 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
   // final readback (:374) -> obs / reward / done
   R qn[4], Rm[9];
   readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
-  const AttitudeArgs<R> att = attitude_args(qn);
+  AttitudeArgs<R> att = attitude_args(qn);
+  bool tilted, up_unused;   // |roll| or |pitch| > 0.4, decided exactly near the limit (attitude_decide)
+  attitude_decide<R, true, false>(s.qx, s.qy, s.qz, s.qw, att, tilted, up_unused);
   float roll, pitch, yaw;
   obs_euler_f32(qn, att, roll, pitch, yaw);
   float reward = -1.0f;
@@ -947,8 +950,7 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
     const R d2 = tx * tx + ty * ty + tz * tz;
     R r = R(2) - d2 * d2;
     r = r > R(0) ? r : R(0);
-    const bool oob = g_abs(s.px) > v.bound_xy || g_abs(s.py) > v.bound_xy || s.pz > R(2) ||
-                     tilted_beyond(att, R(0.38941834230865049), R(0.42279321873816178));  // sin/tan(0.4)
+    const bool oob = g_abs(s.px) > v.bound_xy || g_abs(s.py) > v.bound_xy || s.pz > R(2) || tilted;
     reward = (float)r;
     term = g_sqrt(d2) < R(1e-4);   // np.linalg.norm(...) < .0001 (HoverAviary.py:92)
     trunc = oob || sc >= v.trunc_sc;
@@ -1116,7 +1118,9 @@ __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R>
   // final readback (:374) -> obs / reward / done
   R qn[4], Rm[9];
   readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
-  const AttitudeArgs<R> att = attitude_args(qn);
+  AttitudeArgs<R> att = attitude_args(qn);
+  bool tilted, up_unused;   // |roll| or |pitch| > 0.4, decided exactly near the limit (attitude_decide)
+  attitude_decide<R, true, false>(s.qx, s.qy, s.qz, s.qw, att, tilted, up_unused);
   float roll, pitch, yaw;
   obs_euler_f32(qn, att, roll, pitch, yaw);
   float reward = -1.0f;
@@ -1128,8 +1132,7 @@ __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R>
     const R dist = g_sqrt(d2);
     R r = R(2) - d2 * d2;
     r = r > R(0) ? r : R(0);
-    const bool oob = g_abs(s.px) > v.bound_xy || g_abs(s.py) > v.bound_xy || s.pz > R(2) ||
-                     tilted_beyond(att, R(0.38941834230865049), R(0.42279321873816178));  // sin/tan(0.4)
+    const bool oob = g_abs(s.px) > v.bound_xy || g_abs(s.py) > v.bound_xy || s.pz > R(2) || tilted;
     __syncthreads();
     if (active) { sx[d] = r; sy[d] = dist; sflag[d] = oob ? 1 : 0; }
     __syncthreads();
@@ -1150,6 +1153,9 @@ __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R>
   const bool do_reset = done && v.autoreset;
   float row12[12] = {(float)s.px, (float)s.py, (float)s.pz, roll, pitch, yaw,
                      (float)s.vx, (float)s.vy, (float)s.vz, (float)s.ax, (float)s.ay, (float)s.az};
+  // every wave has read ctr[e] (kernel entry) before lane d == 0 overwrites it below; without a
+  // task, downwash or contact no other workgroup barrier orders the two
+  __syncthreads();
   if (!active) return;
   const int L = v.ring_len, Wd = v.W;
   // history columns: ring slots head+1 .. head+L-1 (oldest first), then the current action
@@ -1230,8 +1236,8 @@ __global__ __launch_bounds__(MAXT) void integrate_kernel_wide(SimView<R> v, cons
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];
     if (TRAJ && active) {
-      R qn[4], Rm[9], roll, pitch, yaw;
-      readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
+      R qn[4], roll, pitch, yaw;   // the literal Bullet readback (as state20): exact gimbal branches
+      quat_readback(s.qx, s.qy, s.qz, s.qw, qn);
       quat_to_euler(qn, roll, pitch, yaw);
       R* o = traj + ((long long)t * N + n) * 20;
       o[0] = s.px; o[1] = s.py; o[2] = s.pz;
@@ -1296,8 +1302,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_INTEG
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];
     if (TRAJ && active) {   // TRAJ: the trajectory variant (its readback / Euler registers stay out of the other)
-      R qn[4], Rm[9], roll, pitch, yaw;
-      readback_fused(s.qx, s.qy, s.qz, s.qw, qn, Rm);
+      R qn[4], roll, pitch, yaw;   // the literal Bullet readback (as state20): exact gimbal branches
+      quat_readback(s.qx, s.qy, s.qz, s.qw, qn);
       quat_to_euler(qn, roll, pitch, yaw);
       R* o = traj + ((long long)t * N + n) * 20;
       o[0] = s.px; o[1] = s.py; o[2] = s.pz;

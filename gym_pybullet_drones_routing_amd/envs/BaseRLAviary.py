@@ -91,12 +91,15 @@ class BaseRLAviary:
         """BaseAviary.step (:259-383): one HIP launch for the PYB_STEPS_PER_CTRL substeps."""
         a = np.asarray(action, dtype=np.float32).reshape(self._act_dev.shape)
         self._act_dev.copy_(torch.from_numpy(a))
-        obs, rew, te, tr = self.sim.step(self._act_dev, terminal_obs=False)
-        out = torch.cat([obs.reshape(-1), rew, te.float(), tr.float()]).cpu().numpy()
+        obs, _, te, tr = self.sim.step(self._act_dev, terminal_obs=False)
+        out = torch.cat([obs.reshape(-1), te.float(), tr.float()]).cpu().numpy()
+        # the reward as the reference returns it: a Python float computed in fp64 from the state
+        # vector (HoverAviary.py:78, MultiHoverAviary.py:84-89), not the batched path's float32 copy
+        self._pos = self.sim.raw_state()[:, 0:3].cpu().numpy().astype(np.float64)
         W = self.NUM_DRONES * self.sim.obs_width
         self.step_counter += self.PYB_STEPS_PER_CTRL
-        return (out[:W].reshape(self.NUM_DRONES, self.sim.obs_width), float(out[W]), bool(out[W + 1]),
-                bool(out[W + 2]), self._computeInfo())
+        return (out[:W].reshape(self.NUM_DRONES, self.sim.obs_width), self._computeReward(), bool(out[W]),
+                bool(out[W + 1]), self._computeInfo())
 
     def close(self):
         self.sim.close()
@@ -113,6 +116,9 @@ class BaseRLAviary:
 
     def _computeInfo(self):
         return {"answer": 42}
+
+    def _computeReward(self):
+        raise NotImplementedError   # HoverAviary / MultiHoverAviary
 
     def _normalizedActionToRPM(self, action):
         """BaseAviary._normalizedActionToRPM (:893-911)."""

@@ -23,3 +23,7 @@ class HoverAviary(BaseRLAviary):
         super().__init__(drone_model=drone_model, num_drones=1, initial_xyzs=initial_xyzs,
                          initial_rpys=initial_rpys, physics=physics, pyb_freq=pyb_freq, ctrl_freq=ctrl_freq,
                          gui=gui, record=record, obs=obs, act=act, episode_len_sec=self.EPISODE_LEN_SEC, **kwargs)
+
+    def _computeReward(self):
+        """HoverAviary._computeReward (:68-79): fp64 from the position after the step."""
+        return max(0, 2 - np.linalg.norm(self.TARGET_POS - self._pos[0]) ** 4)

@@ -25,3 +25,10 @@ class MultiHoverAviary(BaseRLAviary):
                          ctrl_freq=ctrl_freq, gui=gui, record=record, obs=obs, act=act,
                          episode_len_sec=self.EPISODE_LEN_SEC, **kwargs)
         self.TARGET_POS = self.INIT_XYZS + np.array([[0, 0, 1 / (i + 1)] for i in range(num_drones)])
+
+    def _computeReward(self):
+        """MultiHoverAviary._computeReward (:75-89): the per-drone rewards summed in fp64."""
+        ret = 0
+        for i in range(self.NUM_DRONES):
+            ret += max(0, 2 - np.linalg.norm(self.TARGET_POS[i, :] - self._pos[i]) ** 4)
+        return ret

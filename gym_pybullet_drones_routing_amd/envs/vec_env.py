@@ -146,8 +146,8 @@ class ShardedAviaryVecEnv:
     The learner (rank 0) uses this object exactly like ``AviaryVecEnv(output="torch")``:
     ``reset()``, ``step(actions [E, D, A])`` -> (obs [E, D, W], reward [E], done [E], infos) with
     SB3's ``terminal_observation`` / ``TimeLimit.truncated``.  Each call broadcasts a one-word
-    command, then ``shard.LearnerHandoff`` scatters the actions and all-gathers the shards'
-    output packs.  Every other rank runs ``serve()``, which answers commands until ``close()``.
+    command, then ``shard.LearnerHandoff`` scatters the actions and gathers the shards' output
+    packs (and the finished envs' terminal rows) to rank 0.  Every other rank runs ``serve()``, which answers commands until ``close()``.
     """
     STEP, RESET, STOP = 0, 1, 2
 
@@ -162,7 +162,7 @@ class ShardedAviaryVecEnv:
         kw["output"] = "torch"
         self.local = AviaryVecEnv(count, **kw)
         self.sim = self.local.sim
-        self.handoff = LearnerHandoff(self.sim, num_envs)
+        self.handoff = LearnerHandoff(self.sim, num_envs, mode="gather")   # one learner: rank 0
         self.num_envs = int(num_envs)
         self.num_drones = self.local.num_drones
         self.action_space = self.local.action_space
@@ -182,7 +182,7 @@ class ShardedAviaryVecEnv:
 
     def reset(self):
         self._send(self.RESET)
-        return self.handoff.reset().clone()
+        return self.handoff.reset()
 
     def step(self, actions):
         self._actions.copy_(torch.as_tensor(actions, dtype=torch.float32).reshape(self._actions.shape))

@@ -5,9 +5,10 @@ one PyBullet client per env, ``BaseAviary.py:170``), so the path partitions with
 at all.  Rank r owns the contiguous env block [r*E/G, (r+1)*E/G).  The only collectives are
 the hand-off between a learner on rank 0 and the shards (BASELINE config 5):
 ``LearnerHandoff`` scatters the learner's action batch to the ranks, each rank steps its shard,
-and one all-gather of every rank's output pack (obs, reward, terminated, truncated and, when
-asked, the terminal rows) brings the step back, in rank order, exactly as a single process
-stepping all E envs would have produced it (RCCL over xGMI on the GPU box; gloo in the CPU tests).
+and a gather (one learner) or all-gather (data-parallel learners) of every rank's output-pack
+prefix (obs, reward, terminated, truncated) plus the terminal rows of the envs that finished
+brings the step back, in rank order, exactly as a single process stepping all E envs would
+have produced it (RCCL over xGMI on the GPU box; gloo in the CPU tests).
 The caller being replaced is the reference's stepping loop, ``examples/learn.py:52-94``
 (``make_vec_env(..., n_envs=...)`` + PPO), over independent worlds (``BaseAviary.py:170``).
 """
@@ -88,18 +89,35 @@ class LearnerHandoff:
     1. ``scatter`` of the learner's actions [E, D, A] float32 -> each rank's [E/G, D, A]
        (E*D*A*4 bytes leave rank 0 in total);
     2. each rank steps its shard (the kernel writes straight into the output pack);
-    3. one ``all_gather_into_tensor`` of the packs (the prefix without terminal rows when
-       ``terminal_obs=False``): G * pack bytes land on every rank.
+    3. the pack PREFIX (obs | reward | terminated | truncated) of every rank goes to the learner:
+       ``mode="gather"`` (one learner: ``dist.gather`` to rank 0, G x prefix bytes land there
+       only) or ``mode="all_gather"`` (data-parallel learners: ``all_gather_into_tensor``, the
+       batch lands on every rank);
+    4. terminal rows (``terminal_obs=True``) move only for envs that finished this step, packed
+       densely: in "all_gather" mode every rank knows every rank's done count from the gathered
+       flags, and one ``all_gather_into_tensor`` of [max count, D, W] per rank runs when any env
+       finished; in "gather" mode each rank with finished envs ``send``s its k rows to the learner,
+       which ``recv``s exactly the counts it read from the gathered flags.  Steps where no env
+       finished move no terminal bytes.
 
     ``step`` returns (obs [E, D, W], reward [E], terminated [E], truncated [E], terminal_obs or
-    None) on the learner rank and None elsewhere.  With gloo (CPU tests, one-GPU rehearsals)
-    the same collectives run through host memory."""
+    None) - freshly allocated tensors, so a caller may keep them across steps - on the learner
+    rank ("gather") or every rank ("all_gather"), None elsewhere.  Rows of ``terminal_obs`` whose
+    env did not finish are zero.  ``force_collectives=True`` runs the collectives even in a
+    one-rank group (the RCCL path on a one-GPU box; otherwise a one-rank hand-off is a local copy).
+    With gloo (CPU tests, one-GPU rehearsals) the same exchange runs through host memory."""
 
-    def __init__(self, sim, global_envs, learner_rank=0, terminal_obs=True):
+    MODES = ("all_gather", "gather")
+
+    def __init__(self, sim, global_envs, learner_rank=0, terminal_obs=True, mode="all_gather",
+                 force_collectives=False):
+        if mode not in self.MODES:
+            raise ValueError(f"mode must be one of {self.MODES}")
         self.sim = sim
         self.rank = dist.get_rank() if dist.is_initialized() else 0
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.learner = learner_rank
+        self.mode = mode
         self.start, self.count = env_shard(global_envs, self.rank, self.world)
         if sim.n_envs != self.count:
             raise ValueError(f"rank {self.rank} sim has {sim.n_envs} envs, its shard is {self.count}")
@@ -107,24 +125,43 @@ class LearnerHandoff:
         self.terminal_obs = terminal_obs
         L = sim.pack_layout
         self.layout = L
-        self.nbytes = L["total"] if terminal_obs else L["prefix"]
+        self.nbytes = L["prefix"]
+        self.row_bytes = sim.drones_per_env * sim.obs_width * 4
         dev = sim.out_pack.device
+        self.device = dev
         self._gloo = dist.is_initialized() and dist.get_backend() == "gloo"
+        self._coll = dist.is_initialized() and (self.world > 1 or force_collectives)
         self.pack_all = torch.empty((self.world * self.nbytes,), dtype=torch.uint8, device=dev)
         D, A = sim.drones_per_env, sim.act_width
         self.local_actions = torch.empty((self.count, D, A), dtype=torch.float32, device=dev)
+        self.terminal_bytes = 0     # terminal-row bytes received by the learner so far (all steps)
+        self.steps = 0
 
     @property
     def is_learner(self):
         return self.rank == self.learner
 
+    @property
+    def receives(self):
+        return self.mode == "all_gather" or self.is_learner
+
     def bytes_per_step(self):
-        """(action bytes scattered, pack bytes all-gathered onto every rank) per step."""
+        """(action bytes scattered, prefix bytes landing per step: on every rank for
+        "all_gather", on the learner for "gather")."""
         return (self.global_envs * self.sim.drones_per_env * self.sim.act_width * 4,
                 self.world * self.nbytes)
 
+    def stats(self):
+        """Bytes per step of each part of the hand-off (learner side), averaged over the steps."""
+        act_b, pre_b = self.bytes_per_step()
+        return {"mode": self.mode, "action_bytes": act_b, "prefix_bytes": pre_b,
+                "terminal_bytes_avg": self.terminal_bytes / max(1, self.steps),
+                "terminal_row_bytes": self.row_bytes,
+                "lands_on": "every rank" if self.mode == "all_gather" else "learner"}
+
+    # ------------------------------------------------------------------ collectives
     def _scatter_actions(self, global_actions):
-        if self.world == 1:
+        if not self._coll:
             self.local_actions.copy_(global_actions)
             return
         if self.is_learner:
@@ -139,43 +176,132 @@ class LearnerHandoff:
         else:
             dist.scatter(self.local_actions, [p.contiguous() for p in parts] if parts else None, src=self.learner)
 
-    def _gather(self):
+    def _gather_prefix(self):
         local = self.sim.out_pack[:self.nbytes]
-        if self.world == 1:
+        if not self._coll:
             self.pack_all.copy_(local)
-        elif self._gloo:
-            parts = [torch.empty((self.nbytes,), dtype=torch.uint8) for _ in range(self.world)]
-            dist.all_gather(parts, local.cpu())
-            self.pack_all.copy_(torch.cat(parts))
+            return
+        parts = list(self.pack_all.view(self.world, self.nbytes).unbind(0))
+        if self.mode == "all_gather":
+            if self._gloo:
+                host = [torch.empty((self.nbytes,), dtype=torch.uint8) for _ in range(self.world)]
+                dist.all_gather(host, local.cpu())
+                self.pack_all.copy_(torch.cat(host))
+            else:
+                dist.all_gather_into_tensor(self.pack_all, local)
         else:
-            dist.all_gather_into_tensor(self.pack_all, local)
+            if self._gloo:
+                host = [torch.empty((self.nbytes,), dtype=torch.uint8) for _ in range(self.world)] \
+                    if self.is_learner else None
+                dist.gather(local.cpu(), host, dst=self.learner)
+                if self.is_learner:
+                    self.pack_all.copy_(torch.cat(host))
+            else:
+                dist.gather(local, parts if self.is_learner else None, dst=self.learner)
+
+    def _field(self, name, dtype, shape):
+        """Field `name` of every rank's gathered pack, as ONE fresh tensor [G*E, ...]."""
+        G, E = self.world, self.count
+        off, n = self.layout[name]
+        out = torch.empty((G, n), dtype=torch.uint8, device=self.device)
+        out.copy_(self.pack_all.view(G, self.nbytes)[:, off:off + n])
+        return out.view(dtype).reshape((G * E,) + shape)
+
+    def _local(self, name, dtype, shape):
+        off, n = self.layout[name]
+        return self.sim.out_pack[off:off + n].view(dtype).reshape(shape)
+
+    def _terminal_rows(self, te, tr):
+        """Terminal rows of the envs that finished this step ([G*E, D, W], zero elsewhere) on the
+        ranks that receive; None elsewhere.  te / tr: gathered flags (receiving ranks)."""
+        G, E, D, W = self.world, self.count, self.sim.drones_per_env, self.sim.obs_width
+        ldone = (self._local("terminated", torch.uint8, (E,)) | self._local("truncated", torch.uint8, (E,))).bool()
+        lrows = self._local("terminal_obs", torch.float32, (E, D * W))
+        if self.receives:
+            done_all = (te | tr).bool().reshape(G, E)
+            counts = done_all.sum(1).tolist()             # host sync: sizes the exchange
+        else:
+            counts = None
+        out = torch.zeros((G * E, D, W), dtype=torch.float32, device=self.device) if self.receives else None
+        if self.mode == "all_gather" or not self._coll:
+            kmax = max(counts)
+            if kmax == 0:
+                return out
+            buf = torch.zeros((kmax, D * W), dtype=torch.float32, device=self.device)
+            k = counts[self.rank]
+            if k:
+                buf[:k] = lrows[ldone]
+            if self._coll:
+                rows = torch.empty((G * kmax, D * W), dtype=torch.float32, device=self.device)
+                if self._gloo:
+                    host = [torch.empty((kmax, D * W), dtype=torch.float32) for _ in range(G)]
+                    dist.all_gather(host, buf.cpu())
+                    rows.copy_(torch.cat(host))
+                else:
+                    dist.all_gather_into_tensor(rows, buf)
+            else:
+                rows = buf
+            # row j of rank r's block -> global env r*E + (its j-th finished env)
+            within = done_all.to(torch.int64).cumsum(1) - 1
+            src = (torch.arange(G, device=self.device)[:, None] * kmax + within)[done_all]
+            out.view(G * E, D * W)[done_all.reshape(-1)] = rows[src]
+            self.terminal_bytes += G * kmax * D * W * 4
+            return out
+        # "gather": point-to-point from every rank that has finished envs to the learner
+        if self.is_learner:
+            ops, blocks = [], {}
+            for r in range(G):
+                if r == self.rank or counts[r] == 0:
+                    continue
+                blk = torch.empty((counts[r], D * W), dtype=torch.float32,
+                                  device="cpu" if self._gloo else self.device)
+                blocks[r] = blk
+                ops.append(dist.P2POp(dist.irecv, blk, r))
+            if ops:
+                for w in dist.batch_isend_irecv(ops):
+                    w.wait()
+            done_all_flat = done_all.reshape(G, E)
+            dst = out.view(G, E, D * W)
+            for r in range(G):
+                if counts[r] == 0:
+                    continue
+                rows = lrows[ldone] if r == self.rank else blocks[r].to(self.device)
+                dst[r][done_all_flat[r]] = rows
+                self.terminal_bytes += counts[r] * D * W * 4
+            return out
+        k = int(ldone.sum().item())                       # host sync: this rank's count
+        if k:
+            rows = lrows[ldone].contiguous()
+            dist.send(rows.cpu() if self._gloo else rows, self.learner)
+        return None
 
     def _views(self):
         """The learner's global batch, reassembled from the gathered packs (rank order)."""
-        G, E, D = self.world, self.count, self.sim.drones_per_env
-        W = self.sim.obs_width
-        packs = self.pack_all.view(G, self.nbytes)
-
-        def field(name, dtype, shape):
-            off, n = self.layout[name]
-            return packs[:, off:off + n].contiguous().view(dtype).reshape((G * E,) + shape)
-
-        obs = field("obs", torch.float32, (D, W))
-        rew = field("reward", torch.float32, ())
-        te = field("terminated", torch.uint8, ())
-        tr = field("truncated", torch.uint8, ())
-        tobs = field("terminal_obs", torch.float32, (D, W)) if self.terminal_obs else None
-        return obs, rew, te, tr, tobs
+        D, W = self.sim.drones_per_env, self.sim.obs_width
+        obs = self._field("obs", torch.float32, (D, W))
+        rew = self._field("reward", torch.float32, ())
+        te = self._field("terminated", torch.uint8, ())
+        tr = self._field("truncated", torch.uint8, ())
+        return obs, rew, te, tr
 
     def reset(self):
         """Reset every shard; the learner receives the global initial observation [E, D, W]."""
         self.sim.reset()
-        self._gather()
-        return self._views()[0] if self.is_learner else None
+        self._gather_prefix()
+        return self._field("obs", torch.float32, (self.sim.drones_per_env, self.sim.obs_width)) \
+            if self.receives else None
 
     def step(self, global_actions=None):
         """One env.step of every env of every rank driven by the learner's ``global_actions``."""
         self._scatter_actions(global_actions)
         self.sim.step(self.local_actions, terminal_obs=self.terminal_obs)
-        self._gather()
-        return self._views() if self.is_learner else None
+        self._gather_prefix()
+        self.steps += 1
+        if self.receives:
+            obs, rew, te, tr = self._views()
+        else:
+            te = tr = None
+        tobs = self._terminal_rows(te, tr) if self.terminal_obs else None
+        if not self.receives:
+            return None
+        return obs, rew, te, tr, tobs

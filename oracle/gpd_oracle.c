@@ -21,6 +21,7 @@
  * reference cannot run here); pinned through the numpy oracle's analytic KATs.
  */
 #include <math.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -333,6 +334,16 @@ void orc_reset(orc_sim* S, float* obs) {
   }
 }
 
+/* allocation for the per-thread scratch: an out-of-memory oracle stops loudly */
+static void* xmalloc(size_t n) {
+  void* p = malloc(n);
+  if (!p) {
+    fprintf(stderr, "gpd_oracle: out of memory (%zu bytes)\n", n);
+    abort();
+  }
+  return p;
+}
+
 void orc_set_raw(orc_sim* S, const double* raw) { memcpy(S->raw, raw, sizeof(double) * 20 * S->N); }
 void orc_get_raw(const orc_sim* S, double* raw) { memcpy(raw, S->raw, sizeof(double) * 20 * S->N); }
 void orc_get_state20(const orc_sim* S, double* out) {
@@ -343,12 +354,17 @@ void orc_step(orc_sim* S, const float* actions, float* obs, float* reward, uint8
               float* terminal_obs, int nthreads) {
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel
+#endif
+  {
+  /* per-thread scratch, allocated once per call (not per env) */
+  const int D = S->D, A = S->A;
+  double* rpm = (double*)xmalloc(sizeof(double) * 4 * (size_t)D);
+  double* scratch = (double*)xmalloc(sizeof(double) * 20 * (size_t)D);
+#ifdef _OPENMP
+#pragma omp for schedule(static)
 #endif
   for (int e = 0; e < S->E; ++e) {
-    const int D = S->D, A = S->A;
-    double* rpm = (double*)malloc(sizeof(double) * 4 * (size_t)D);
-    double* scratch = (double*)malloc(sizeof(double) * 20 * (size_t)D);
     double* env = S->raw + (size_t)e * D * 20;
     for (int d = 0; d < D; ++d) {
       size_t n = (size_t)e * D + d;
@@ -392,19 +408,24 @@ void orc_step(orc_sim* S, const float* actions, float* obs, float* reward, uint8
         obs_row(S, e, d, env + (size_t)d * 20, obs + n * S->W);
       }
     }
-    free(rpm);
-    free(scratch);
+  }
+  free(rpm);
+  free(scratch);
   }
 }
 
 void orc_integrate(orc_sim* S, const double* rpm, int T, double* traj, int nthreads) {
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel
+#endif
+  {
+  const int D = S->D;
+  double* scratch = (double*)xmalloc(sizeof(double) * 20 * (size_t)D);
+#ifdef _OPENMP
+#pragma omp for schedule(static)
 #endif
   for (int e = 0; e < S->E; ++e) {
-    const int D = S->D;
-    double* scratch = (double*)malloc(sizeof(double) * 20 * (size_t)D);
     double* env = S->raw + (size_t)e * D * 20;
     for (int t = 0; t < T; ++t) {
       env_substep(S, env, rpm + ((size_t)t * S->N + (size_t)e * D) * 4, scratch);
@@ -412,6 +433,7 @@ void orc_integrate(orc_sim* S, const double* rpm, int T, double* traj, int nthre
         for (int d = 0; d < D; ++d)
           state20_row(env + (size_t)d * 20, traj + ((size_t)t * S->N + (size_t)e * D + d) * 20);
     }
-    free(scratch);
+  }
+  free(scratch);
   }
 }

@@ -110,52 +110,67 @@ class _PackedOracleShard:
             self._put(name, getattr(self.o, name))
 
 
-def _handoff_worker(rank, world, port, E, T, q):
+def _handoff_worker(rank, world, port, E, T, q, mode, force, ack):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from gym_pybullet_drones_routing_amd.shard import LearnerHandoff, env_shard
         _, count = env_shard(E, rank, world)
-        h = LearnerHandoff(_PackedOracleShard(count, task="hover"), E)
+        h = LearnerHandoff(_PackedOracleShard(count, task="hover"), E, mode=mode, force_collectives=force)
         rng = np.random.default_rng(1)
         acts = rng.uniform(-1, 1, (T, E, 1, 4)).astype(np.float32)
         acts[:, :2] *= 0.05                          # long-lived envs beside ones that end early
         outs = [h.reset()]
+        prev = None
         for t in range(T):
             # only the learner holds the action batch
             r = h.step(torch.from_numpy(acts[t]) if rank == 0 else None)
-            assert (r is None) == (rank != 0)
+            receives = rank == 0 or mode == "all_gather"
+            assert (r is None) == (not receives)
+            if prev is not None:                    # returned tensors are fresh, not views of a buffer
+                for x, xc in zip(*prev):
+                    np.testing.assert_array_equal(x.numpy(), xc)
             if rank == 0:
                 outs.append(tuple(x.numpy().copy() for x in r))
+                prev = (r, outs[-1])
         if rank == 0:
-            q.put((outs, h.bytes_per_step()))
+            q.put((outs, h.bytes_per_step(), h.stats()))
+            ack.wait(120)          # stay alive until the parent has read the whole message
     finally:
         dist.destroy_process_group()
 
 
-def test_learner_handoff_gloo_matches_one_process():
-    """Rank-0 learner scatters actions, shards step, one all-gather of the output packs: the
-    learner's batch (incl. terminal rows after auto-resets) equals one process stepping all envs."""
+@pytest.mark.parametrize("world,mode,force", [(2, "all_gather", False), (2, "gather", False),
+                                              (1, "all_gather", True), (1, "gather", True),
+                                              (1, "all_gather", False)])
+def test_learner_handoff_gloo_matches_one_process(world, mode, force):
+    """Rank-0 learner scatters actions, shards step, the output-pack prefixes are gathered (or
+    all-gathered) and the finished envs' terminal rows follow: the learner's batch (incl.
+    terminal rows after auto-resets) equals one process stepping all envs.  World size 1 with
+    and without forced collectives (the one-rank shortcut must still return fresh tensors)."""
     from oracle.c_oracle import COracle
-    E, T, world = 8, 40, 2
+    E, T = 8, 40
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
+    ack = ctx.Event()
     port = _free_port()
-    procs = [ctx.Process(target=_handoff_worker, args=(r, world, port, E, T, q)) for r in range(world)]
+    procs = [ctx.Process(target=_handoff_worker, args=(r, world, port, E, T, q, mode, force, ack))
+             for r in range(world)]
     for p in procs:
         p.start()
-    outs, (act_bytes, pack_bytes) = q.get(timeout=300)
+    outs, (act_bytes, pack_bytes), stats = q.get(timeout=300)
+    ack.set()
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert act_bytes == E * 4 * 4 and pack_bytes > 2 * E * 72 * 4
+    assert act_bytes == E * 4 * 4 and pack_bytes == world * _prefix_bytes(E // world)
     ref = COracle(n_envs=E, task="hover", threads=1)
     np.testing.assert_array_equal(outs[0], ref.reset())
     rng = np.random.default_rng(1)
     acts = rng.uniform(-1, 1, (T, E, 1, 4)).astype(np.float32)
     acts[:, :2] *= 0.05
-    n_done = 0
+    n_done, row_bytes = 0, 0
     for t in range(T):
         o, r, te, tr = ref.step(acts[t])
         obs, rew, gte, gtr, tobs = outs[t + 1]
@@ -166,4 +181,17 @@ def test_learner_handoff_gloo_matches_one_process():
         done = te | tr
         n_done += int(done.sum())
         np.testing.assert_array_equal(tobs[done], ref.terminal_obs[done])
+        assert not tobs[~done].any()                  # only finished envs' rows are sent
+        row_bytes += int(done.sum()) * 72 * 4
     assert n_done > 0
+    # terminal bytes: exactly the finished rows when gathered point to point; the all-gather
+    # pads every rank's block to the largest count of the step
+    if mode == "gather" or world == 1:
+        assert stats["terminal_bytes_avg"] * T == row_bytes
+    else:
+        assert row_bytes <= stats["terminal_bytes_avg"] * T <= world * row_bytes
+
+
+def _prefix_bytes(e):
+    from gym_pybullet_drones_routing_amd.sim import pack_layout
+    return pack_layout(e, 1, 72)["prefix"]

@@ -184,8 +184,8 @@ def test_gpu_reproduces_integrate_fixture(name, prec):
             assert err.max() <= TOL_CONTACT and np.median(err) <= 1e-10
         else:
             assert err.max() <= 1e-10
-    elif _integrator(fx) == "bullet":                 # float32 through chaotic landings: median
-        assert np.median(err) <= 1e-5
+    elif _integrator(fx) == "bullet":                 # float32 through chaotic landings: median,
+        assert np.median(err) <= 1e-5 and err.max() <= 5e-2   # and a generous bound on every drone
     else:
         assert np.median(err) <= 1e-5 and err.max() <= 1e-3
     sim.close()

@@ -29,16 +29,20 @@ def _actions(E, T, D, A, seed):
     return acts
 
 
-def _worker(rank, world, port, kw, E, T, q):
+def _worker(rank, world, port, kw, E, T, q, backend="gloo", mode="all_gather", ack=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    extra = {"device_id": torch.device("cuda:0")} if backend == "nccl" else {}
+    dist.init_process_group(backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60), **extra)
     try:
         from gym_pybullet_drones_routing_amd.shard import LearnerHandoff, env_shard
         from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
         _, count = env_shard(E, rank, world)
         sim = BatchedAviarySim(n_envs=count, device="cuda:0", **kw)
-        h = LearnerHandoff(sim, E)
+        # a one-rank group runs the real collectives (RCCL on the one-GPU box), not the local copy
+        h = LearnerHandoff(sim, E, mode=mode, force_collectives=True)
+        if backend == "nccl":
+            assert dist.get_backend() == "nccl"
         acts = _actions(E, T, sim.drones_per_env, sim.act_width, 5)
         o0 = h.reset()
         outs = [o0.cpu().numpy() if rank == 0 else None]
@@ -49,6 +53,8 @@ def _worker(rank, world, port, kw, E, T, q):
         sim.close()
         if rank == 0:
             q.put(outs)
+            if ack is not None:
+                ack.wait(120)      # stay alive until the parent has read the whole message
     finally:
         dist.destroy_process_group()
 
@@ -75,20 +81,23 @@ def _collect(q, procs, limit=150):
     return outs
 
 
-@pytest.mark.parametrize("kw", [
-    dict(task="hover"),
-    dict(task="multihover", drones_per_env=4, aero=("dw", "gnd", "drag")),
-], ids=["hover", "multihover4_dw"])
-def test_handoff_two_ranks_bit_identical_to_one_sim(kw):
-    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
-    E, T, world = 64, 260, 2          # 260 ctrl steps: past the 242-step time truncation
+def _run(kw, E, T, world, backend, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
+    ack = ctx.Event()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, kw, E, T, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kw, E, T, q, backend, mode, ack))
+             for r in range(world)]
     for p in procs:
         p.start()
-    outs = _collect(q, procs)
+    try:
+        return _collect(q, procs)
+    finally:
+        ack.set()
+
+
+def _check_against_one_sim(outs, kw, E, T):
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
     sim = BatchedAviarySim(n_envs=E, device="cuda:0", **kw)
     acts = _actions(E, T, sim.drones_per_env, sim.act_width, 5)
     np.testing.assert_array_equal(outs[0], sim.reset().cpu().numpy())
@@ -103,5 +112,29 @@ def test_handoff_two_ranks_bit_identical_to_one_sim(kw):
         done = (gte | gtr).astype(bool)
         n_done += int(done.sum())
         np.testing.assert_array_equal(tobs[done], sim.terminal_obs.cpu().numpy()[done])
+        assert not tobs[~done].any()
     sim.close()
     assert n_done > 0
+
+
+@pytest.mark.parametrize("kw,mode", [
+    (dict(task="hover"), "all_gather"),
+    (dict(task="hover"), "gather"),
+    (dict(task="multihover", drones_per_env=4, aero=("dw", "gnd", "drag")), "all_gather"),
+], ids=["hover", "hover_gather", "multihover4_dw"])
+def test_handoff_two_ranks_bit_identical_to_one_sim(kw, mode):
+    E, T, world = 64, 260, 2          # 260 ctrl steps: past the 242-step time truncation
+    outs = _run(kw, E, T, world, "gloo", mode)
+    _check_against_one_sim(outs, kw, E, T)
+
+
+@pytest.mark.parametrize("mode", ["all_gather", "gather"])
+def test_handoff_rccl_one_rank(mode):
+    """The RCCL code path of the hand-off (backend "nccl" = RCCL on ROCm) on the one-GPU box:
+    a one-rank group with the collectives forced on, so that dist.scatter, the prefix
+    gather / all_gather_into_tensor and the terminal-row all-gather of uint8 / float32 device
+    tensors really execute on RCCL.  Bit-identical to one sim stepping the same envs."""
+    kw = dict(task="hover")
+    E, T = 64, 260
+    outs = _run(kw, E, T, 1, "nccl", mode)
+    _check_against_one_sim(outs, kw, E, T)
