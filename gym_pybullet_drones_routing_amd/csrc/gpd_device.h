@@ -776,6 +776,149 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
   s.wz = any ? s.wz + pc_dot(Rm[6], Rm[7], Rm[8], da0, da1, da2) : s.wz;
 }
 
+// plane_contact with every row in VGPRs, for the kernels compiled for a PYB flag set (one-wave
+// blocks; at the PYB configs' sizes a block is one thin wave per CU, so registers cost no
+// occupancy).  The same solve, operation for operation:
+//   * setup once per solve: per point p and row j (normal n, friction u, e) the arm a = r_p x d_j
+//     (pc_arm, the zero components dropped), a . I^-1, jacDiag, 1/jacDiag and the rhs;
+//   * each iteration runs on registers only: no LDS round trip on the Gauss-Seidel chain, and no
+//     per-iteration recomputation of the (loop-invariant) arms;
+//   * rows nobody in the wave needs are skipped with a wave ballot: a normal row when no solving
+//     lane has point p in contact, a friction pair when no solving lane has a positive normal
+//     impulse at p (those rows solve to a zero impulse, as the oracle's skipped rows).
+// Drone 0 of a crashing batch typically touches with one or two rim points, and a solve that runs
+// into the iteration cap holds its whole launch, so both the per-iteration latency and the
+// skipped rows shorten the PYB step directly.
+template <typename R>
+__device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], const Consts<R>& c, const DynK<R>& k) {
+  const R nx = Rm[6], ny = Rm[7], nz = Rm[8];          // base-frame world +z
+  const R ux = -Rm[3], uy = -Rm[4], uz = -Rm[5];       // (0,-1,0)
+  const R ex = Rm[0], ey = Rm[1], ez = Rm[2];          // (1,0,0)
+  const R zc = (-Rm[8] < R(0) ? -c.cyl_hh : c.cyl_hh) + c.cyl_zoff;
+  const R cr = c.cyl_r;
+  const R vbx = pc_dot(Rm[0], Rm[3], Rm[6], s.vx, s.vy, s.vz);
+  const R vby = pc_dot(Rm[1], Rm[4], Rm[7], s.vx, s.vy, s.vz);
+  const R vbz = pc_dot(Rm[2], Rm[5], Rm[8], s.vx, s.vy, s.vz);
+  const R wbx = pc_dot(Rm[0], Rm[3], Rm[6], s.wx, s.wy, s.wz);
+  const R wby = pc_dot(Rm[1], Rm[4], Rm[7], s.wx, s.wy, s.wz);
+  const R wbz = pc_dot(Rm[2], Rm[5], Rm[8], s.wx, s.wy, s.wz);
+  const R dx[3] = {nx, ux, ex}, dy[3] = {ny, uy, ey}, dz[3] = {nz, uz, ez};
+  R ar[4][3][3];                        // arm per point and row (arm . I^-1 is formed per use:
+                                        // three products off the chain, and 72 fewer VGPRs)
+  R rhs[4][3], jdi[4][3], jdn[4], lam[4][3];
+  bool act[4];
+  bool any = false;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const R rx = p == 0 ? cr : (p == 2 ? -cr : R(0)), ry = p == 1 ? cr : (p == 3 ? -cr : R(0));
+    const R dist = s.pz + pc_dot(nx, ny, nz, rx, ry, zc);
+    const R wxp = s.px + pc_dot(Rm[0], Rm[1], Rm[2], rx, ry, zc);
+    const R wyp = s.py + pc_dot(Rm[3], Rm[4], Rm[5], rx, ry, zc);
+    act[p] = dist < c.brk && g_abs(wxp) <= c.plane_half && g_abs(wyp) <= c.plane_half;
+    any = any || act[p];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      R ax, ay, az;
+      if (p == 0) pc_arm<0>(cr, zc, dx[j], dy[j], dz[j], ax, ay, az);
+      if (p == 1) pc_arm<1>(cr, zc, dx[j], dy[j], dz[j], ax, ay, az);
+      if (p == 2) pc_arm<2>(cr, zc, dx[j], dy[j], dz[j], ax, ay, az);
+      if (p == 3) pc_arm<3>(cr, zc, dx[j], dy[j], dz[j], ax, ay, az);
+      ar[p][j][0] = ax; ar[p][j][1] = ay; ar[p][j][2] = az;
+      const R jd = k.inv_m + ((ax * (ax * k.ijx) + ay * (ay * k.ijy)) + az * (az * k.ijz));
+      const R inv = R(1) / jd;
+      const R rel = pc_dot(dx[j], dy[j], dz[j], vbx, vby, vbz) + pc_dot(ax, ay, az, wbx, wby, wbz);
+      R r;
+      if (j == 0) {
+        const R pen = dist + c.slop;
+        r = pen > R(0) ? (-rel - pen / k.dt) * inv : (-pen * c.erp / k.dt - rel) * inv;
+        jdn[p] = act[p] ? jd : R(0);
+      } else {
+        r = -rel * inv;
+      }
+      jdi[p][j] = act[p] ? inv : R(0);
+      rhs[p][j] = act[p] ? r : R(0);
+      lam[p][j] = R(0);
+    }
+  }
+  R dl0 = R(0), dl1 = R(0), dl2 = R(0), da0 = R(0), da1 = R(0), da2 = R(0);
+  bool done = !any;
+  const R mu = c.mu, resid = c.resid;
+  const int iters = c.iters;
+#ifdef GPD_CONTACT_STATS
+  int it_used = 0;
+  const unsigned long long nact = __ballot(any);
+#endif
+  for (int it = 0; it < iters; ++it) {
+    if (__ballot(!done) == 0ull) break;
+#ifdef GPD_CONTACT_STATS
+    it_used = it + 1;
+#endif
+    if (!done) {
+      R res = R(0);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {                  // normal rows
+        if (__ballot(act[p]) == 0ull) continue;      // wave-uniform: no solving lane touches at p
+        // vpin: the products arm . I^-1 stay inside the loop (hoisted, they would need 72 VGPRs)
+        const R ax = vpin(ar[p][0][0]), ay = vpin(ar[p][0][1]), az = vpin(ar[p][0][2]);
+        const R jv = pc_dot(nx, ny, nz, dl0, dl1, dl2) + pc_dot(ax, ay, az, da0, da1, da2);
+        R delta = rhs[p][0] - jdi[p][0] * jv;
+        const R sum = lam[p][0] + delta;
+        const bool neg = sum < R(0);
+        delta = neg ? -lam[p][0] : delta;
+        lam[p][0] = neg ? R(0) : sum;
+        const R dm = k.inv_m * delta;
+        dl0 = dl0 + nx * dm; dl1 = dl1 + ny * dm; dl2 = dl2 + nz * dm;
+        da0 = da0 + (ax * k.ijx) * delta; da1 = da1 + (ay * k.ijy) * delta; da2 = da2 + (az * k.ijz) * delta;
+        const R rr = delta * jdn[p];
+        res = g_fmax(res, rr * rr);   // the oracle's max(res, x); x = rr^2 is never -0, NaN keeps res
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {                  // friction pairs on the cone
+        const R lnrm = lam[p][0];
+        const bool on = lnrm > R(0);
+        if (__ballot(on) == 0ull) continue;          // wave-uniform: no positive normal impulse at p
+        const R bx = vpin(ar[p][1][0]), by = vpin(ar[p][1][1]), bz = vpin(ar[p][1][2]);
+        const R cx = vpin(ar[p][2][0]), cy = vpin(ar[p][2][1]), cz = vpin(ar[p][2][2]);
+        const R lim = mu * lnrm;
+        const R l1 = lam[p][1], l2 = lam[p][2];
+        const R j1 = pc_dot(ux, uy, uz, dl0, dl1, dl2) + pc_dot(bx, by, bz, da0, da1, da2);
+        const R j2 = pc_dot(ex, ey, ez, dl0, dl1, dl2) + pc_dot(cx, cy, cz, da0, da1, da2);
+        R s1 = l1 + (rhs[p][1] - jdi[p][1] * j1);
+        R s2 = l2 + (rhs[p][2] - jdi[p][2] * j2);
+        const R m2 = s1 * s1 + s2 * s2;
+        const bool clip = m2 > lim * lim;
+        const R f = clip ? lim * g_rsqrt(clip ? m2 : R(1)) : R(1);
+        s1 = s1 * f;
+        s2 = s2 * f;
+        const R d1 = on ? s1 - l1 : R(0);
+        const R d2 = on ? s2 - l2 : R(0);
+        lam[p][1] = on ? s1 : l1;
+        lam[p][2] = on ? s2 : l2;
+        const R m1 = k.inv_m * d1, m2v = k.inv_m * d2;
+        dl0 = dl0 + ux * m1; dl1 = dl1 + uy * m1; dl2 = dl2 + uz * m1;
+        da0 = da0 + (bx * k.ijx) * d1; da1 = da1 + (by * k.ijy) * d1; da2 = da2 + (bz * k.ijz) * d1;
+        dl0 = dl0 + ex * m2v; dl1 = dl1 + ey * m2v; dl2 = dl2 + ez * m2v;
+        da0 = da0 + (cx * k.ijx) * d2; da1 = da1 + (cy * k.ijy) * d2; da2 = da2 + (cz * k.ijz) * d2;
+        const R rr = (d1 + d2) * (d1 + d2);
+        res = g_fmax(res, rr);
+      }
+      done = res <= resid;
+    }
+  }
+#ifdef GPD_CONTACT_STATS
+  if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) {
+    atomicAdd(&g_pc_hist[it_used], 1ull);
+    atomicAdd(&g_pc_hist[51 + __popcll(nact)], 1ull);
+  }
+#endif
+  s.vx = any ? s.vx + pc_dot(Rm[0], Rm[1], Rm[2], dl0, dl1, dl2) : s.vx;
+  s.vy = any ? s.vy + pc_dot(Rm[3], Rm[4], Rm[5], dl0, dl1, dl2) : s.vy;
+  s.vz = any ? s.vz + pc_dot(Rm[6], Rm[7], Rm[8], dl0, dl1, dl2) : s.vz;
+  s.wx = any ? s.wx + pc_dot(Rm[0], Rm[1], Rm[2], da0, da1, da2) : s.wx;
+  s.wy = any ? s.wy + pc_dot(Rm[3], Rm[4], Rm[5], da0, da1, da2) : s.wy;
+  s.wz = any ? s.wz + pc_dot(Rm[6], Rm[7], Rm[8], da0, da1, da2) : s.wz;
+}
+
 // Lowest height of the contact candidates (the cap facing down, rim at 0/90/180/270 deg): the
 // wave gate of plane_contact.
 template <typename R>
@@ -853,7 +996,12 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, const R rpm[4], cons
   if (!pf_on<PF>(k.flags, F_NO_PLANE)) {
     const bool low = contact_low(s, Rm, c) < c.brk + R(1e-6);
     if (CW == 1) {
-      if (GPD_RARE(__ballot(low) != 0ull)) plane_contact<R>(s, Rm, c, k);
+      // compiled-in PYB flag sets: the register-resident solve; run-time flags (every other
+      // combination, whose kernels also serve non-contact configs) keep the LDS rows
+      if (GPD_RARE(__ballot(low) != 0ull)) {
+        if (PF != kPfRuntime) plane_contact_regs<R>(s, Rm, c, k);
+        else plane_contact<R>(s, Rm, c, k);
+      }
     } else {
       // multi-wave workgroups (envs of more than 64 drones, step_kernel_wide): the LDS rows hold
       // one wave's lanes, so the waves take turns (the whole workgroup runs this code)

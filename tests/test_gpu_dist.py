@@ -59,7 +59,7 @@ def _worker(rank, world, port, kw, E, T, q, backend="gloo", mode="all_gather", a
         dist.destroy_process_group()
 
 
-def _collect(q, procs, limit=150):
+def _collect(q, procs, limit=150, ack=None):
     """Rank 0's result; fails as soon as a rank dies instead of waiting out the collective."""
     for _ in range(limit):
         try:
@@ -75,6 +75,8 @@ def _collect(q, procs, limit=150):
         for p in procs:
             p.kill()
         raise AssertionError("ranks did not finish")
+    if ack is not None:
+        ack.set()                 # rank 0 may exit now that its message has been read
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -91,7 +93,7 @@ def _run(kw, E, T, world, backend, mode):
     for p in procs:
         p.start()
     try:
-        return _collect(q, procs)
+        return _collect(q, procs, ack=ack)
     finally:
         ack.set()
 
