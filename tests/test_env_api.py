@@ -160,13 +160,14 @@ def test_per_env_reward_is_the_fp64_reference_value(num_drones):
         _, rr, rte, rtr, _ = ref.step(a)
         assert isinstance(r, float)
         # bit for bit the reference's fp64 formula on the GPU's own state, and the oracle's
-        # value to the positions' rounding (|r| ~ 1: a few ulp)
+        # value within what the state gate (1e-10 relative) allows: the open-loop positions drift
+        # apart by ~1e-15 per step
         pos = env.sim.raw_state().cpu().numpy()[:, 0:3]
         exp = 0
         for i in range(num_drones):
             exp += max(0, 2 - np.linalg.norm(env.TARGET_POS.reshape(num_drones, 3)[i] - pos[i]) ** 4)
         assert r == exp, (t, r, exp)
-        assert abs(r - rr) <= 1e-14 * max(1.0, abs(rr)), (t, r, rr)
+        assert abs(r - rr) <= 1e-12 * max(1.0, abs(rr)), (t, r, rr)
         assert (te, tr) == (rte, rtr)
         n_f32_differs += float(np.float32(rr)) != rr
         if te or tr:
