@@ -776,57 +776,68 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
   s.wz = any ? s.wz + pc_dot(Rm[6], Rm[7], Rm[8], da0, da1, da2) : s.wz;
 }
 
-// plane_contact with every row in VGPRs, for the kernels compiled for a PYB flag set (one-wave
-// blocks; at the PYB configs' sizes a block is one thin wave per CU, so registers cost no
-// occupancy).  The same solve, operation for operation:
-//   * setup once per solve: per point p and row j (normal n, friction u, e) the arm a = r_p x d_j
-//     (pc_arm, the zero components dropped), a . I^-1, jacDiag, 1/jacDiag and the rhs;
-//   * each iteration runs on registers only: no LDS round trip on the Gauss-Seidel chain, and no
-//     per-iteration recomputation of the (loop-invariant) arms;
+// plane_contact solved in WORLD coordinates with every row in VGPRs, for the kernels compiled for
+// a PYB flag set (one-wave blocks; at the PYB configs' sizes a block is one thin wave per CU, so
+// registers cost no occupancy).  The same projected Gauss-Seidel solve - same rows, order,
+// projections and stopping rule - in the frame where the rows are sparse.  The row directions
+// are the world axes (+z, (0,-1,0), (1,0,0)); with the solver's velocity changes kept in world
+// coordinates (DL = R dl, DA = R da) a row's Jacobian product d.DL + (r x d).DA has ONE linear
+// and TWO angular terms (r = the rim point's world arm), and a linear update touches one
+// component.  Per row the base-frame products of the LDS solve (two 3-term dot products, three
+// linear and three angular updates, the arm . I^-1 products) become 2 FMAs + 1 + 3 FMAs with
+// g = I_w^-1 (r x d), I_w^-1 = R diag(1/I) R^T formed once per solve.  In exact arithmetic every
+// quantity equals the base-frame one (R is orthonormal); the results differ by rounding only
+// (tests/test_gpu_bullet.py's resynced and long-run contact gates).
 //   * rows nobody in the wave needs are skipped with a wave ballot: a normal row when no solving
 //     lane has point p in contact, a friction pair when no solving lane has a positive normal
-//     impulse at p (those rows solve to a zero impulse, as the oracle's skipped rows).
-// Drone 0 of a crashing batch typically touches with one or two rim points, and a solve that runs
-// into the iteration cap holds its whole launch, so both the per-iteration latency and the
-// skipped rows shorten the PYB step directly.
+//     impulse at p (those rows solve to a zero impulse, as the oracle's skipped rows);
+//   * residual: the largest |row residual| is squared once per iteration (squaring is monotonic,
+//     so this equals the largest squared residual exactly).
+// A crashing batch's solves touch with one or two rim points and a few run into the iteration
+// cap (50); such a solve holds its whole launch, so the per-iteration instruction count is what
+// the PYB step time follows.
 template <typename R>
 __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], const Consts<R>& c, const DynK<R>& k) {
-  const R nx = Rm[6], ny = Rm[7], nz = Rm[8];          // base-frame world +z
-  const R ux = -Rm[3], uy = -Rm[4], uz = -Rm[5];       // (0,-1,0)
-  const R ex = Rm[0], ey = Rm[1], ez = Rm[2];          // (1,0,0)
   const R zc = (-Rm[8] < R(0) ? -c.cyl_hh : c.cyl_hh) + c.cyl_zoff;
   const R cr = c.cyl_r;
-  const R vbx = pc_dot(Rm[0], Rm[3], Rm[6], s.vx, s.vy, s.vz);
-  const R vby = pc_dot(Rm[1], Rm[4], Rm[7], s.vx, s.vy, s.vz);
-  const R vbz = pc_dot(Rm[2], Rm[5], Rm[8], s.vx, s.vy, s.vz);
-  const R wbx = pc_dot(Rm[0], Rm[3], Rm[6], s.wx, s.wy, s.wz);
-  const R wby = pc_dot(Rm[1], Rm[4], Rm[7], s.wx, s.wy, s.wz);
-  const R wbz = pc_dot(Rm[2], Rm[5], Rm[8], s.wx, s.wy, s.wz);
-  const R dx[3] = {nx, ux, ex}, dy[3] = {ny, uy, ey}, dz[3] = {nz, uz, ez};
-  R ar[4][3][3];                        // arm per point and row (arm . I^-1 is formed per use:
-                                        // three products off the chain, and 72 fewer VGPRs)
+  // world inverse inertia I_w^-1 = R diag(1/I) R^T (symmetric)
+  const R q00 = k.ijx * Rm[0], q01 = k.ijy * Rm[1], q02 = k.ijz * Rm[2];
+  const R q10 = k.ijx * Rm[3], q11 = k.ijy * Rm[4], q12 = k.ijz * Rm[5];
+  const R q20 = k.ijx * Rm[6], q21 = k.ijy * Rm[7], q22 = k.ijz * Rm[8];
+  const R i00 = pc_dot(q00, q01, q02, Rm[0], Rm[1], Rm[2]);
+  const R i01 = pc_dot(q00, q01, q02, Rm[3], Rm[4], Rm[5]);
+  const R i02 = pc_dot(q00, q01, q02, Rm[6], Rm[7], Rm[8]);
+  const R i11 = pc_dot(q10, q11, q12, Rm[3], Rm[4], Rm[5]);
+  const R i12 = pc_dot(q10, q11, q12, Rm[6], Rm[7], Rm[8]);
+  const R i22 = pc_dot(q20, q21, q22, Rm[6], Rm[7], Rm[8]);
+  R rwx[4], rwy[4], rwz[4];              // world arms of the rim points
+  R g[4][3][3];                          // I_w^-1 (r x d) per point and row
   R rhs[4][3], jdi[4][3], jdn[4], lam[4][3];
   bool act[4];
   bool any = false;
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const R rx = p == 0 ? cr : (p == 2 ? -cr : R(0)), ry = p == 1 ? cr : (p == 3 ? -cr : R(0));
-    const R dist = s.pz + pc_dot(nx, ny, nz, rx, ry, zc);
-    const R wxp = s.px + pc_dot(Rm[0], Rm[1], Rm[2], rx, ry, zc);
-    const R wyp = s.py + pc_dot(Rm[3], Rm[4], Rm[5], rx, ry, zc);
-    act[p] = dist < c.brk && g_abs(wxp) <= c.plane_half && g_abs(wyp) <= c.plane_half;
+    rwx[p] = pc_dot(Rm[0], Rm[1], Rm[2], rx, ry, zc);
+    rwy[p] = pc_dot(Rm[3], Rm[4], Rm[5], rx, ry, zc);
+    rwz[p] = pc_dot(Rm[6], Rm[7], Rm[8], rx, ry, zc);
+    const R dist = s.pz + rwz[p];
+    act[p] = dist < c.brk && g_abs(s.px + rwx[p]) <= c.plane_half && g_abs(s.py + rwy[p]) <= c.plane_half;
     any = any || act[p];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      R ax, ay, az;
-      if (p == 0) pc_arm<0>(cr, zc, dx[j], dy[j], dz[j], ax, ay, az);
-      if (p == 1) pc_arm<1>(cr, zc, dx[j], dy[j], dz[j], ax, ay, az);
-      if (p == 2) pc_arm<2>(cr, zc, dx[j], dy[j], dz[j], ax, ay, az);
-      if (p == 3) pc_arm<3>(cr, zc, dx[j], dy[j], dz[j], ax, ay, az);
-      ar[p][j][0] = ax; ar[p][j][1] = ay; ar[p][j][2] = az;
-      const R jd = k.inv_m + ((ax * (ax * k.ijx) + ay * (ay * k.ijy)) + az * (az * k.ijz));
+      // world angular Jacobian a = r x d:  +z: (ry, -rx, 0);  (0,-1,0): (rz, 0, -rx);  (1,0,0): (0, rz, -ry)
+      const R ax = j == 0 ? rwy[p] : (j == 1 ? rwz[p] : R(0));
+      const R ay = j == 0 ? -rwx[p] : (j == 1 ? R(0) : rwz[p]);
+      const R az = j == 0 ? R(0) : (j == 1 ? -rwx[p] : -rwy[p]);
+      const R gx = pc_dot(i00, i01, i02, ax, ay, az);
+      const R gy = pc_dot(i01, i11, i12, ax, ay, az);
+      const R gz = pc_dot(i02, i12, i22, ax, ay, az);
+      g[p][j][0] = gx; g[p][j][1] = gy; g[p][j][2] = gz;
+      const R jd = k.inv_m + pc_dot(ax, ay, az, gx, gy, gz);
       const R inv = R(1) / jd;
-      const R rel = pc_dot(dx[j], dy[j], dz[j], vbx, vby, vbz) + pc_dot(ax, ay, az, wbx, wby, wbz);
+      const R vl = j == 0 ? s.vz : (j == 1 ? -s.vy : s.vx);
+      const R rel = vl + pc_dot(ax, ay, az, s.wx, s.wy, s.wz);
       R r;
       if (j == 0) {
         const R pen = dist + c.slop;
@@ -840,9 +851,9 @@ __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], c
       lam[p][j] = R(0);
     }
   }
-  R dl0 = R(0), dl1 = R(0), dl2 = R(0), da0 = R(0), da1 = R(0), da2 = R(0);
+  R DLx = R(0), DLy = R(0), DLz = R(0), DAx = R(0), DAy = R(0), DAz = R(0);
   bool done = !any;
-  const R mu = c.mu, resid = c.resid;
+  const R mu = c.mu, resid = c.resid, im = k.inv_m;
   const int iters = c.iters;
 #ifdef GPD_CONTACT_STATS
   int it_used = 0;
@@ -858,35 +869,31 @@ __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], c
 #pragma unroll
       for (int p = 0; p < 4; ++p) {                  // normal rows
         if (__ballot(act[p]) == 0ull) continue;      // wave-uniform: no solving lane touches at p
-        // vpin: the products arm . I^-1 stay inside the loop (hoisted, they would need 72 VGPRs)
-        const R ax = vpin(ar[p][0][0]), ay = vpin(ar[p][0][1]), az = vpin(ar[p][0][2]);
-        const R jv = pc_dot(nx, ny, nz, dl0, dl1, dl2) + pc_dot(ax, ay, az, da0, da1, da2);
+        const R jv = DLz + (rwy[p] * DAx - rwx[p] * DAy);
         R delta = rhs[p][0] - jdi[p][0] * jv;
         const R sum = lam[p][0] + delta;
         const bool neg = sum < R(0);
         delta = neg ? -lam[p][0] : delta;
         lam[p][0] = neg ? R(0) : sum;
-        const R dm = k.inv_m * delta;
-        dl0 = dl0 + nx * dm; dl1 = dl1 + ny * dm; dl2 = dl2 + nz * dm;
-        da0 = da0 + (ax * k.ijx) * delta; da1 = da1 + (ay * k.ijy) * delta; da2 = da2 + (az * k.ijz) * delta;
-        const R rr = delta * jdn[p];
-        res = g_fmax(res, rr * rr);   // the oracle's max(res, x); x = rr^2 is never -0, NaN keeps res
+        DLz = DLz + im * delta;
+        DAx = DAx + g[p][0][0] * delta; DAy = DAy + g[p][0][1] * delta; DAz = DAz + g[p][0][2] * delta;
+        res = g_fmax(res, g_abs(delta * jdn[p]));   // NaN keeps res, as the oracle's max
       }
 #pragma unroll
       for (int p = 0; p < 4; ++p) {                  // friction pairs on the cone
         const R lnrm = lam[p][0];
         const bool on = lnrm > R(0);
         if (__ballot(on) == 0ull) continue;          // wave-uniform: no positive normal impulse at p
-        const R bx = vpin(ar[p][1][0]), by = vpin(ar[p][1][1]), bz = vpin(ar[p][1][2]);
-        const R cx = vpin(ar[p][2][0]), cy = vpin(ar[p][2][1]), cz = vpin(ar[p][2][2]);
         const R lim = mu * lnrm;
         const R l1 = lam[p][1], l2 = lam[p][2];
-        const R j1 = pc_dot(ux, uy, uz, dl0, dl1, dl2) + pc_dot(bx, by, bz, da0, da1, da2);
-        const R j2 = pc_dot(ex, ey, ez, dl0, dl1, dl2) + pc_dot(cx, cy, cz, da0, da1, da2);
+        const R j1 = (rwz[p] * DAx - rwx[p] * DAz) - DLy;
+        const R j2 = (rwz[p] * DAy - rwy[p] * DAz) + DLx;
         R s1 = l1 + (rhs[p][1] - jdi[p][1] * j1);
         R s2 = l2 + (rhs[p][2] - jdi[p][2] * j2);
         const R m2 = s1 * s1 + s2 * s2;
         const bool clip = m2 > lim * lim;
+        // onto the cone: (s1, s2) * lim / |s| (a select, and the Newton-refined rsqrt instead of a
+        // square root and a divide; within ~2 ulp of them)
         const R f = clip ? lim * g_rsqrt(clip ? m2 : R(1)) : R(1);
         s1 = s1 * f;
         s2 = s2 * f;
@@ -894,15 +901,13 @@ __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], c
         const R d2 = on ? s2 - l2 : R(0);
         lam[p][1] = on ? s1 : l1;
         lam[p][2] = on ? s2 : l2;
-        const R m1 = k.inv_m * d1, m2v = k.inv_m * d2;
-        dl0 = dl0 + ux * m1; dl1 = dl1 + uy * m1; dl2 = dl2 + uz * m1;
-        da0 = da0 + (bx * k.ijx) * d1; da1 = da1 + (by * k.ijy) * d1; da2 = da2 + (bz * k.ijz) * d1;
-        dl0 = dl0 + ex * m2v; dl1 = dl1 + ey * m2v; dl2 = dl2 + ez * m2v;
-        da0 = da0 + (cx * k.ijx) * d2; da1 = da1 + (cy * k.ijy) * d2; da2 = da2 + (cz * k.ijz) * d2;
-        const R rr = (d1 + d2) * (d1 + d2);
-        res = g_fmax(res, rr);
+        DLy = DLy - im * d1;
+        DLx = DLx + im * d2;
+        DAx = DAx + g[p][1][0] * d1; DAy = DAy + g[p][1][1] * d1; DAz = DAz + g[p][1][2] * d1;
+        DAx = DAx + g[p][2][0] * d2; DAy = DAy + g[p][2][1] * d2; DAz = DAz + g[p][2][2] * d2;
+        res = g_fmax(res, g_abs(d1 + d2));
       }
-      done = res <= resid;
+      done = res * res <= resid;
     }
   }
 #ifdef GPD_CONTACT_STATS
@@ -911,12 +916,12 @@ __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], c
     atomicAdd(&g_pc_hist[51 + __popcll(nact)], 1ull);
   }
 #endif
-  s.vx = any ? s.vx + pc_dot(Rm[0], Rm[1], Rm[2], dl0, dl1, dl2) : s.vx;
-  s.vy = any ? s.vy + pc_dot(Rm[3], Rm[4], Rm[5], dl0, dl1, dl2) : s.vy;
-  s.vz = any ? s.vz + pc_dot(Rm[6], Rm[7], Rm[8], dl0, dl1, dl2) : s.vz;
-  s.wx = any ? s.wx + pc_dot(Rm[0], Rm[1], Rm[2], da0, da1, da2) : s.wx;
-  s.wy = any ? s.wy + pc_dot(Rm[3], Rm[4], Rm[5], da0, da1, da2) : s.wy;
-  s.wz = any ? s.wz + pc_dot(Rm[6], Rm[7], Rm[8], da0, da1, da2) : s.wz;
+  s.vx = any ? s.vx + DLx : s.vx;
+  s.vy = any ? s.vy + DLy : s.vy;
+  s.vz = any ? s.vz + DLz : s.vz;
+  s.wx = any ? s.wx + DAx : s.wx;
+  s.wy = any ? s.wy + DAy : s.wy;
+  s.wz = any ? s.wz + DAz : s.wz;
 }
 
 // Lowest height of the contact candidates (the cap facing down, rim at 0/90/180/270 deg): the
