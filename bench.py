@@ -461,9 +461,9 @@ def other_configs(device, precision, act):
 
 
 def hbm_copy_gbps(device, n=1 << 28, reps=5):
-    """Live ceiling beside the 8 TB/s spec: torch copy_ of n float32 (1 GiB, far past the 256 MB
-    Infinity Cache), bytes read + written per second (scripts/ubench/rw_mix.hip measures the
-    step's own read/write shape)."""
+    """torch copy_ of n float32 (1 GiB, far past the 256 MB Infinity Cache), bytes read + written
+    per second: reported beside the HIP ceiling below (torch's copy keeps one load per lane in
+    flight and measured ~5.0 TB/s where a deeper copy reaches ~6.1)."""
     x = torch.empty(n, device=device)
     y = torch.empty(n, device=device)
     y.copy_(x)
@@ -476,6 +476,32 @@ def hbm_copy_gbps(device, n=1 << 28, reps=5):
     del x, y
     torch.cuda.empty_cache()
     return 2 * n * 4 / el / 1e9
+
+
+HBM_CEILING_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "ubench", "libhbm_ceiling.so")
+
+
+def hbm_ceiling(device):
+    """The achievable HBM rate on this box, measured live (scripts/ubench/hbm_ceiling.hip,
+    built in-tree as libhbm_ceiling.so): coalesced float4 copy / read-only streams far past the
+    Infinity Cache, best over 1-8 loads in flight per lane, plain or nontemporal, 1-8 blocks of 256
+    threads per CU (MI355X_MICROARCH.md: 6.29 TB/s for a float4 copy).  None when the library is
+    absent (the torch copy_ figure stays beside it)."""
+    if not os.path.exists(HBM_CEILING_LIB):
+        return None
+    import ctypes
+    lib = ctypes.CDLL(HBM_CEILING_LIB)
+    lib.hbm_ceiling_gbps.restype = ctypes.c_double
+    lib.hbm_ceiling_gbps.argtypes = [ctypes.c_int, ctypes.c_int]
+    with torch.cuda.device(device):
+        copy = lib.hbm_ceiling_gbps(0, 0)
+        read = lib.hbm_ceiling_gbps(1, 0)
+    torch.cuda.empty_cache()
+    if copy <= 0 or read <= 0:
+        return None
+    return {"copy_GBps": copy, "read_GBps": read,
+            "source": "scripts/ubench/hbm_ceiling.hip (float4 streams, 704 MB per launch, best of the "
+                      "in-flight-depth x policy x blocks-per-CU sweep)"}
 
 
 def raw_integrator(device, precision, n_drones=1 << 20, n_sub=32):
@@ -724,11 +750,20 @@ def run(args):
             s2.close()
             del p2
             torch.cuda.empty_cache()
-        copy = hbm_copy_gbps(device)
+        torch_copy = hbm_copy_gbps(device)
+        ceil = hbm_ceiling(device)
+        copy = ceil["copy_GBps"] if ceil else torch_copy
         for row in sweep:
             row["frac_of_copy"] = row["achieved_GBps"] / copy
+            if row["n_envs"] * alg_bytes_per_drone_step(args.act, rbytes) < 256 * 2 ** 20:
+                # the whole working set fits the 256 MB Infinity Cache: not an HBM measurement
+                row["mall_resident"] = True
+                row["frac"] = None
+                row["frac_of_copy"] = None
         result["sweep"] = sweep
         result["hbm_copy_GBps"] = copy
+        result["hbm_copy_torch_GBps"] = torch_copy
+        result["hbm_ceiling"] = ceil
 
     if rank == 0 and world == 1 and not args.no_sweep:
         import warnings

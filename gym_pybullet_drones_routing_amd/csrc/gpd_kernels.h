@@ -91,14 +91,17 @@ __device__ unsigned long long g_stamps[65536 * kStampPhases];
 // memory when the wave stores them, so less of that write-back is left for the kernel's end.
 typedef int gpd_v4i __attribute__((ext_vector_type(4)));
 typedef unsigned gpd_v2u __attribute__((ext_vector_type(2)));
+#ifndef GPD_WT_AUX
+#define GPD_WT_AUX 16   // sc1 (write-through); diagnostic builds try other cache-policy bits
+#endif
 __device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, int off, float4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gpd_v4i, v), r, off, 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gpd_v4i, v), r, off, 0, GPD_WT_AUX);
 }
 __device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, int off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, GPD_WT_AUX);
 }
 __device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, int off, double v) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(gpd_v2u, v), r, off, 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(gpd_v2u, v), r, off, 0, GPD_WT_AUX);
 }
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
@@ -485,19 +488,26 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
   rpm_wrench<R, PF>(rpm, dk, c, W);
   // substeps 1..nsub-1 skip the (write-only) world ang_v; the last one produces it
   // (the first substep is peeled so the loop body stays one basic block)
+#ifdef GPD_DMA_EARLY
+  history_dma();   // diagnostic build: the DMA behind the state loads instead of the first substep
+#endif
   if (dk.nsub > 1) {
     substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
     GPD_STAMP(1);
+#ifndef GPD_DMA_EARLY
     history_dma();
+#endif
     for (int it = 1; it < dk.nsub - 1; ++it)
       substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
   }
   substep_block<R, MULTI, PF, true>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
 #pragma unroll
   for (int k = 0; k < 4; ++k) last[k] = rpm[k];
+#ifndef GPD_DMA_EARLY
   if (dk.nsub == 1) history_dma();
+#endif
   GPD_STAMP(2);
   // final readback (:374) -> obs / reward / done
   R qn[4], Rm[9];

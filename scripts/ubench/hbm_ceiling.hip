@@ -16,6 +16,7 @@
       return -1.0;                                                                    \
     }                                                                                 \
   } while (0)
+// (also built as libhbm_ceiling.so with -DHBM_CEILING_LIB -shared -fPIC: hbm_ceiling_gbps below)
 
 template <bool NT>
 __device__ __forceinline__ float4 ld(const float4* p) {
@@ -93,7 +94,7 @@ double run(float4* src, float4* dst, long long n, int blocks) {
 }
 
 template <int R, int W>
-void shape(const char* name, float4* src, float4* dst, long long n) {
+double shape(const char* name, float4* src, float4* dst, long long n, bool print) {
   double best = 0;
   int bu = 0, bb = 0, bnt = 0;
   for (int bpc : {1, 2, 4, 8}) {
@@ -107,27 +108,40 @@ void shape(const char* name, float4* src, float4* dst, long long n) {
     g[5] = run<R, W, 2, true>(src, dst, n, blocks);
     g[6] = run<R, W, 4, true>(src, dst, n, blocks);
     g[7] = run<R, W, 8, true>(src, dst, n, blocks);
-    std::printf("%-14s %d blocks/CU  plain U=1,2,4,8: %6.0f %6.0f %6.0f %6.0f   nt: %6.0f %6.0f %6.0f %6.0f GB/s\n",
-                name, bpc, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7]);
+    if (print)
+      std::printf("%-14s %d blocks/CU  plain U=1,2,4,8: %6.0f %6.0f %6.0f %6.0f   nt: %6.0f %6.0f %6.0f %6.0f GB/s\n",
+                  name, bpc, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7]);
     for (int k = 0; k < 8; ++k)
       if (g[k] > best) { best = g[k]; bu = 1 << (k & 3); bb = bpc; bnt = k >= 4; }
   }
-  std::printf("BEST %-14s %6.0f GB/s  (U=%d, %d blocks/CU, %s)\n", name, best, bu, bb, bnt ? "nt" : "plain");
+  if (print) std::printf("BEST %-14s %6.0f GB/s  (U=%d, %d blocks/CU, %s)\n", name, best, bu, bb, bnt ? "nt" : "plain");
+  return best;
 }
 
-int main() {
-  // 22 read streams + 29 write streams of n float4 with n = 1M: 352 MB + 464 MB, like 1M drones
+// shape 0: copy 1:1, 1: read 1:0, 2: fill 0:1, 3: the step's 22:29; returns the best GB/s of the
+// sweep (bench.py loads this as libhbm_ceiling.so: the large-N rows' achievable ceiling)
+extern "C" double hbm_ceiling_gbps(int which, int print) {
   const long long n = 1 << 20;
   float4 *src = nullptr, *dst = nullptr;
-  if (hipMalloc(&src, 22 * n * sizeof(float4)) != hipSuccess || hipMalloc(&dst, 29 * n * sizeof(float4)) != hipSuccess)
-    return 1;
-  if (hipMemset(src, 0, 22 * n * sizeof(float4)) != hipSuccess || hipMemset(dst, 0, 29 * n * sizeof(float4)) != hipSuccess)
-    return 1;
-  shape<1, 1>("copy 1:1", src, dst, 22 * n);
-  shape<1, 0>("read 1:0", src, dst, 22 * n);
-  shape<0, 1>("fill 0:1", src, dst, 29 * n);
-  shape<22, 29>("step 22:29", src, dst, n);
+  if (hipMalloc(&src, 22 * n * sizeof(float4)) != hipSuccess) return -1;
+  if (hipMalloc(&dst, 29 * n * sizeof(float4)) != hipSuccess) { (void)hipFree(src); return -1; }
+  (void)hipMemset(src, 0, 22 * n * sizeof(float4));
+  (void)hipMemset(dst, 0, 29 * n * sizeof(float4));
+  double r = -1;
+  if (which == 0) r = shape<1, 1>("copy 1:1", src, dst, 22 * n, print);
+  if (which == 1) r = shape<1, 0>("read 1:0", src, dst, 22 * n, print);
+  if (which == 2) r = shape<0, 1>("fill 0:1", src, dst, 29 * n, print);
+  if (which == 3) r = shape<22, 29>("step 22:29", src, dst, n, print);
+  (void)hipDeviceSynchronize();
   (void)hipFree(src);
   (void)hipFree(dst);
+  return r;
+}
+
+#ifndef HBM_CEILING_LIB
+int main() {
+  for (int k = 0; k < 4; ++k)
+    if (hbm_ceiling_gbps(k, 1) < 0) return 1;
   return 0;
 }
+#endif
