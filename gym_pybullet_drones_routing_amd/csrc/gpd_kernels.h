@@ -91,6 +91,9 @@ __device__ unsigned long long g_stamps[65536 * kStampPhases];
 // memory when the wave stores them, so less of that write-back is left for the kernel's end.
 typedef int gpd_v4i __attribute__((ext_vector_type(4)));
 typedef unsigned gpd_v2u __attribute__((ext_vector_type(2)));
+#ifndef GPD_DMA_AUX
+#define GPD_DMA_AUX 0    // cache policy of the single-wave step kernel's history LDS-DMA
+#endif
 #ifndef GPD_WT_AUX
 #define GPD_WT_AUX 16   // sc1 (write-through); diagnostic builds try other cache-policy bits
 #endif
@@ -157,13 +160,18 @@ __host__ __device__ __forceinline__ long long ridx(long long n, int slot, int L,
 }
 
 // Only what the dynamics reads: ang_v is write-only, last_clipped_action is read only by drag.
+#ifdef GPD_LOAD_NT
+template <typename R> __device__ __forceinline__ R ldst(const R* p) { return __builtin_nontemporal_load(p); }
+#else
+template <typename R> __device__ __forceinline__ R ldst(const R* p) { return *p; }
+#endif
 template <typename R>
 __device__ __forceinline__ void load_drone(const SimView<R>& v, long long n, Drone<R>& s, R last[4], bool need_last) {
   const R* st = v.state + tidx(n, 0, kStateComps);
-  s.px = st[0 * 64]; s.py = st[1 * 64]; s.pz = st[2 * 64];
-  s.qx = st[3 * 64]; s.qy = st[4 * 64]; s.qz = st[5 * 64]; s.qw = st[6 * 64];
-  s.vx = st[7 * 64]; s.vy = st[8 * 64]; s.vz = st[9 * 64];
-  s.wx = st[10 * 64]; s.wy = st[11 * 64]; s.wz = st[12 * 64];
+  s.px = ldst(st + 0 * 64); s.py = ldst(st + 1 * 64); s.pz = ldst(st + 2 * 64);
+  s.qx = ldst(st + 3 * 64); s.qy = ldst(st + 4 * 64); s.qz = ldst(st + 5 * 64); s.qw = ldst(st + 6 * 64);
+  s.vx = ldst(st + 7 * 64); s.vy = ldst(st + 8 * 64); s.vz = ldst(st + 9 * 64);
+  s.wx = ldst(st + 10 * 64); s.wy = ldst(st + 11 * 64); s.wz = ldst(st + 12 * 64);
   s.ax = s.ay = s.az = R(0);
   if (need_last) {
     last[0] = st[16 * 64]; last[1] = st[17 * 64]; last[2] = st[18 * 64]; last[3] = st[19 * 64];
@@ -474,12 +482,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
       slot -= slot >= v.ring_len ? v.ring_len : 0;
       const float* src = v.ring + ridx(nn, slot, v.ring_len, A);
       if (A == 4) {
-        __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tile4 + (3 + k) * kPad), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tile4 + (3 + k) * kPad), 16, 0, GPD_DMA_AUX);
       } else {
 #pragma unroll
         for (int j = 0; j < A; ++j)
           __builtin_amdgcn_global_load_lds((gbl_void_ptr)(src + j), (lds_void_ptr)(tilef + (12 + k * A + j) * kPad), 4,
-                                           0, 0);
+                                           0, GPD_DMA_AUX);
       }
     }
   };
