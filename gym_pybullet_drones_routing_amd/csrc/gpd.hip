@@ -119,6 +119,7 @@ struct gpd_sim {
   bool duo = false;               // step launches step_kernel_duo (two or three waves per block)
   bool wide = false;              // D > 64: step_kernel_wide / integrate_kernel_wide, one env per workgroup
   int step_waves = 1;             // waves per step block (1, 2, or 3 with the io wave)
+  bool stream = false;            // streaming cache policies (step_kernel STREAM): batches past the MALL
   DwPairs dw_pairs{0, 0};         // SimView::dw_pairs
   double bound_xy;
   std::vector<double> init_tmpl;  // [D][10]
@@ -229,7 +230,7 @@ constexpr int kPfAero = F_GND | F_DRAG;
 constexpr int kPfPyb = F_BULLET | F_GEOM;
 constexpr int kPfPybAll = F_BULLET | F_GEOM | F_GND | F_DRAG | F_DW;
 template <typename R, int ACT>
-const void* step_fn_act(bool multi, int flags) {
+const void* step_fn_act(bool multi, int flags, bool stream) {
   if (multi) {
     switch (flags) {
       case 0: return (const void*)step_kernel<R, ACT, true, 0>;
@@ -239,7 +240,7 @@ const void* step_fn_act(bool multi, int flags) {
     }
   }
   switch (flags) {
-    case 0: return (const void*)step_kernel<R, ACT, false, 0>;
+    case 0: return stream ? (const void*)step_kernel<R, ACT, false, 0, true> : (const void*)step_kernel<R, ACT, false, 0>;
     case kPfAero: return (const void*)step_kernel<R, ACT, false, kPfAero>;
     case kPfPyb: return (const void*)step_kernel<R, ACT, false, kPfPyb>;
     default: return (const void*)step_kernel<R, ACT, false, kPfRuntime>;
@@ -266,8 +267,8 @@ const void* step_kernel_fn(const gpd_sim* s) {
   // the flags the kernel sees (Consts::flags, make_consts)
   const int pf = s->cfg.physics_flags | ((s->cfg.physics_flags & GPD_F_BULLET) ? GPD_F_GEOM_WRENCH : 0);
   switch (s->cfg.act_type) {
-    case GPD_ACT_RPM: return step_fn_act<R, ACT_RPM>(multi, pf);
-    case GPD_ACT_ONE_D_RPM: return step_fn_act<R, ACT_ONE_D_RPM>(multi, pf);
+    case GPD_ACT_RPM: return step_fn_act<R, ACT_RPM>(multi, pf, s->stream);
+    case GPD_ACT_ONE_D_RPM: return step_fn_act<R, ACT_ONE_D_RPM>(multi, pf, s->stream);
     case GPD_ACT_PID: return step_fn_pid<R, ACT_PID>(multi, pf);
     case GPD_ACT_VEL: return step_fn_pid<R, ACT_VEL>(multi, pf);
     default: return step_fn_pid<R, ACT_ONE_D_PID>(multi, pf);
@@ -591,6 +592,12 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
       if ((t * s->nc_magic) >> 16 != t / NC) waves = 1;
     s->step_waves = waves;
     s->duo = waves >= 2;
+    // streaming cache policies for the single-wave plain-DYN kernel once a step's working set
+    // (~820 B per drone: state, ring, rows) is well past the 256 MB Infinity Cache (>= 512K drones;
+    // 262144 envs = 215 MB stay with the default policies, 1M envs 194 -> 145 us with STREAM,
+    // 4096 envs 4.93 -> 6.31 us had it been used there)
+    s->stream = !s->duo && s->D == 1 && C.physics_flags == 0 &&
+                (C.act_type == GPD_ACT_RPM || C.act_type == GPD_ACT_ONE_D_RPM) && s->N >= (1 << 19);
     // the multi-wave kernels store their state plainly (measured 4096 envs 5.47 -> 5.37 us/step);
     // the single-wave kernel keeps write-through state stores (262144 envs 36.7 -> 35.9 us)
     if (s->duo && C.store_policy <= 0) s->wt &= ~2;

@@ -91,20 +91,27 @@ __device__ unsigned long long g_stamps[65536 * kStampPhases];
 // memory when the wave stores them, so less of that write-back is left for the kernel's end.
 typedef int gpd_v4i __attribute__((ext_vector_type(4)));
 typedef unsigned gpd_v2u __attribute__((ext_vector_type(2)));
-#ifndef GPD_DMA_AUX
-#define GPD_DMA_AUX 0    // cache policy of the single-wave step kernel's history LDS-DMA
-#endif
 #ifndef GPD_WT_AUX
 #define GPD_WT_AUX 16   // sc1 (write-through); diagnostic builds try other cache-policy bits
 #endif
+// Cache policies of the step kernel's streams: the default one for cache-resident batches (the
+// state, ring and rows of the last step are re-read from L2 / Infinity Cache), and STREAM for
+// batches far past the 256 MB Infinity Cache: nt (nontemporal) on the state loads and the
+// history LDS-DMA, sc1|nt on the write-through stores.  Measured (scripts/large_n_ab2.sh,
+// profiles/r3/large_n_ab_nt.log, U[-1,1] actions): 1M envs 194 -> 145 us, 4M envs 780 -> 608 us;
+// at 4096 envs the same bits cost 4.93 -> 6.31 us, hence the size-dependent choice (gpd.hip).
+constexpr int kAuxWt = GPD_WT_AUX, kAuxWtStream = 18, kAuxDmaStream = 2;
+template <int AUX = kAuxWt>
 __device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, int off, float4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gpd_v4i, v), r, off, 0, GPD_WT_AUX);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gpd_v4i, v), r, off, 0, AUX);
 }
+template <int AUX = kAuxWt>
 __device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, int off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, GPD_WT_AUX);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, AUX);
 }
+template <int AUX = kAuxWt>
 __device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, int off, double v) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(gpd_v2u, v), r, off, 0, GPD_WT_AUX);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(gpd_v2u, v), r, off, 0, AUX);
 }
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
@@ -160,18 +167,18 @@ __host__ __device__ __forceinline__ long long ridx(long long n, int slot, int L,
 }
 
 // Only what the dynamics reads: ang_v is write-only, last_clipped_action is read only by drag.
-#ifdef GPD_LOAD_NT
-template <typename R> __device__ __forceinline__ R ldst(const R* p) { return __builtin_nontemporal_load(p); }
-#else
-template <typename R> __device__ __forceinline__ R ldst(const R* p) { return *p; }
-#endif
-template <typename R>
+template <bool NT, typename R>
+__device__ __forceinline__ R ldst(const R* p) {
+  if (NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <typename R, bool NT = false>
 __device__ __forceinline__ void load_drone(const SimView<R>& v, long long n, Drone<R>& s, R last[4], bool need_last) {
   const R* st = v.state + tidx(n, 0, kStateComps);
-  s.px = ldst(st + 0 * 64); s.py = ldst(st + 1 * 64); s.pz = ldst(st + 2 * 64);
-  s.qx = ldst(st + 3 * 64); s.qy = ldst(st + 4 * 64); s.qz = ldst(st + 5 * 64); s.qw = ldst(st + 6 * 64);
-  s.vx = ldst(st + 7 * 64); s.vy = ldst(st + 8 * 64); s.vz = ldst(st + 9 * 64);
-  s.wx = ldst(st + 10 * 64); s.wy = ldst(st + 11 * 64); s.wz = ldst(st + 12 * 64);
+  s.px = ldst<NT>(st + 0 * 64); s.py = ldst<NT>(st + 1 * 64); s.pz = ldst<NT>(st + 2 * 64);
+  s.qx = ldst<NT>(st + 3 * 64); s.qy = ldst<NT>(st + 4 * 64); s.qz = ldst<NT>(st + 5 * 64); s.qw = ldst<NT>(st + 6 * 64);
+  s.vx = ldst<NT>(st + 7 * 64); s.vy = ldst<NT>(st + 8 * 64); s.vz = ldst<NT>(st + 9 * 64);
+  s.wx = ldst<NT>(st + 10 * 64); s.wy = ldst<NT>(st + 11 * 64); s.wz = ldst<NT>(st + 12 * 64);
   s.ax = s.ay = s.az = R(0);
   if (need_last) {
     last[0] = st[16 * 64]; last[1] = st[17 * 64]; last[2] = st[18 * 64]; last[3] = st[19 * 64];
@@ -187,7 +194,7 @@ __device__ __forceinline__ void load_drone_full(const SimView<R>& v, long long n
   s.ax = st[13 * 64]; s.ay = st[14 * 64]; s.az = st[15 * 64];
 }
 
-template <typename R>
+template <typename R, int AUX = kAuxWt>
 __device__ __forceinline__ void store_drone_wt(const SimView<R>& v, long long n, const Drone<R>& s, const R last[4]) {
   const __amdgpu_buffer_rsrc_t r =
       __builtin_amdgcn_make_buffer_rsrc(v.state, 0, (int)(kStateComps * v.npad * (long long)sizeof(R)), 0x00020000);
@@ -197,7 +204,7 @@ __device__ __forceinline__ void store_drone_wt(const SimView<R>& v, long long n,
   const bool skip_last = (v.wt & 4) != 0;   // store_drone_step
 #pragma unroll
   for (int k = 0; k < 20; ++k, o += 64 * (int)sizeof(R))
-    if (k < 16 || !skip_last) store_wt(r, o, vals[k]);
+    if (k < 16 || !skip_last) store_wt<AUX>(r, o, vals[k]);
 }
 
 template <typename R>
@@ -216,11 +223,11 @@ __device__ __forceinline__ void store_drone(const SimView<R>& v, long long n, co
 // action_to_rpm of the ring's newest slot, or 0 in an env that has not stepped since its reset,
 // and last_from_ring_kernel writes it back before any reader of state[16..19] (32 B per drone
 // and step less HBM traffic in f64).  The kernel marks that with ctr[E].x = 1 (mark_last_in_ring).
-template <typename R>
+template <typename R, int AUX = kAuxWt>
 __device__ __forceinline__ void store_drone_step(const SimView<R>& v, long long n, const Drone<R>& s,
                                                  const R last[4]) {
   if (v.wt & 2) {
-    store_drone_wt(v, n, s, last);
+    store_drone_wt<R, AUX>(v, n, s, last);
     return;
   }
   R* st = v.state + tidx(n, 0, kStateComps);
@@ -298,7 +305,7 @@ __host__ __device__ inline int step_tile_bytes(int A, int ring_len) {
 // stores; rows flagged in done_rows also go to terminal_obs (their non-state columns - the
 // state part was stored from registers).  t / NC is (t * nc_magic) >> 16 for t <= NL.  U tile
 // elements per lane per batch (LDS reads in flight); lanes past the end are masked off.
-template <int A, int NL, int U = 6>
+template <int A, int NL, int U = 6, int AUX = kAuxWt>
 __device__ __forceinline__ void tile_copy_out(const float4* tile4, const float* tilef, int lane, int nact, int NC,
                                               int nc_magic, int wt, unsigned long long done_rows, float* obs,
                                               float* terminal_obs, long long n0) {
@@ -336,7 +343,7 @@ __device__ __forceinline__ void tile_copy_out(const float4* tile4, const float* 
         // (no exec-mask branch per element)
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, 0, total * 16, 0x00020000);
 #pragma unroll
-        for (int u = 0; u < U; ++u) store_wt(r, ok[u] ? idx[u] * 16 : total * 16, val[u]);
+        for (int u = 0; u < U; ++u) store_wt<AUX>(r, ok[u] ? idx[u] * 16 : total * 16, val[u]);
       } else {
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -370,7 +377,7 @@ __device__ __forceinline__ void tile_copy_out(const float4* tile4, const float* 
       if (wt & 1) {
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, 0, total * 4, 0x00020000);
 #pragma unroll
-        for (int u = 0; u < U; ++u) store_wt(r, ok[u] ? idx[u] * 4 : total * 4, val[u]);
+        for (int u = 0; u < U; ++u) store_wt<AUX>(r, ok[u] ? idx[u] * 4 : total * 4, val[u]);
       } else {
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -393,7 +400,8 @@ __device__ __forceinline__ void tile_copy_out(const float4* tile4, const float* 
 // ACT: action type (GPD_ACT_*); PID types run DSLPIDControl before the substeps.
 // PF: the physics flags compiled in (pf_on): 0 = plain DYN (the bench path, aero / PYB-wrench code
 // compiled out), a flag set for the BASELINE configs' combinations, kPfRuntime for the rest.
-template <typename R, int ACT, bool MULTI, int PF>
+template <typename R, int ACT, bool MULTI, int PF, bool STREAM = false>
+// STREAM: the cache policies for batches far past the Infinity Cache (kAuxWtStream above).
 // The leading scalar arguments duplicate the SimView / StepIO fields the first loads need: the
 // library is built with kernarg preloading, so they arrive in SGPRs at wave launch instead of
 // through an s_load round trip on the kernel-argument segment before the first state load.
@@ -428,7 +436,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
 
   Drone<R> s;
   R last[4];
-  load_drone(v, nn, s, last, drag);
+  load_drone<R, STREAM>(v, nn, s, last, drag);
   const int2 cv = v.ctr[e];
   const int sc = cv.x;        // step_counter
   const int head = cv.y;      // ring slot receiving this step's action
@@ -482,12 +490,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
       slot -= slot >= v.ring_len ? v.ring_len : 0;
       const float* src = v.ring + ridx(nn, slot, v.ring_len, A);
       if (A == 4) {
-        __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tile4 + (3 + k) * kPad), 16, 0, GPD_DMA_AUX);
+        __builtin_amdgcn_global_load_lds((gbl_void_ptr)src, (lds_void_ptr)(tile4 + (3 + k) * kPad), 16, 0,
+                                         STREAM ? kAuxDmaStream : 0);
       } else {
 #pragma unroll
         for (int j = 0; j < A; ++j)
           __builtin_amdgcn_global_load_lds((gbl_void_ptr)(src + j), (lds_void_ptr)(tilef + (12 + k * A + j) * kPad), 4,
-                                           0, GPD_DMA_AUX);
+                                           0, STREAM ? kAuxDmaStream : 0);
       }
     }
   };
@@ -634,11 +643,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
   }
   __syncthreads();
   GPD_STAMP(6);
-  tile_copy_out<A, kWave>(tile4, tilef, tid, nact, NC, v.nc_magic, v.wt, done_rows, io.obs, io.terminal_obs, n0);
+  tile_copy_out<A, kWave, 6, STREAM ? kAuxWtStream : kAuxWt>(tile4, tilef, tid, nact, NC, v.nc_magic, v.wt, done_rows,
+                                                             io.obs, io.terminal_obs, n0);
   GPD_STAMP(7);
   GPD_RSTAMP(12);
   if (!active) return;
-  store_drone_step(v, n, s, last);
+  store_drone_step<R, STREAM ? kAuxWtStream : kAuxWt>(v, n, s, last);
   mark_last_in_ring(v, n);
   if (act_is_pid(ACT)) {
 #pragma unroll
