@@ -601,6 +601,12 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     // the multi-wave kernels store their state plainly (measured 4096 envs 5.47 -> 5.37 us/step);
     // the single-wave kernel keeps write-through state stores (262144 envs 36.7 -> 35.9 us)
     if (s->duo && C.store_policy <= 0) s->wt &= ~2;
+    // the io-wave kernel writes each observation row in two parts from two waves (12 state columns,
+    // history columns): write-through row stores leave those lines partially written twice, +0.29 MB
+    // of HBM writes per launch at 4096 envs (PMC/alg 1.232 -> 1.143 with plain row stores and
+    // write-through state, store_policy 3; step time 4.93 vs 4.97 us, within the run-to-run spread:
+    // profiles/r3/pmc4096, profiles/r3/policy_4096.log)
+    if (waves == 3 && C.store_policy <= 0) s->wt = (s->wt & ~1) | 2;
   }
   if (s->tile_bytes > 160 * 1024) {
     delete s;
