@@ -633,10 +633,11 @@ __device__ __forceinline__ void pc_arm(R cr, R zc, R dx, R dy, R dz, R& ax, R& a
 
 template <typename R>
 __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const Consts<R>& c, const DynK<R>& k) {
-  // The rows' constants (rhs, 1/jacDiag, jacDiag) live in LDS, one column per lane of the
-  // block's single wave; the impulses stay in registers.  Kept in registers with the point loops
-  // unrolled, the 12 rows' Jacobians would be hoisted out of the iteration loop and raise the
-  // whole kernel's VGPR count for a path that only grounded drones take.
+  // The rows' constants (rhs, 1/jacDiag, jacDiag) and impulses live in LDS, one column per lane
+  // of the block's single wave (the run-time-flag kernels, which also serve non-contact configs,
+  // and the multi-wave envs; the PYB flag-set kernels use plane_contact_regs below).  Kept in
+  // registers with the point loops unrolled, the 12 rows' Jacobians would be hoisted out of the
+  // iteration loop and raise the whole kernel's VGPR count for a path that only grounded drones take.
   enum { kRhs = 0, kJdi = 3, kJdn = 6, kLam = 7, kPer = 10 };
   __shared__ R pc[4 * kPer][64];
   const int ln = threadIdx.x & 63;

@@ -166,6 +166,16 @@ __host__ __device__ __forceinline__ long long ridx(long long n, int slot, int L,
   return ((n >> 6) * L + slot) * (64LL * A) + (n & 63) * A;
 }
 
+// Lanes past a block's drones compute on a copy of drone 0 (or of their env's drone 0) and store
+// nothing.  Parked far above the plane they never enter the contact solve: a wave's solve lasts as
+// long as its slowest lane, and drone 0's copies made every block of a launch wait for drone 0's
+// solve (512 x 8 PYB_GND_DRAG_DW: 42 % of the solving waves ran into the 50-iteration cap, most of
+// them on copies of a grounded drone 0; profiles/r3/contact_stats.log).
+template <typename R>
+__device__ __forceinline__ void park_lane(Drone<R>& s, bool active) {
+  s.pz = active ? s.pz : R(1e3);
+}
+
 // Only what the dynamics reads: ang_v is write-only, last_clipped_action is read only by drag.
 template <bool NT, typename R>
 __device__ __forceinline__ R ldst(const R* p) {
@@ -437,6 +447,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
   Drone<R> s;
   R last[4];
   load_drone<R, STREAM>(v, nn, s, last, drag);
+  if (PF == kPfRuntime || (PF & F_BULLET)) park_lane(s, active);
   const int2 cv = v.ctr[e];
   const int sc = cv.x;        // step_counter
   const int head = cv.y;      // ring slot receiving this step's action
@@ -1111,6 +1122,7 @@ __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R>
   Drone<R> s;
   R last[4];
   load_drone(v, n, s, last, drag);
+  park_lane(s, active);
   const int2 cv = v.ctr[e];
   const int sc = cv.x, head = cv.y;
   float a[A];
@@ -1250,6 +1262,7 @@ __global__ __launch_bounds__(MAXT) void integrate_kernel_wide(SimView<R> v, cons
   Drone<R> s;
   R last[4];
   load_drone(v, n, s, last, true);
+  park_lane(s, active);
   const DynK<R> dk = dyn_consts(c);
   const int nw = (D + kWave - 1) / kWave;
   const long long N = v.N;
@@ -1299,6 +1312,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_INTEG
   Drone<R> s;
   R last[4];
   load_drone(v, nn, s, last, true);
+  if (PF == kPfRuntime || (PF & F_BULLET)) park_lane(s, active);
   const long long N = v.N;
   const DynK<R> dk = dyn_consts(c);
   // RPMs are loaded two substeps ahead of their use (substeps t+1 and t+2 in flight while t
