@@ -376,7 +376,9 @@ int launch_integrate(gpd_sim* s, const void* rpm, int n_sub, void* traj, hipStre
   } else if (s->D > 1) {
     f = plain ? (const void*)integrate_kernel<R, true, 0, false> : (const void*)integrate_kernel<R, true, kPfRuntime, false>;
   } else {
-    f = plain ? (const void*)integrate_kernel<R, false, 0, false> : (const void*)integrate_kernel<R, false, kPfRuntime, false>;
+    f = plain ? (s->N >= (1 << 19) ? (const void*)integrate_kernel<R, false, 0, false, true>
+                                    : (const void*)integrate_kernel<R, false, 0, false>)
+              : (const void*)integrate_kernel<R, false, kPfRuntime, false>;
   }
   void* args[] = {(void*)&v, (void*)&c, (void*)&r, (void*)&n_sub, (void*)&tr};
   HIP_TRY(hipLaunchKernel(f, dim3(grid), dim3(kWave), args, 0, st));

@@ -166,16 +166,6 @@ __host__ __device__ __forceinline__ long long ridx(long long n, int slot, int L,
   return ((n >> 6) * L + slot) * (64LL * A) + (n & 63) * A;
 }
 
-// Lanes past a block's drones compute on a copy of drone 0 (or of their env's drone 0) and store
-// nothing.  Parked far above the plane they never enter the contact solve: a wave's solve lasts as
-// long as its slowest lane, and drone 0's copies made every block of a launch wait for drone 0's
-// solve (512 x 8 PYB_GND_DRAG_DW: 42 % of the solving waves ran into the 50-iteration cap, most of
-// them on copies of a grounded drone 0; profiles/r3/contact_stats.log).
-template <typename R>
-__device__ __forceinline__ void park_lane(Drone<R>& s, bool active) {
-  s.pz = active ? s.pz : R(1e3);
-}
-
 // Only what the dynamics reads: ang_v is write-only, last_clipped_action is read only by drag.
 template <bool NT, typename R>
 __device__ __forceinline__ R ldst(const R* p) {
@@ -217,15 +207,16 @@ __device__ __forceinline__ void store_drone_wt(const SimView<R>& v, long long n,
     if (k < 16 || !skip_last) store_wt<AUX>(r, o, vals[k]);
 }
 
-template <typename R>
+template <typename R, bool NT = false>
 __device__ __forceinline__ void store_drone(const SimView<R>& v, long long n, const Drone<R>& s, const R last[4]) {
   R* st = v.state + tidx(n, 0, kStateComps);
-  st[0 * 64] = s.px; st[1 * 64] = s.py; st[2 * 64] = s.pz;
-  st[3 * 64] = s.qx; st[4 * 64] = s.qy; st[5 * 64] = s.qz; st[6 * 64] = s.qw;
-  st[7 * 64] = s.vx; st[8 * 64] = s.vy; st[9 * 64] = s.vz;
-  st[10 * 64] = s.wx; st[11 * 64] = s.wy; st[12 * 64] = s.wz;
-  st[13 * 64] = s.ax; st[14 * 64] = s.ay; st[15 * 64] = s.az;
-  st[16 * 64] = last[0]; st[17 * 64] = last[1]; st[18 * 64] = last[2]; st[19 * 64] = last[3];
+  const R vals[20] = {s.px, s.py, s.pz, s.qx, s.qy, s.qz, s.qw, s.vx, s.vy, s.vz,
+                      s.wx, s.wy, s.wz, s.ax, s.ay, s.az, last[0], last[1], last[2], last[3]};
+#pragma unroll
+  for (int k = 0; k < 20; ++k) {
+    if (NT) __builtin_nontemporal_store(vals[k], st + k * 64);
+    else st[k * 64] = vals[k];
+  }
 }
 
 // The step kernels' state store.  With SimView::wt bit 2 (RPM / ONE_D_RPM action types without
@@ -440,14 +431,16 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
   const long long n = n0 + tid;
   const int nact = (int)((v.N - n0) < v.tpb ? (v.N - n0) : v.tpb);  // drones owned by this block
   const bool active = tid < nact;
-  const long long nn = active ? n : 0;  // inactive lanes compute on drone 0 and store nothing
+  // inactive lanes compute on the block's first drone and store nothing: a copy of a drone the
+  // block integrates anyway, so a wave-uniform solve (the PYB contact) never waits for a drone
+  // of another block (with drone 0's copies, every block paid drone 0's contact iterations)
+  const long long nn = active ? n : n0;
   const long long e = MULTI ? nn / D : nn;
   const bool drag = pf_on<PF>(c.flags, F_DRAG);
 
   Drone<R> s;
   R last[4];
   load_drone<R, STREAM>(v, nn, s, last, drag);
-  if (PF == kPfRuntime || (PF & F_BULLET)) park_lane(s, active);
   const int2 cv = v.ctr[e];
   const int sc = cv.x;        // step_counter
   const int head = cv.y;      // ring slot receiving this step's action
@@ -718,7 +711,7 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
   const long long n = n0 + tid;
   const int nact = (int)((v.N - n0) < v.tpb ? (v.N - n0) : v.tpb);
   const bool active = tid < nact;
-  const long long nn = active ? n : 0;   // inactive lanes compute on drone 0 and store nothing
+  const long long nn = active ? n : n0;  // inactive lanes compute on the block's first drone, store nothing
 #ifdef GPD_STAMPS
   {   // diagnostic: which SIMD / CU each wave of the block runs on (HW_ID: SIMD_ID bits 5:4)
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
@@ -1117,12 +1110,13 @@ __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R>
   const int d = threadIdx.x;
   const bool active = d < D;
   const long long e = blockIdx.x;
-  const long long n = e * D + (active ? d : 0);
+  // lanes d >= D compute on the first drone of their own wave (a drone this wave integrates anyway:
+  // the waves take turns in the contact solve) and store nothing
+  const long long n = e * D + (active ? d : (d & ~(kWave - 1)));
   const bool drag = (c.flags & F_DRAG) != 0;
   Drone<R> s;
   R last[4];
   load_drone(v, n, s, last, drag);
-  park_lane(s, active);
   const int2 cv = v.ctr[e];
   const int sc = cv.x, head = cv.y;
   float a[A];
@@ -1258,11 +1252,10 @@ __global__ __launch_bounds__(MAXT) void integrate_kernel_wide(SimView<R> v, cons
   const int D = v.D;
   const int d = threadIdx.x;
   const bool active = d < D;
-  const long long n = (long long)blockIdx.x * D + (active ? d : 0);
+  const long long n = (long long)blockIdx.x * D + (active ? d : (d & ~(kWave - 1)));   // (step_kernel_wide)
   Drone<R> s;
   R last[4];
   load_drone(v, n, s, last, true);
-  park_lane(s, active);
   const DynK<R> dk = dyn_consts(c);
   const int nw = (D + kWave - 1) / kWave;
   const long long N = v.N;
@@ -1296,7 +1289,9 @@ __global__ __launch_bounds__(MAXT) void integrate_kernel_wide(SimView<R> v, cons
 // gpd_integrate: n_sub raw substeps with explicit per-substep RPMs, each followed by a readback.
 // PF as in step_kernel: 0 (plain DYN, the raw-integrator bench) or kPfRuntime; TRAJ: record the
 // [n_sub][N][20] trajectory.
-template <typename R, bool MULTI, int PF, bool TRAJ>
+// STREAM (plain DYN batches past the Infinity Cache): nt loads of the once-read RPM stream and the
+// state, nt stores of the state (as step_kernel's STREAM).
+template <typename R, bool MULTI, int PF, bool TRAJ, bool STREAM = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_INTEGRATE_WPE))) void integrate_kernel(SimView<R> v, const Consts<R>* __restrict__ cp,
                                                           const R* __restrict__ rpm_in, int n_sub, R* __restrict__ traj) {
   __shared__ R sx[MULTI ? 2 * kWave : 1], sy[MULTI ? 2 * kWave : 1], sz[MULTI ? 2 * kWave : 1];
@@ -1307,12 +1302,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_INTEG
   const int base = tid - d;
   const long long n = (long long)blockIdx.x * v.tpb + tid;
   const bool active = tid < v.tpb && n < v.N;
-  const long long nn = active ? n : 0;
+  const long long nn = active ? n : (long long)blockIdx.x * v.tpb;   // the block's first drone (step_kernel)
   (void)d;
   Drone<R> s;
   R last[4];
-  load_drone(v, nn, s, last, true);
-  if (PF == kPfRuntime || (PF & F_BULLET)) park_lane(s, active);
+  load_drone<R, STREAM>(v, nn, s, last, true);
   const long long N = v.N;
   const DynK<R> dk = dyn_consts(c);
   // RPMs are loaded two substeps ahead of their use (substeps t+1 and t+2 in flight while t
@@ -1321,11 +1315,21 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_INTEG
   using V = typename std::conditional<sizeof(R) == 8, double2, float4>::type;
   auto load4 = [&](int t, R out[4]) {
     const R* src = rpm_in + ((long long)t * N + nn) * 4;
+    typedef double gpd_d2 __attribute__((ext_vector_type(2)));
+    typedef float gpd_f4 __attribute__((ext_vector_type(4)));
     if (sizeof(R) == 8) {
-      const double2 a = reinterpret_cast<const double2*>(src)[0], b = reinterpret_cast<const double2*>(src)[1];
+      gpd_d2 a, b;
+      if (STREAM) {
+        a = __builtin_nontemporal_load(reinterpret_cast<const gpd_d2*>(src));
+        b = __builtin_nontemporal_load(reinterpret_cast<const gpd_d2*>(src) + 1);
+      } else {
+        a = reinterpret_cast<const gpd_d2*>(src)[0];
+        b = reinterpret_cast<const gpd_d2*>(src)[1];
+      }
       out[0] = (R)a.x; out[1] = (R)a.y; out[2] = (R)b.x; out[3] = (R)b.y;
     } else {
-      const float4 a = *reinterpret_cast<const float4*>(src);
+      const gpd_f4 a = STREAM ? __builtin_nontemporal_load(reinterpret_cast<const gpd_f4*>(src))
+                              : *reinterpret_cast<const gpd_f4*>(src);
       out[0] = (R)a.x; out[1] = (R)a.y; out[2] = (R)a.z; out[3] = (R)a.w;
     }
   };
@@ -1358,7 +1362,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_INTEG
   }
   if (!active) return;
   if (n_sub == 0) return;
-  store_drone(v, n, s, last);
+  store_drone<R, STREAM>(v, n, s, last);
 }
 
 // ---------------------------------------------------------------------------------------
