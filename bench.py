@@ -64,6 +64,17 @@ def pmc_traffic(grid, precision):
     return best
 
 
+def instruction_fetch_bytes(kernel, grid):
+    """FETCH_SIZE bytes per launch that are instruction fetch (SQC I-cache misses x the FETCH_SIZE
+    per miss of scripts/ubench/ifetch_probe.hip), from profiles/r3/icache/calibration.json."""
+    f = os.path.join(ROOT, "profiles", "r3", "icache", "calibration.json")
+    try:
+        k = json.load(open(f))["step_kernels"][kernel]
+    except Exception:
+        return None
+    return k["instruction_fetch_size_bytes"] if k.get("grid") == grid else None
+
+
 def rocprof_kernel_us(kernel, grid, precision):
     """Mean duration of `kernel` at `grid` lanes in the newest committed rocprofv3 kernel trace
     (profiles/*_summary.json "kernels" rows): the rocprof figure the live event time must match."""
@@ -705,6 +716,12 @@ def run(args):
     if tr is not None:
         result["roofline"]["traffic"] = tr[0]
         result["roofline"]["traffic_source"] = tr[1] + " (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate passes)"
+        ifetch = instruction_fetch_bytes(result["roofline"]["kernel"], grid_lanes)
+        if ifetch is not None:
+            # FETCH_SIZE also counts the kernel's instruction fetch (calibrated on a kernel that
+            # touches no data, profiles/r3/icache/): the data traffic is what remains
+            result["roofline"]["traffic_instruction_fetch"] = 2 * ifetch
+            result["roofline"]["traffic_data"] = tr[0] - 2 * ifetch
     if world > 1:
         # config 5: the learner hand-off (shard.LearnerHandoff): rank 0 scatters the global action
         # batch, every rank steps its shard, the output-pack prefixes (obs, reward, terminated,
