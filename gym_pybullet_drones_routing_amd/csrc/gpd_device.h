@@ -616,6 +616,7 @@ __device__ __forceinline__ void body_wrench(const Drone<R>& s, const R Rm[9], bo
 // The caller gates the call on a wave ballot: a wave without a low drone never enters.
 template <typename R>
 __device__ __forceinline__ R pc_dot(R ax, R ay, R az, R bx, R by, R bz) { return (ax * bx + ay * by) + az * bz; }
+constexpr int kWaveLanes = 64;
 
 #ifdef GPD_CONTACT_STATS
 // diagnostic build only: per solving wave, the iterations run [0..50] and the active lanes [51..115]
@@ -797,8 +798,15 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
 // A crashing batch's solves touch with one or two rim points and a few run into the iteration
 // cap (50); such a solve holds its whole launch, so the per-iteration instruction count is what
 // the PYB step time follows.
-template <typename R>
+#ifndef GPD_CONTACT_LDSC
+#define GPD_CONTACT_LDSC 0
+#endif
+template <typename R, bool LDSC = GPD_CONTACT_LDSC != 0>
 __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], const Consts<R>& c, const DynK<R>& k) {
+  // LDSC (diagnostic): the read-only row constants (rhs, 1/jacDiag, jacDiag) in LDS columns instead
+  // of VGPRs, re-read every iteration (off the Gauss-Seidel chain), to take VGPR pressure off the loop
+  __shared__ R pcs[LDSC ? 28 : 1][kWaveLanes];
+  const int ln = threadIdx.x & (kWaveLanes - 1);
   const R zc = (-Rm[8] < R(0) ? -c.cyl_hh : c.cyl_hh) + c.cyl_zoff;
   const R cr = c.cyl_r;
   // world inverse inertia I_w^-1 = R diag(1/I) R^T (symmetric)
@@ -849,6 +857,11 @@ __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], c
       }
       jdi[p][j] = act[p] ? inv : R(0);
       rhs[p][j] = act[p] ? r : R(0);
+      if (LDSC) {
+        pcs[p * 3 + j][ln] = jdi[p][j];
+        pcs[12 + p * 3 + j][ln] = rhs[p][j];
+        if (j == 0) pcs[24 + p][ln] = jdn[p];
+      }
       lam[p][j] = R(0);
     }
   }
@@ -867,6 +880,15 @@ __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], c
 #endif
     if (!done) {
       R res = R(0);
+      if (LDSC) {
+        asm volatile("" ::: "memory");   // the row constants are re-read each iteration (not hoisted)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          jdn[p] = pcs[24 + p][ln];
+#pragma unroll
+          for (int j = 0; j < 3; ++j) { jdi[p][j] = pcs[p * 3 + j][ln]; rhs[p][j] = pcs[12 + p * 3 + j][ln]; }
+        }
+      }
 #pragma unroll
       for (int p = 0; p < 4; ++p) {                  // normal rows
         if (__ballot(act[p]) == 0ull) continue;      // wave-uniform: no solving lane touches at p
