@@ -217,13 +217,10 @@ class LearnerHandoff:
         G, E, D, W = self.world, self.count, self.sim.drones_per_env, self.sim.obs_width
         ldone = (self._local("terminated", torch.uint8, (E,)) | self._local("truncated", torch.uint8, (E,))).bool()
         lrows = self._local("terminal_obs", torch.float32, (E, D * W))
-        if self.receives:
-            done_all = (te | tr).bool().reshape(G, E)
-            counts = done_all.sum(1).tolist()             # host sync: sizes the exchange
-        else:
-            counts = None
+        done_all = (te | tr).bool().reshape(G, E) if self.receives else None
         out = torch.zeros((G * E, D, W), dtype=torch.float32, device=self.device) if self.receives else None
         if self.mode == "all_gather" or not self._coll:
+            counts = done_all.sum(1).tolist()             # host sync: sizes the exchange
             kmax = max(counts)
             if kmax == 0:
                 return out
@@ -247,33 +244,32 @@ class LearnerHandoff:
             out.view(G * E, D * W)[done_all.reshape(-1)] = rows[src]
             self.terminal_bytes += G * kmax * D * W * 4
             return out
-        # "gather": point-to-point from every rank that has finished envs to the learner
-        if self.is_learner:
-            ops, blocks = [], {}
-            for r in range(G):
-                if r == self.rank or counts[r] == 0:
-                    continue
-                blk = torch.empty((counts[r], D * W), dtype=torch.float32,
-                                  device="cpu" if self._gloo else self.device)
-                blocks[r] = blk
-                ops.append(dist.P2POp(dist.irecv, blk, r))
-            if ops:
-                for w in dist.batch_isend_irecv(ops):
-                    w.wait()
-            done_all_flat = done_all.reshape(G, E)
-            dst = out.view(G, E, D * W)
-            for r in range(G):
-                if counts[r] == 0:
-                    continue
-                rows = lrows[ldone] if r == self.rank else blocks[r].to(self.device)
-                dst[r][done_all_flat[r]] = rows
-                self.terminal_bytes += counts[r] * D * W * 4
-            return out
+        # "gather": the largest per-rank count by one all_reduce(MAX) of a single int, then one
+        # dist.gather of [kmax, D*W] blocks to the learner (collectives only: no point-to-point
+        # pairs to set up; every rank pads its block to the common count)
         k = int(ldone.sum().item())                       # host sync: this rank's count
+        kt = torch.tensor([k], dtype=torch.int64, device="cpu" if self._gloo else self.device)
+        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
+        kmax = int(kt.item())
+        if kmax == 0:
+            return out
+        buf = torch.zeros((kmax, D * W), dtype=torch.float32, device=self.device)
         if k:
-            rows = lrows[ldone].contiguous()
-            dist.send(rows.cpu() if self._gloo else rows, self.learner)
-        return None
+            buf[:k] = lrows[ldone]
+        if self._gloo:
+            host = [torch.empty((kmax, D * W), dtype=torch.float32) for _ in range(G)] if self.is_learner else None
+            dist.gather(buf.cpu(), host, dst=self.learner)
+            rows = torch.cat(host).to(self.device) if self.is_learner else None
+        else:
+            rows = torch.empty((G * kmax, D * W), dtype=torch.float32, device=self.device) if self.is_learner else None
+            dist.gather(buf, list(rows.view(G, kmax, D * W).unbind(0)) if self.is_learner else None, dst=self.learner)
+        if not self.is_learner:
+            return None
+        within = done_all.to(torch.int64).cumsum(1) - 1
+        src = (torch.arange(G, device=self.device)[:, None] * kmax + within)[done_all]
+        out.view(G * E, D * W)[done_all.reshape(-1)] = rows[src]
+        self.terminal_bytes += G * kmax * D * W * 4
+        return out
 
     def _views(self):
         """The learner's global batch, reassembled from the gathered packs (rank order)."""
