@@ -3,6 +3,7 @@ committed rocprof / PMC figures it reads back, and the rank-count checks that mu
 anything touches a GPU."""
 import json
 import os
+import re
 import subprocess
 import sys
 
@@ -23,12 +24,16 @@ def test_algorithmic_bytes_match_survey():
 
 def test_committed_profiles_are_read_back():
     """The headline kernel's rocprof figures and PMC traffic come from the newest committed
-    summary, which must hold them (profiles/r2_summary.json)."""
-    s = json.load(open(os.path.join(ROOT, "profiles", "r2_summary.json")))
-    row = [r for r in s["kernels"] if r["kernel"] == "gpd::step_kernel_duo<double, 0, true>" and "bench" in r["trace"]]
+    summary (profiles/rN_summary.json, highest N), which must hold them."""
+    newest = max((f for f in os.listdir(os.path.join(ROOT, "profiles")) if re.fullmatch(r"r\d+_summary\.json", f)),
+                 key=lambda f: int(f[1:f.index("_")]))
+    name = "gpd::step_kernel_duo<double, 0, true>"
+    rp = bench.rocprof_kernel_us(name, 49152, "f64")
+    assert rp is not None and rp[1] == "profiles/" + newest
+    s = json.load(open(os.path.join(ROOT, rp[1])))
+    row = [r for r in s["kernels"] if r["kernel"] == name and "bench" in r["trace"]]
     assert row and row[0]["b2b_launches"] > 0
-    rp = bench.rocprof_kernel_us("gpd::step_kernel_duo<double, 0, true>", 49152, "f64")
-    assert rp is not None and rp[0] == pytest.approx(row[0]["mean_us"]) and rp[2] == pytest.approx(row[0]["b2b_median_us"])
+    assert rp[0] == pytest.approx(row[0]["mean_us"]) and rp[2] == pytest.approx(row[0]["b2b_median_us"])
     tr = bench.pmc_traffic(49152, "f64")
     assert tr is not None and 3.17e6 < tr[0] < 4.5e6          # >= the algorithmic 774 B x 4096
     big = bench.pmc_traffic(1 << 20, "f64")

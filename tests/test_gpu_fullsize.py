@@ -171,3 +171,31 @@ def test_large_n_hover_kat():
     assert abs(float(st[0, 2]) - 0.1125) < 1e-4      # hovering (drift from the f32 action map only)
     sim.close()
     orc.close()
+
+
+def test_large_n_integrate_stream_bit_identical():
+    """gpd_integrate from 512K drones runs the STREAM instantiation (nontemporal loads of the RPM
+    stream and the state, nontemporal state stores: cache policies only).  Drone j fed drone
+    (j mod 4096)'s RPMs must end bit-identical to it and to a separate 4096-drone sim (the default
+    policies), from a spread of stored states."""
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+    N, P, T_sub = 1 << 19, 4096, 16
+    rng = np.random.default_rng(9)
+    raw = np.zeros((P, 20))
+    raw[:, 0:3] = rng.uniform(-1, 1, (P, 3)) + np.array([0, 0, 2.0])
+    q = rng.normal(size=(P, 4))
+    raw[:, 3:7] = q / np.linalg.norm(q, axis=1, keepdims=True)
+    raw[:, 7:10] = rng.uniform(-1, 1, (P, 3))
+    raw[:, 10:13] = rng.uniform(-5, 5, (P, 3))
+    rpm = torch.from_numpy(14468.43 * (1 + 0.05 * rng.uniform(-1, 1, (T_sub, P, 4)))).cuda()
+    big = BatchedAviarySim(n_envs=N, task="none", device="cuda:0")
+    small = BatchedAviarySim(n_envs=P, task="none", device="cuda:0")
+    big.set_raw_state(np.tile(raw, (N // P, 1)))
+    small.set_raw_state(raw)
+    big.integrate(rpm.repeat(1, N // P, 1).contiguous())
+    small.integrate(rpm)
+    rb = big.raw_state().view(N // P, P, 20)
+    assert torch.equal(rb, rb[:1].expand_as(rb))
+    assert torch.equal(rb[0], small.raw_state())
+    big.close()
+    small.close()
