@@ -182,6 +182,9 @@ Consts<R> make_consts(const gpd_sim* s) {
   c.plane_half = (R)15.0;    // plane.urdf collision box 30 x 30
   c.resid = (R)1e-7;         // m_leastSquaresResidualThreshold (pybullet)
   c.iters = 50;              // m_numIterations (pybullet numSolverIterations)
+#ifdef GPD_DIAG_RESID
+  c.resid = (R)GPD_DIAG_RESID;   // diagnostic builds only (e.g. -1: every solve runs c.iters iterations)
+#endif
   c.nsub = s->nsub;
   const gpd_pid_params& Q = s->pid;
   PidConsts<R>& k = c.pid;

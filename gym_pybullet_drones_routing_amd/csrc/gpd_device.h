@@ -162,11 +162,13 @@ __device__ __forceinline__ DynK<R> dyn_consts(const Consts<R>& c, int warm0 = 0,
   // one statement for all of them: hipcc issues the scalar loads of every constant-block line
   // back to back and waits once (K$ misses in parallel), instead of a load + wait pair per use
   // behind each model / flag branch
+#ifndef GPD_NO_DYNK_PIN
   asm volatile("" : "+v"(k.dt), "+v"(k.inv_m), "+v"(k.gravity), "+v"(k.jx), "+v"(k.jy), "+v"(k.jz),
                "+v"(k.ijx), "+v"(k.ijy), "+v"(k.ijz), "+v"(k.hdt), "+v"(k.hdt2), "+v"(k.kf), "+v"(k.km),
                "+v"(k.L), "+v"(k.Ls2), "+v"(k.hover_f32), "+s"(k.model), "+s"(k.flags),
                "+s"(k.nsub)
                : "s"(warm0), "s"(warm1));
+#endif
   return k;
 }
 
@@ -790,23 +792,50 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
 // g = I_w^-1 (r x d), I_w^-1 = R diag(1/I) R^T formed once per solve.  In exact arithmetic every
 // quantity equals the base-frame one (R is orthonormal); the results differ by rounding only
 // (tests/test_gpu_bullet.py's resynced and long-run contact gates).
-//   * rows nobody in the wave needs are skipped with a wave ballot: a normal row when no solving
-//     lane has point p in contact, a friction pair when no solving lane has a positive normal
-//     impulse at p (those rows solve to a zero impulse, as the oracle's skipped rows);
+//   * normal rows nobody in the wave touches are skipped (wave-uniform, decided once per solve);
+//     a friction pair runs exec-masked on the lanes with a positive normal impulse at its point
+//     (the others skip it, as the oracle does), and the cone projection on the lanes whose
+//     impulse leaves the cone;
+//   * a normal row's clamp at 0 applies new - old (== -old when clamped, the oracle's form);
 //   * residual: the largest |row residual| is squared once per iteration (squaring is monotonic,
 //     so this equals the largest squared residual exactly).
-// A crashing batch's solves touch with one or two rim points and a few run into the iteration
-// cap (50); such a solve holds its whole launch, so the per-iteration instruction count is what
-// the PYB step time follows.
-#ifndef GPD_CONTACT_LDSC
-#define GPD_CONTACT_LDSC 0
+// A solve holds its wave for (setup + iterations x ~300 instructions); a crashing
+// batch's worst solve and the multi-drone batches' solves run into the iteration cap (50), so the
+// per-iteration instruction count is what the PYB step time follows.  PK's park() / unpark()
+// run after the setup and after the iterations: the caller moves what it keeps across the solve
+// out of VGPRs for the iterations (bullet_substep).
+#ifndef GPD_CONTACT_PARK
+#define GPD_CONTACT_PARK 1   // 0: diagnostic builds (A/B of the parking)
 #endif
-template <typename R, bool LDSC = GPD_CONTACT_LDSC != 0>
-__device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], const Consts<R>& c, const DynK<R>& k) {
-  // LDSC (diagnostic): the read-only row constants (rhs, 1/jacDiag, jacDiag) in LDS columns instead
-  // of VGPRs, re-read every iteration (off the Gauss-Seidel chain), to take VGPR pressure off the loop
-  __shared__ R pcs[LDSC ? 28 : 1][kWaveLanes];
-  const int ln = threadIdx.x & (kWaveLanes - 1);
+struct NoPark {
+  __device__ void park() const {}
+  __device__ void unpark() const {}
+};
+template <class A, class B>
+struct ParkFns {
+  A a;
+  B b;
+  __device__ void park() const { a(); }
+  __device__ void unpark() const { b(); }
+};
+// max(r, |x|) for a running residual r that is already canonical: one v_max_f64 (fmax would add
+// a canonicalising max of r per call).  A NaN x keeps r, as the oracle's max(res, x).
+__device__ __forceinline__ double max_abs(double r, double x) {
+  double o;
+  asm("v_max_f64 %0, %1, |%2|" : "=v"(o) : "v"(r), "v"(x));
+  return o;
+}
+__device__ __forceinline__ float max_abs(float r, float x) {
+  float o;
+  asm("v_max_f32 %0, %1, |%2|" : "=v"(o) : "v"(r), "v"(x));
+  return o;
+}
+template <typename R, class PK = NoPark>
+__device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], const Consts<R>& c, const DynK<R>& k,
+                                                   const PK& pk = PK()) {
+#ifdef GPD_CONTACT_STATS
+  const unsigned long long t_setup = __builtin_readcyclecounter();
+#endif
   const R zc = (-Rm[8] < R(0) ? -c.cyl_hh : c.cyl_hh) + c.cyl_zoff;
   const R cr = c.cyl_r;
   // world inverse inertia I_w^-1 = R diag(1/I) R^T (symmetric)
@@ -822,6 +851,7 @@ __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], c
   R rwx[4], rwy[4], rwz[4];              // world arms of the rim points
   R g[4][3][3];                          // I_w^-1 (r x d) per point and row
   R rhs[4][3], jdi[4][3], jdn[4], lam[4][3];
+  const R idt = g_rcp(k.dt);
   bool act[4];
   bool any = false;
 #pragma unroll
@@ -844,24 +874,21 @@ __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], c
       const R gz = pc_dot(i02, i12, i22, ax, ay, az);
       g[p][j][0] = gx; g[p][j][1] = gy; g[p][j][2] = gz;
       const R jd = k.inv_m + pc_dot(ax, ay, az, gx, gy, gz);
-      const R inv = R(1) / jd;
+      // 1/jd and x/dt as Newton-refined reciprocals (jd >= 1/m > 0): ~1 ulp from the quotients,
+      // a third of an f64 divide's instructions on the setup of every solve
+      const R inv = g_rcp(jd);
       const R vl = j == 0 ? s.vz : (j == 1 ? -s.vy : s.vx);
       const R rel = vl + pc_dot(ax, ay, az, s.wx, s.wy, s.wz);
       R r;
       if (j == 0) {
         const R pen = dist + c.slop;
-        r = pen > R(0) ? (-rel - pen / k.dt) * inv : (-pen * c.erp / k.dt - rel) * inv;
+        r = pen > R(0) ? (-rel - pen * idt) * inv : (-pen * c.erp * idt - rel) * inv;
         jdn[p] = act[p] ? jd : R(0);
       } else {
         r = -rel * inv;
       }
       jdi[p][j] = act[p] ? inv : R(0);
       rhs[p][j] = act[p] ? r : R(0);
-      if (LDSC) {
-        pcs[p * 3 + j][ln] = jdi[p][j];
-        pcs[12 + p * 3 + j][ln] = rhs[p][j];
-        if (j == 0) pcs[24 + p][ln] = jdn[p];
-      }
       lam[p][j] = R(0);
     }
   }
@@ -869,9 +896,16 @@ __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], c
   bool done = !any;
   const R mu = c.mu, resid = c.resid, im = k.inv_m;
   const int iters = c.iters;
+  // normal rows some lane of the wave touches (a row that only finished lanes need runs with
+  // them masked off and changes nothing)
+  bool wrow[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) wrow[p] = __ballot(act[p]) != 0ull;
+  pk.park();   // from here on only the solve's own values are live in this thread
 #ifdef GPD_CONTACT_STATS
   int it_used = 0;
   const unsigned long long nact = __ballot(any);
+  const unsigned long long t_loop = __builtin_readcyclecounter();
 #endif
   for (int it = 0; it < iters; ++it) {
     if (__ballot(!done) == 0ull) break;
@@ -880,63 +914,56 @@ __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], c
 #endif
     if (!done) {
       R res = R(0);
-      if (LDSC) {
-        asm volatile("" ::: "memory");   // the row constants are re-read each iteration (not hoisted)
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          jdn[p] = pcs[24 + p][ln];
-#pragma unroll
-          for (int j = 0; j < 3; ++j) { jdi[p][j] = pcs[p * 3 + j][ln]; rhs[p][j] = pcs[12 + p * 3 + j][ln]; }
-        }
-      }
 #pragma unroll
       for (int p = 0; p < 4; ++p) {                  // normal rows
-        if (__ballot(act[p]) == 0ull) continue;      // wave-uniform: no solving lane touches at p
+        if (!wrow[p]) continue;
         const R jv = DLz + (rwy[p] * DAx - rwx[p] * DAy);
-        R delta = rhs[p][0] - jdi[p][0] * jv;
-        const R sum = lam[p][0] + delta;
-        const bool neg = sum < R(0);
-        delta = neg ? -lam[p][0] : delta;
-        lam[p][0] = neg ? R(0) : sum;
-        DLz = DLz + im * delta;
-        DAx = DAx + g[p][0][0] * delta; DAy = DAy + g[p][0][1] * delta; DAz = DAz + g[p][0][2] * delta;
-        res = g_fmax(res, g_abs(delta * jdn[p]));   // NaN keeps res, as the oracle's max
+        const R sum = lam[p][0] + (rhs[p][0] - jdi[p][0] * jv);
+        const R ln = sum < R(0) ? R(0) : sum;
+        const R d = ln - lam[p][0];
+        lam[p][0] = ln;
+        DLz = DLz + im * d;
+        DAx = DAx + g[p][0][0] * d; DAy = DAy + g[p][0][1] * d; DAz = DAz + g[p][0][2] * d;
+        res = max_abs(res, d * jdn[p]);
       }
 #pragma unroll
       for (int p = 0; p < 4; ++p) {                  // friction pairs on the cone
         const R lnrm = lam[p][0];
-        const bool on = lnrm > R(0);
-        if (__ballot(on) == 0ull) continue;          // wave-uniform: no positive normal impulse at p
-        const R lim = mu * lnrm;
-        const R l1 = lam[p][1], l2 = lam[p][2];
-        const R j1 = (rwz[p] * DAx - rwx[p] * DAz) - DLy;
-        const R j2 = (rwz[p] * DAy - rwy[p] * DAz) + DLx;
-        R s1 = l1 + (rhs[p][1] - jdi[p][1] * j1);
-        R s2 = l2 + (rhs[p][2] - jdi[p][2] * j2);
-        const R m2 = s1 * s1 + s2 * s2;
-        const bool clip = m2 > lim * lim;
-        // onto the cone: (s1, s2) * lim / |s| (a select, and the Newton-refined rsqrt instead of a
-        // square root and a divide; within ~2 ulp of them)
-        const R f = clip ? lim * g_rsqrt(clip ? m2 : R(1)) : R(1);
-        s1 = s1 * f;
-        s2 = s2 * f;
-        const R d1 = on ? s1 - l1 : R(0);
-        const R d2 = on ? s2 - l2 : R(0);
-        lam[p][1] = on ? s1 : l1;
-        lam[p][2] = on ? s2 : l2;
-        DLy = DLy - im * d1;
-        DLx = DLx + im * d2;
-        DAx = DAx + g[p][1][0] * d1; DAy = DAy + g[p][1][1] * d1; DAz = DAz + g[p][1][2] * d1;
-        DAx = DAx + g[p][2][0] * d2; DAy = DAy + g[p][2][1] * d2; DAz = DAz + g[p][2][2] * d2;
-        res = g_fmax(res, g_abs(d1 + d2));
+        if (lnrm > R(0)) {
+          const R lim = mu * lnrm;
+          const R l1 = lam[p][1], l2 = lam[p][2];
+          const R j1 = (rwz[p] * DAx - rwx[p] * DAz) - DLy;
+          const R j2 = (rwz[p] * DAy - rwy[p] * DAz) + DLx;
+          R s1 = l1 + (rhs[p][1] - jdi[p][1] * j1);
+          R s2 = l2 + (rhs[p][2] - jdi[p][2] * j2);
+          const R m2 = s1 * s1 + s2 * s2;
+          if (m2 > lim * lim) {                      // onto the cone: (s1, s2) * lim / |s|
+            const R f = lim * g_rsqrt(m2);
+            s1 = s1 * f;
+            s2 = s2 * f;
+          }
+          const R d1 = s1 - l1, d2 = s2 - l2;
+          lam[p][1] = s1;
+          lam[p][2] = s2;
+          DLy = DLy - im * d1;
+          DLx = DLx + im * d2;
+          DAx = DAx + g[p][1][0] * d1; DAy = DAy + g[p][1][1] * d1; DAz = DAz + g[p][1][2] * d1;
+          DAx = DAx + g[p][2][0] * d2; DAy = DAy + g[p][2][1] * d2; DAz = DAz + g[p][2][2] * d2;
+          res = max_abs(res, d1 + d2);
+        }
       }
       done = res * res <= resid;
     }
   }
+  pk.unpark();
 #ifdef GPD_CONTACT_STATS
+  const unsigned long long t_end = __builtin_readcyclecounter();
   if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) {
     atomicAdd(&g_pc_hist[it_used], 1ull);
     atomicAdd(&g_pc_hist[51 + __popcll(nact)], 1ull);
+    atomicAdd(&g_pc_hist[120], t_loop - t_setup);   // setup cycles (s_memtime)
+    atomicAdd(&g_pc_hist[121], t_end - t_loop);     // iteration-loop cycles (incl. the unpark)
+    atomicAdd(&g_pc_hist[122], (unsigned long long)it_used);
   }
 #endif
   s.vx = any ? s.vx + DLx : s.vx;
@@ -974,9 +1001,11 @@ __device__ __forceinline__ R contact_low(const Drone<R>& s, const R Rm[9], const
 // The exponential map's half angle is clamped at pi/8 < 0.5, so the cos / sinc series always
 // applies (a select, no branch; below Bullet's f < 0.001 Taylor switch the series agrees with
 // Bullet's two-term expansion to ~1e-30).
+// rpm / W / last / k are the caller's loop-carried values: a contact solve parks them in LDS and
+// hands back the reloaded copies (see the contact block below).
 template <typename R, int PF, bool ANGV, int CW = 1>
-__device__ __forceinline__ void bullet_substep(Drone<R>& s, const R rpm[4], const R W[4], const R last[4], R dwsum,
-                                               R q0[4], R d, const Consts<R>& c, const DynK<R>& k) {
+__device__ __forceinline__ void bullet_substep(Drone<R>& s, R rpm[4], R W[4], R last[4], R dwsum,
+                                               R q0[4], R d, const Consts<R>& c, DynK<R>& k) {
   R inv, Rm[9];
   readback_unit<R, true, false>(q0[0], q0[1], q0[2], q0[3], d, inv, Rm);
   bool up = true;
@@ -1027,8 +1056,45 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, const R rpm[4], cons
       // compiled-in PYB flag sets: the register-resident solve; run-time flags (every other
       // combination, whose kernels also serve non-contact configs) keep the LDS rows
       if (GPD_RARE(__ballot(low) != 0ull)) {
-        if (PF != kPfRuntime) plane_contact_regs<R>(s, Rm, c, k);
-        else plane_contact<R>(s, Rm, c, k);
+        if (PF != kPfRuntime) {
+#if GPD_CONTACT_PARK
+          // Everything this thread keeps across the solve (the caller's constants, RPMs and
+          // wrench, the pose and velocities) goes to LDS columns for the iterations and comes
+          // back after them: the solve's ~200 VGPRs then fit beside the kernel's own state
+          // instead of spilling the row constants into AGPR round trips on the Gauss-Seidel chain.
+          // The reload goes through an opaque lane offset, so nothing forwards the stored values
+          // past the solve; a memory clobber keeps the stores ahead of it.
+          constexpr int kPark = 15 + 12 + 4 + 12;
+          __shared__ R pk[kPark][kWaveLanes];
+          const int pl = threadIdx.x & (kWaveLanes - 1);
+          auto each = [&](auto&& f) {
+            f(k.dt); f(k.inv_m); f(k.gravity); f(k.jx); f(k.jy); f(k.jz); f(k.ijx); f(k.ijy); f(k.ijz);
+            f(k.hdt); f(k.hdt2); f(k.kf); f(k.km); f(k.L); f(k.Ls2);
+            f(s.px); f(s.py); f(s.pz); f(s.vx); f(s.vy); f(s.vz); f(s.wx); f(s.wy); f(s.wz);
+            f(s.ax); f(s.ay); f(s.az);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) f(q0[j]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { f(rpm[j]); f(W[j]); f(last[j]); }
+          };
+          auto park = [&]() {
+            int i = 0;
+            each([&](R& x) { pk[i++][pl] = x; });
+            asm volatile("" ::: "memory");
+          };
+          auto unpark = [&]() {
+            int o = pl;
+            asm volatile("" : "+v"(o));
+            int i = 0;
+            each([&](R& x) { x = pk[i++][o]; });
+          };
+          plane_contact_regs<R>(s, Rm, c, k, ParkFns<decltype(park), decltype(unpark)>{park, unpark});
+#else
+          plane_contact_regs<R>(s, Rm, c, k);
+#endif
+        } else {
+          plane_contact<R>(s, Rm, c, k);
+        }
       }
     } else {
       // multi-wave workgroups (envs of more than 64 drones, step_kernel_wide): the LDS rows hold
@@ -1079,8 +1145,8 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, const R rpm[4], cons
 // |theta| >= 0.5 (|omega| >= 240 rad/s at 240 Hz: library sin/cos) are redone in a
 // wave-uniform branch at the end.
 template <typename R, int PF, bool ANGV = true, int CW = 1>
-__device__ __forceinline__ void dyn_substep(Drone<R>& s, const R rpm[4], const R W[4], const R last[4], R dwsum,
-                                            const Consts<R>& c, const DynK<R>& k) {
+__device__ __forceinline__ void dyn_substep(Drone<R>& s, R rpm[4], R W[4], R last[4], R dwsum,
+                                            const Consts<R>& c, DynK<R>& k) {
   R q0[4] = {s.qx, s.qy, s.qz, s.qw};
   R d = q0[0] * q0[0] + q0[1] * q0[1] + q0[2] * q0[2] + q0[3] * q0[3];
   // |q| = 1 +- eps for every quaternion _integrateQ produces from a unit one (its update matrix

@@ -265,8 +265,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 // One physics substep of every drone of the block, including the readback that precedes it
 // (BaseAviary.py:343-372 loop body).  MULTI: envs have D > 1 drones and may need downwash.
 template <typename R, bool MULTI, int PF, bool ANGV = true>
-__device__ __forceinline__ void substep_block(Drone<R>& s, const R rpm[4], const R W[4], const R last[4],
-                                              const Consts<R>& c, const DynK<R>& k, R* sx, R* sy, R* sz, int tid,
+__device__ __forceinline__ void substep_block(Drone<R>& s, R rpm[4], R W[4], R last[4],
+                                              const Consts<R>& c, DynK<R>& k, R* sx, R* sy, R* sz, int tid,
                                               int base, int D, DwPairs pairs = DwPairs{0, 0}, R* spair = nullptr) {
   R dw = R(0);
   if (MULTI && pf_on<PF>(k.flags, F_DW)) {
@@ -454,7 +454,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
   }
 
   // the constants of the whole step, loaded in one batch while the state loads are in flight
-  const DynK<R> dk = dyn_consts(c);
+  DynK<R> dk = dyn_consts(c);
   // warm the scalar cache with the kernel-argument lines the rest of the step reads (ring /
   // counters, task fields + obs pointers, done-flag pointers): one batch of misses now, in the
   // shadow of the state loads, instead of serialised misses behind later branches
@@ -849,7 +849,7 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
     // ------------------------------------------------------------ wave 1: body rates
     R wx = st[10 * 64], wy = st[11 * 64], wz = st[12 * 64];
     const int head = v.ctr[nn].y;
-    const DynK<R> dk = dyn_consts(c);   // the ring fields are first needed after the substeps
+    DynK<R> dk = dyn_consts(c);   // the ring fields are first needed after the substeps
     const int nsub = dk.nsub, nh = v.ring_len - 1;
     const int NC = A == 4 ? 3 + v.ring_len : 12 + v.ring_len * A;
     R rpm[4], W[4];
@@ -922,7 +922,7 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
   const int2 cv = v.ctr[nn];
   const int sc = cv.x;          // step_counter
   const int head = cv.y;        // ring slot receiving this step's action
-  const DynK<R> dk = dyn_consts(c, v.task, io.trunc);
+  DynK<R> dk = dyn_consts(c, v.task, io.trunc);
   const int nsub = dk.nsub;
   const int NC = A == 4 ? 3 + v.ring_len : 12 + v.ring_len * A;
 #ifdef GPD_STAMPS
@@ -1122,7 +1122,7 @@ __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R>
   float a[A];
 #pragma unroll
   for (int j = 0; j < A; ++j) a[j] = io.actions[n * A + j];
-  const DynK<R> dk = dyn_consts(c);
+  DynK<R> dk = dyn_consts(c);
   R rpm[4];
   R cs[9];
   if (!act_is_pid(ACT)) {
@@ -1256,7 +1256,7 @@ __global__ __launch_bounds__(MAXT) void integrate_kernel_wide(SimView<R> v, cons
   Drone<R> s;
   R last[4];
   load_drone(v, n, s, last, true);
-  const DynK<R> dk = dyn_consts(c);
+  DynK<R> dk = dyn_consts(c);
   const int nw = (D + kWave - 1) / kWave;
   const long long N = v.N;
   for (int t = 0; t < n_sub; ++t) {
@@ -1308,7 +1308,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_INTEG
   R last[4];
   load_drone<R, STREAM>(v, nn, s, last, true);
   const long long N = v.N;
-  const DynK<R> dk = dyn_consts(c);
+  DynK<R> dk = dyn_consts(c);
   // RPMs are loaded two substeps ahead of their use (substeps t+1 and t+2 in flight while t
   // integrates): more bytes in flight per wave for the HBM stream.  A drone's 4 RPMs are one
   // aligned 4*sizeof(R)-byte vector (rows of the [T][N][4] tensor).

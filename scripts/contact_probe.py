@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Step time of the Physics.PYB kernels with and without ground contact (4096 HoverAviary envs, f64).
 
-Cases: 'crash' = U[-1,1] RPM actions (many drones end up on the plane, as in bench.py's PYB row),
+Cases ('multi' / 'multifly': bench.py's 512 x 8 PYB_GND_DRAG_DW row with U[-1,1] / hover actions):
+'crash' = U[-1,1] RPM actions (many drones end up on the plane, as in bench.py's PYB row),
 'rest' = zero actions of thrust 0.8 hover (every drone resting on the plane after ~0.3 s),
 'fly' = hover actions (no contact), 'noplane' = U[-1,1] with the plane off.  Prints one line
 per case: mean us/step over a timed region of replayed steps and the fraction of low drones.
@@ -24,7 +25,7 @@ STAG = [[0.15 * math.cos(2 * math.pi * i / 8), 0.15 * math.sin(2 * math.pi * i /
 
 def run(case, E=4096, warm=60, steps=200):
     aero = ("no_plane",) if case == "noplane" else ()
-    if case == "multi":    # bench.py's PYB_GND_DRAG_DW row: 512 MultiHover envs x 8 drones, staggered
+    if case in ("multi", "multifly"):    # bench.py's PYB_GND_DRAG_DW row: 512 MultiHover envs x 8 drones, staggered
         E, D = 512, 8
         sim = BatchedAviarySim(n_envs=E, drones_per_env=D, task="multihover", act=ActionType.RPM,
                                physics=Physics.PYB_GND_DRAG_DW, initial_xyzs=STAG, device="cuda:0")
@@ -37,7 +38,7 @@ def run(case, E=4096, warm=60, steps=200):
         acts = torch.rand((n, E, D, 4), generator=g, device="cuda:0", dtype=torch.float32) * 2 - 1
     elif case == "rest":
         acts = torch.full((n, E, D, 4), -1.0, device="cuda:0")      # 0.95 hover RPM: sinks and rests
-    else:
+    else:                  # fly / multifly: hover actions, no contact
         acts = torch.zeros((n, E, D, 4), device="cuda:0")
     for t in range(warm):
         sim.step(acts[t])
@@ -62,6 +63,9 @@ def run(case, E=4096, warm=60, steps=200):
             print(f"   solves {it.sum()}  iterations: mean {np.dot(np.arange(51), it) / it.sum():.2f} "
                   f"hist {dict((i, int(v)) for i, v in enumerate(it) if v)}  active lanes mean "
                   f"{np.dot(np.arange(65), la) / la.sum():.1f}", flush=True)
+            if h[122]:
+                print(f"   shader cycles: setup {h[120] / it.sum():.0f} per solve, loop {h[121] / h[122]:.0f} per "
+                      f"iteration ({h[121] / it.sum():.0f} per solve)", flush=True)
     sim.close()
 
 

@@ -1,0 +1,26 @@
+# Round 3: contact solve with the angular responses in LDS (GLDS): bullet parity on the default
+# library, step-time A/B against the register-resident v2 (cv2), cycle counters (sgl natural,
+# fgl / fv2 forced to 50 iterations).
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+OUT=gpurun_out/${RUN_TAG:-r3t}
+mkdir -p $OUT
+P=gym_pybullet_drones_routing_amd
+timeout -k 10 400 python -u -m pytest tests/test_gpu_bullet.py -m gpu -q -p no:cacheprovider -rf --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> $OUT/gpu_tests.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+for rep in 1 2; do
+  for v in gpd gpd_cv2; do
+    echo "== $v rep $rep" >> $OUT/ab.log
+    GPD_LIB=$P/lib$v.so timeout -k 10 200 python -u scripts/contact_probe.py crash rest multi 2>&1 | grep -v "amdgpu\|UserWarning\|sim = " >> $OUT/ab.log || exit $?
+  done
+done
+for v in sgl; do
+  echo "== $v" >> $OUT/stats.log
+  GPD_LIB=$P/libgpd_$v.so timeout -k 10 200 python -u scripts/contact_probe.py crash rest multi 2>&1 | grep -v "amdgpu\|UserWarning\|sim = " >> $OUT/stats.log || exit $?
+done
+for v in fgl fv2; do
+  echo "== $v" >> $OUT/stats.log
+  GPD_LIB=$P/libgpd_$v.so timeout -k 10 200 python -u scripts/contact_probe.py rest multi 2>&1 | grep -v "amdgpu\|UserWarning\|sim = " >> $OUT/stats.log || exit $?
+done
+echo ALLDONE
