@@ -14,6 +14,7 @@ masks as device tensors, so the whole loop (policy, env step, GAE, update) stays
     python examples/learn.py --multiagent true   # MultiHoverAviary, 2 drones
     python examples/learn.py --physics dyn       # the explicit DYN integrator instead
     python examples/learn.py --gpus 8 --n_envs 32768   # envs sharded over 8 GPUs, learner on rank 0
+    python examples/learn.py --gpus 8 --n_envs 32768 --learner per-rank   # a learner per GPU, gradient all-reduce
 
 Physics defaults to the env classes' default, Physics.PYB (the reference's learn.py does not
 pass one), i.e. the restated Bullet multibody step.
@@ -86,6 +87,49 @@ def evaluate(policy, multiagent, device, act, physics=Physics.PYB):
     return ret, steps
 
 
+def _collective(fn, t, *args):
+    """Run a torch.distributed collective on `t` in place; gloo (the rehearsal backend) gets a host
+    copy of a device tensor."""
+    import torch.distributed as dist
+    if t.is_cuda and dist.get_backend() == "gloo":
+        h = t.cpu()
+        fn(h, *args)
+        t.copy_(h)
+    else:
+        fn(t, *args)
+    return t
+
+
+def sync_grads(params, world):
+    """Per-rank learners (SURVEY §8(e)'s alternative to the single learner): average the
+    gradients over the ranks with ONE all-reduce of a flat bucket (the 64-64 actor / critic pair
+    is ~10^4 parameters, ~40 KB: one latency-bound RCCL call per minibatch).  Every rank then
+    holds the same gradients, so the same clip and Adam step keep the parameters identical."""
+    import torch.distributed as dist
+    params = [p for p in params if p.grad is not None]
+    flat = torch.cat([p.grad.reshape(-1) for p in params])
+    _collective(dist.all_reduce, flat)
+    flat.div_(world)
+    off = 0
+    for p in params:
+        n = p.grad.numel()
+        p.grad.copy_(flat[off:off + n].view_as(p.grad))
+        off += n
+
+
+def broadcast_params(module):
+    """Rank 0's initial parameters on every rank (one flat broadcast)."""
+    import torch.distributed as dist
+    ps = list(module.parameters())
+    flat = torch.cat([p.detach().reshape(-1) for p in ps])
+    _collective(dist.broadcast, flat, 0)
+    off = 0
+    with torch.no_grad():
+        for p in ps:
+            p.copy_(flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+
+
 def make_env(multiagent, n_envs, act, physics, device, seed=0, distributed=False):
     env_cls = MultiHoverAviary if multiagent else HoverAviary
     kw = dict(obs=DEFAULT_OBS, act=act, physics=Physics(physics))
@@ -98,9 +142,14 @@ def make_env(multiagent, n_envs, act, physics, device, seed=0, distributed=False
 def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), lr=3e-4, epochs=10,
           minibatch=16384, gamma=0.99, gae_lambda=0.95, clip=0.2, vf_coef=0.5, max_grad_norm=0.5,
           eval_every=2, seed=0, device="cuda:0", act=DEFAULT_ACT, target_reward=None, max_seconds=None,
-          log=print, physics=Physics.PYB, env=None):
+          log=print, physics=Physics.PYB, env=None, world=1, rank=0):
     """PPO on the batched env.  ``env``: an already built torch-output VecEnv (e.g. the
-    multi-GPU ``ShardedAviaryVecEnv``); by default one ``AviaryVecEnv`` on ``device``."""
+    multi-GPU ``ShardedAviaryVecEnv``); by default one ``AviaryVecEnv`` on ``device``.
+    world > 1: per-rank learners under torch.distributed — this rank trains on its own
+    ``n_envs`` envs with ``minibatch / world`` samples per minibatch, gradients are averaged over
+    the ranks (sync_grads), rank 0 evaluates and decides when every rank stops; ``timesteps``
+    and the history count all ranks' samples."""
+    import torch.distributed as dist
     torch.manual_seed(seed)
     physics = Physics(physics)
     if env is None:
@@ -115,6 +164,10 @@ def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), l
     D, A = env.num_drones, env.sim.act_width
     n_obs, n_act = D * env.sim.obs_width, D * A
     policy = ActorCritic(n_obs, n_act).to(device)
+    if world > 1:
+        broadcast_params(policy)
+        torch.manual_seed(seed + 1000003 * rank)   # each rank samples its own actions / minibatches
+        minibatch = max(1, minibatch // world)
     opt = torch.optim.Adam(policy.parameters(), lr=lr, eps=1e-5)
     E = n_envs
     buf_obs = torch.zeros((n_steps, E, n_obs), device=device)
@@ -172,23 +225,34 @@ def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), l
                 loss = pg + vf_coef * vl
                 opt.zero_grad(set_to_none=True)
                 loss.backward()
+                if world > 1:
+                    sync_grads(policy.parameters(), world)
                 nn.utils.clip_grad_norm_(policy.parameters(), max_grad_norm)
                 opt.step()
-        timesteps += N
+        timesteps += N * world
         it += 1
-        rec = {"iter": it, "timesteps": timesteps, "mean_step_reward": float(buf_rew.mean()),
+        mean_rew = buf_rew.mean()
+        if world > 1:
+            mean_rew = _collective(dist.all_reduce, mean_rew.reshape(1)) / world
+        rec = {"iter": it, "timesteps": timesteps, "mean_step_reward": float(mean_rew),
                "rollout_s": round(t_upd - t_roll, 3), "update_s": round(time.time() - t_upd, 3),
                "wall_s": round(time.time() - t0, 1)}
-        if it % eval_every == 0:
+        if it % eval_every == 0 and rank == 0:
             er, el = evaluate(policy, multiagent, device, act, physics)
             rec.update(eval_return=er, eval_len=el)
             best = max(best, er)
         history.append(rec)
-        log(json.dumps(rec))
-        if rec.get("eval_return", -1e9) >= target_reward:
+        if rank == 0:
+            log(json.dumps(rec))
+        reached = rec.get("eval_return", -1e9) >= target_reward
+        stop = reached or bool(max_seconds and time.time() - t0 > max_seconds)
+        if world > 1:   # rank 0's decision for every rank
+            flag = torch.tensor([1 if stop else 0, 1 if reached else 0], device=device)
+            _collective(dist.broadcast, flag, 0)
+            stop, reached = bool(flag[0]), bool(flag[1])
+        if reached and rank == 0:
             log(f"[INFO] reward threshold {target_reward} reached after {timesteps} timesteps")
-            break
-        if max_seconds and time.time() - t0 > max_seconds:
+        if stop:
             break
     env.close()
     return policy, history, best, target_reward
@@ -207,11 +271,15 @@ def parse_args(argv=None):
                         "(without WORLD_SIZE in the env, learn.py starts the ranks itself)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL over xGMI); gloo only to rehearse several ranks on one GPU")
+    p.add_argument("--learner", default="rank0", choices=["rank0", "per-rank"],
+                   help="rank0: one learner on the gathered batch (ShardedAviaryVecEnv); per-rank: a learner "
+                        "per GPU on its own env shard, gradients all-reduced")
     return p.parse_args(argv)
 
 
 def run(a):
-    """One rank: shard of the envs; rank 0 also runs PPO on the gathered batch."""
+    """One rank: shard of the envs; rank 0 also runs PPO on the gathered batch (--learner rank0),
+    or every rank runs PPO on its own shard with averaged gradients (--learner per-rank)."""
     import torch.distributed as dist
     multi = str(a.multiagent).lower() in ("1", "true", "yes")
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -227,6 +295,23 @@ def run(a):
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group("gloo")
+        if a.learner == "per-rank":
+            from gym_pybullet_drones_routing_amd.shard import env_shard
+            _, n_local = env_shard(a.n_envs, rank, world)
+            policy, hist, best, target = train(multiagent=multi, n_envs=n_local,
+                                               total_timesteps=int(a.total_timesteps), max_seconds=a.max_seconds,
+                                               physics=Physics(a.physics), device=device, world=world, rank=rank,
+                                               log=print if rank == 0 else (lambda *x: None))
+            if rank == 0:
+                out = {"multiagent": multi, "physics": a.physics, "n_envs": a.n_envs, "gpus": world,
+                       "learner": "per-rank", "target_reward": target, "best_eval_return": best,
+                       "reached": best >= target, "history": hist}
+                print(json.dumps({k: v for k, v in out.items() if k != "history"}), flush=True)
+                if a.output:
+                    with open(a.output, "w") as f:
+                        json.dump(out, f, indent=1)
+            dist.destroy_process_group()
+            return
         env = make_env(multi, a.n_envs, DEFAULT_ACT, Physics(a.physics), device, distributed=True)
         if rank != 0:
             env.serve()

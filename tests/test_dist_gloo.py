@@ -195,3 +195,70 @@ def test_learner_handoff_gloo_matches_one_process(world, mode, force):
 def _prefix_bytes(e):
     from gym_pybullet_drones_routing_amd.sim import pack_layout
     return pack_layout(e, 1, 72)["prefix"]
+
+
+def _learner_worker(rank, world, port, q, ack):
+    """examples/learn.py --learner per-rank, the learner half: rank-local init (different seeds),
+    broadcast_params, a rank-local loss, sync_grads, clip + Adam as train() does."""
+    import sys
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples"))
+        import learn
+        torch.manual_seed(100 + rank)                    # deliberately different initialisations
+        pol = learn.ActorCritic(6, 2)
+        learn.broadcast_params(pol)
+        flat0 = torch.cat([p.detach().reshape(-1) for p in pol.parameters()])
+        opt = torch.optim.Adam(pol.parameters(), lr=1e-3, eps=1e-5)
+        g = torch.Generator().manual_seed(7 + rank)      # rank-local batches
+        out = []
+        for _ in range(3):
+            obs = torch.randn(32, 6, generator=g)
+            act = torch.randn(32, 2, generator=g)
+            loss = -pol.dist(obs).log_prob(act).sum(-1).mean() + (pol.value(obs) ** 2).mean()
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            local = torch.cat([p.grad.reshape(-1) for p in pol.parameters()])
+            allg = [torch.zeros_like(local) for _ in range(world)]
+            dist.all_gather(allg, local)
+            learn.sync_grads(pol.parameters(), world)
+            synced = torch.cat([p.grad.reshape(-1) for p in pol.parameters()])
+            out.append((torch.stack(allg).mean(0), synced))
+            torch.nn.utils.clip_grad_norm_(pol.parameters(), 0.5)
+            opt.step()
+        flat = torch.cat([p.detach().reshape(-1) for p in pol.parameters()])
+        pars = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(pars, flat)
+        f0 = [torch.zeros_like(flat0) for _ in range(world)]
+        dist.all_gather(f0, flat0)
+        if rank == 0:
+            q.put((out, pars, f0))
+            ack.wait(60)          # keep the queue's feeder alive until the parent has read it
+    finally:
+        dist.destroy_process_group()
+
+
+def test_per_rank_learners_stay_in_sync_gloo():
+    """SURVEY §8(e)'s alternative hand-off: a PPO learner per rank.  After broadcast_params every
+    rank starts from rank 0's weights; sync_grads leaves every rank with the mean of the ranks'
+    gradients (one flat all-reduce), so the parameters stay identical through clip + Adam."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ack = ctx.Event()
+    procs = [ctx.Process(target=_learner_worker, args=(r, world, port, q, ack)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out, pars, f0 = q.get(timeout=120)
+    ack.set()
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert torch.equal(f0[0], f0[1])
+    for mean, synced in out:
+        torch.testing.assert_close(synced, mean, rtol=1e-6, atol=1e-7)
+    assert torch.equal(pars[0], pars[1])
+    assert not torch.equal(pars[0], f0[0])             # the steps did move the weights

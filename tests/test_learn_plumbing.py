@@ -75,3 +75,50 @@ def test_ppo_sharded_two_ranks_matches_single_process():
         assert a["timesteps"] == b["timesteps"]
         assert math.isclose(a["mean_step_reward"], b["mean_step_reward"], rel_tol=1e-6)
         assert math.isclose(a["eval_return"], b["eval_return"], rel_tol=1e-5) and a["eval_len"] == b["eval_len"]
+
+
+def _per_rank_worker(rank, world, port, q, ack):
+    import datetime
+
+    import torch
+    import torch.distributed as dist
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    try:
+        import learn
+        pol, hist, best, _ = learn.train(n_envs=64, n_steps=8, total_timesteps=2 * 128 * 8, minibatch=512, epochs=2,
+                                         eval_every=1, log=lambda *a: None, device=torch.device("cuda:0"),
+                                         world=world, rank=rank)
+        flat = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).cpu()
+        allp = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(allp, flat)
+        if rank == 0:
+            q.put((hist, best, all(torch.equal(allp[0], x) for x in allp[1:])))
+            ack.wait(60)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ppo_per_rank_learners_two_ranks():
+    """examples/learn.py --gpus 2 --learner per-rank (SURVEY §8(e)'s alternative): every rank
+    steps its own 64-env shard and trains on it, gradients averaged by one all-reduce per
+    minibatch (gloo, both ranks on this GPU).  Both ranks end with identical weights, the history
+    counts both ranks' samples, and rank 0 evaluates."""
+    import socket
+
+    import torch.multiprocessing as mp
+    from tests.test_gpu_dist import _collect
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ack = ctx.Event()
+    procs = [ctx.Process(target=_per_rank_worker, args=(r, 2, port, q, ack)) for r in range(2)]
+    for p in procs:
+        p.start()
+    hist, best, same = _collect(q, procs, ack=ack)
+    assert same
+    assert [h["timesteps"] for h in hist] == [2 * 64 * 8, 2 * 2 * 64 * 8]
+    assert all(math.isfinite(h["mean_step_reward"]) and h["eval_len"] >= 1 for h in hist)
+    assert math.isfinite(best)
