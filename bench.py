@@ -32,6 +32,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+STRONG_ENVS = 32768          # config 5's global env count, the strong-scaling leg
 
 
 def alg_bytes_per_drone_step(act="rpm", real_bytes=8):
@@ -722,6 +723,21 @@ def run(args):
             # touches no data, profiles/r3/icache/): the data traffic is what remains
             result["roofline"]["traffic_instruction_fetch"] = 2 * ifetch
             result["roofline"]["traffic_data"] = tr[0] - 2 * ifetch
+    # strong scaling: config 5's 32768 envs in total, split over the ranks (at N = 8
+    # the weak line's 4096 per GPU); the driver's N = 1/2/4/8 runs then hold both curves
+    if STRONG_ENVS % world == 0:
+        Es = STRONG_ENVS // world
+        ss = BatchedAviarySim(n_envs=Es, task="hover", act=ActionType(args.act), precision=args.precision,
+                              autoreset=True, device=device)
+        sp = make_pool(Es, A, device, seed=rank_seed(2000, rank), pool=16)
+        Ks = 64
+        ws, ns, ks = time_graph(ss, sp, Ks, 16)
+        ws = max_over_ranks(ws, device)
+        result["strong"] = {"scaling": "strong", "global_envs": STRONG_ENVS, "envs_per_gpu": Es,
+                            "ms_per_step": 1000.0 * ws / ns, "value": STRONG_ENVS * nsub * ns / ws,
+                            "kernel_us": ks, "steps": ns}
+        ss.close()
+        del sp
     if world > 1:
         # config 5: the learner hand-off (shard.LearnerHandoff): rank 0 scatters the global action
         # batch, every rank steps its shard, the output-pack prefixes (obs, reward, terminated,
