@@ -24,6 +24,7 @@ static_assert(GPD_ACT_RPM == ACT_RPM && GPD_ACT_ONE_D_RPM == ACT_ONE_D_RPM && GP
                   GPD_ACT_VEL == ACT_VEL && GPD_ACT_ONE_D_PID == ACT_ONE_D_PID,
               "action type codes of gpd.h and the kernels must agree");
 constexpr int kCtrlComps = 9;
+constexpr size_t kLdsBytes = 160 * 1024;   // LDS per workgroup on gfx950
 
 namespace {
 
@@ -120,6 +121,8 @@ struct gpd_sim {
   bool wide = false;              // D > 64: step_kernel_wide / integrate_kernel_wide, one env per workgroup
   int step_waves = 1;             // waves per step block (1, 2, or 3 with the io wave)
   bool stream = false;            // streaming cache policies (step_kernel STREAM): batches past the MALL
+  bool generic_pf = false;        // the run-time-flag step kernel even where a flag set is compiled in
+                                  // (its static LDS + the observation tile would not fit: upload_tables)
   DwPairs dw_pairs{0, 0};         // SimView::dw_pairs
   double bound_xy;
   std::vector<double> init_tmpl;  // [D][10]
@@ -226,9 +229,11 @@ SimView<R> make_view(const gpd_sim* s) {
 // The step_kernel instantiation of a sim: action type x (D > 1) x (plain DYN fast path).  The
 // fast specialisation exists for the RPM action types only (the bench path).
 // Physics-flag sets compiled into their own kernels (pf_on): the BASELINE configs' combinations
-// (config 3: ground effect + drag; config 4: downwash; Physics.PYB and PYB_GND_DRAG_DW) for the
-// RPM action types, plain DYN and Physics.PYB for the single-drone PID types; every other
-// combination tests Consts::flags at run time.
+// (config 3: ground effect + drag; config 4: downwash) and Physics.PYB / PYB_GND_DRAG_DW (single-
+// and multi-drone envs) for the RPM action types, plain DYN and Physics.PYB for the single-drone
+// PID types; every other combination tests Consts::flags at run time.  The PYB flag sets run the
+// register-resident contact solve (gpd_device.h plane_contact_regs), the run-time kernels the
+// LDS one.
 constexpr int kPfAero = F_GND | F_DRAG;
 constexpr int kPfPyb = F_BULLET | F_GEOM;
 constexpr int kPfPybAll = F_BULLET | F_GEOM | F_GND | F_DRAG | F_DW;
@@ -238,6 +243,7 @@ const void* step_fn_act(bool multi, int flags, bool stream) {
     switch (flags) {
       case 0: return (const void*)step_kernel<R, ACT, true, 0>;
       case F_DW: return (const void*)step_kernel<R, ACT, true, F_DW>;
+      case kPfPyb: return (const void*)step_kernel<R, ACT, true, kPfPyb>;   // MultiHoverAviary's default physics
       case kPfPybAll: return (const void*)step_kernel<R, ACT, true, kPfPybAll>;
       default: return (const void*)step_kernel<R, ACT, true, kPfRuntime>;
     }
@@ -246,6 +252,7 @@ const void* step_fn_act(bool multi, int flags, bool stream) {
     case 0: return stream ? (const void*)step_kernel<R, ACT, false, 0, true> : (const void*)step_kernel<R, ACT, false, 0>;
     case kPfAero: return (const void*)step_kernel<R, ACT, false, kPfAero>;
     case kPfPyb: return (const void*)step_kernel<R, ACT, false, kPfPyb>;
+    case kPfPybAll: return (const void*)step_kernel<R, ACT, false, kPfPybAll>;
     default: return (const void*)step_kernel<R, ACT, false, kPfRuntime>;
   }
 }
@@ -268,7 +275,8 @@ const void* step_kernel_fn(const gpd_sim* s) {
                                           : (const void*)step_kernel_duo<R, ACT_ONE_D_RPM, false>;
   const bool multi = s->D > 1;
   // the flags the kernel sees (Consts::flags, make_consts)
-  const int pf = s->cfg.physics_flags | ((s->cfg.physics_flags & GPD_F_BULLET) ? GPD_F_GEOM_WRENCH : 0);
+  const int pf = s->generic_pf ? kPfRuntime
+                              : s->cfg.physics_flags | ((s->cfg.physics_flags & GPD_F_BULLET) ? GPD_F_GEOM_WRENCH : 0);
   switch (s->cfg.act_type) {
     case GPD_ACT_RPM: return step_fn_act<R, ACT_RPM>(multi, pf, s->stream);
     case GPD_ACT_ONE_D_RPM: return step_fn_act<R, ACT_ONE_D_RPM>(multi, pf, s->stream);
@@ -286,11 +294,23 @@ int upload_tables(gpd_sim* s) {
   HIP_TRY(hipMemcpy(s->d_init, ini.data(), ini.size() * sizeof(R), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(s->d_target, tgt.data(), tgt.size() * sizeof(R), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(s->d_consts, &c, sizeof(c), hipMemcpyHostToDevice));
-  // the observation tile can exceed the 64 KiB default dynamic-LDS limit for long histories
-  if (s->tile_bytes > 65536) {
-    const void* f = step_kernel_fn<R>(s);
-    HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, s->tile_bytes));
+  // the step kernel's static LDS (the PYB flag-set kernels park 44 KB of per-lane values around
+  // the contact solve, gpd_device.h bullet_substep) beside the observation tile must fit the
+  // workgroup's LDS; a long action history (high ctrl_freq) that leaves no room for it gets the
+  // run-time-flag kernel, which solves the contact with its rows in 20 KB of LDS
+  const void* f = step_kernel_fn<R>(s);
+  hipFuncAttributes fa;
+  HIP_TRY(hipFuncGetAttributes(&fa, f));
+  if (fa.sharedSizeBytes + (size_t)s->tile_bytes > kLdsBytes && !s->generic_pf) {
+    s->generic_pf = true;
+    f = step_kernel_fn<R>(s);
+    HIP_TRY(hipFuncGetAttributes(&fa, f));
   }
+  if (fa.sharedSizeBytes + (size_t)s->tile_bytes > kLdsBytes)
+    return fail(GPD_EUNSUPPORTED, "gpd_create: ctrl_freq too high (observation tile + the step kernel's LDS exceed 160 KiB)");
+  // the observation tile can exceed the 64 KiB default dynamic-LDS limit for long histories
+  if (s->tile_bytes > 65536)
+    HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, s->tile_bytes));
   return GPD_OK;
 }
 
@@ -613,7 +633,7 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     // profiles/r3/pmc4096, profiles/r3/policy_4096.log)
     if (waves == 3 && C.store_policy <= 0) s->wt = (s->wt & ~1) | 2;
   }
-  if (s->tile_bytes > 160 * 1024) {
+  if (s->tile_bytes > kLdsBytes) {
     delete s;
     return fail(GPD_EUNSUPPORTED, "gpd_create: ctrl_freq too high (observation tile exceeds 160 KiB of LDS)");
   }

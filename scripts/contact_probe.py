@@ -29,12 +29,16 @@ def run(case, E=4096, warm=60, steps=200):
         E, D = 512, 8
         sim = BatchedAviarySim(n_envs=E, drones_per_env=D, task="multihover", act=ActionType.RPM,
                                physics=Physics.PYB_GND_DRAG_DW, initial_xyzs=STAG, device="cuda:0")
+    elif case == "multi2pyb":   # MultiHoverAviary's default: 2 drones, Physics.PYB (examples/learn.py --multiagent)
+        E, D = 2048, 2
+        sim = BatchedAviarySim(n_envs=E, drones_per_env=D, task="multihover", act=ActionType.RPM,
+                               physics=Physics.PYB, device="cuda:0")
     else:
         D = 1
         sim = BatchedAviarySim(n_envs=E, act=ActionType.RPM, physics=Physics.PYB, aero=aero, device="cuda:0")
     g = torch.Generator(device="cuda:0").manual_seed(0)
     n = warm + steps
-    if case in ("crash", "noplane", "multi"):
+    if case in ("crash", "noplane", "multi", "multi2pyb"):
         acts = torch.rand((n, E, D, 4), generator=g, device="cuda:0", dtype=torch.float32) * 2 - 1
     elif case == "rest":
         acts = torch.full((n, E, D, 4), -1.0, device="cuda:0")      # 0.95 hover RPM: sinks and rests

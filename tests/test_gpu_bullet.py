@@ -321,3 +321,48 @@ def test_contact_step_parity_hover_pyb_crashes():
     err = state_rel_err(sim.state20().cpu().numpy(), np.concatenate([e.state20() for e in envs]))
     assert err.max() <= TOL["f64"], err.max()
     sim.close()
+
+
+@pytest.mark.parametrize("D,aero,freq", [(8, ("gnd", "drag", "dw"), 120), (4, (), 120), (1, ("gnd", "drag", "dw"), 120),
+                                         (1, (), 120), (1, (), 240)],
+                         ids=["multi8_pyb_gnd_drag_dw", "multi4_pyb", "single_pyb_gnd_drag_dw", "single_pyb",
+                              "single_pyb_240hz_runtime_kernel"])
+def test_contact_step_resynced_pyb_flag_kernels(D, aero, freq):
+    """The register-resident contact solve inside the compiled PYB flag-set STEP kernels (the
+    integrate tests above run the run-time-flag kernels and their LDS solve), checked locally as
+    the integrate tests are: ctrl_freq = pyb_freq makes one env.step() one substep, the GPU is set
+    to the oracle's state before every step, and the substep must agree to rounding (1e-12).
+    At 240 Hz control the 120-step action history's observation tile leaves no LDS for the
+    flag-set kernel's parked values, and gpd_create falls back to the run-time-flag kernel (LDS
+    contact rows): the last case checks that path through step().
+    Over the usual 8 substeps a crash batch's rounding can flip a rim point across the contact
+    threshold between the two runs (seen once: 1.4e-7 in an 8-drone env), the same chaos that
+    makes every contact check here a resynced one.  Drones start low and tumbling, with thrust
+    mostly below hover."""
+    from gym_pybullet_drones_routing_amd.enums import ActionType
+    rng = np.random.default_rng(45)
+    E, T = 8, freq                                         # one second of flight
+    raw0 = _crash_case(rng, E * D)
+    acts = rng.uniform(-1, 0.2, (T, E, D, 4)).astype(np.float32)
+    task = "multihover" if D > 1 else "hover"
+    envs = [RefAviary(num_drones=D, task=task, aero=aero, integrator="bullet", pyb_freq=freq, ctrl_freq=freq)
+            for _ in range(E)]
+    for e in range(E):
+        envs[e].set_raw_state(raw0[e * D:(e + 1) * D])
+    sim = _sim(n_envs=E, drones_per_env=D, task=task, precision="f64", act=ActionType.RPM,
+               physics=_physics(aero), autoreset=False, pyb_freq=freq, ctrl_freq=freq)
+    errs, low = [], 0
+    for t in range(T):
+        sim.set_raw_state(np.concatenate([oracle_raw(ev) for ev in envs]))
+        sim.step(torch.from_numpy(acts[t]).cuda())
+        g = sim.raw_state().cpu().numpy()
+        for e, ev in enumerate(envs):
+            ev.step(acts[t, e])
+        r = np.concatenate([oracle_raw(ev) for ev in envs])
+        low += int((r[:, 2] < 0.02).sum())
+        errs.append(state_rel_err(g[:, :16], r[:, :16]))
+    err = np.array(errs)
+    print(f"\n[parity] contact step resynced D={D} {aero} {freq} Hz: max {err.max():.3e} median {np.median(err):.3e}")
+    assert low > E * D * T // 4                            # the batch really works the contact
+    assert err.max() <= 1e-12
+    sim.close()
