@@ -323,11 +323,12 @@ def test_contact_step_parity_hover_pyb_crashes():
     sim.close()
 
 
-@pytest.mark.parametrize("D,aero,freq", [(8, ("gnd", "drag", "dw"), 120), (4, (), 120), (1, ("gnd", "drag", "dw"), 120),
-                                         (1, (), 120), (1, (), 240)],
+@pytest.mark.parametrize("D,aero,freq,prec", [(8, ("gnd", "drag", "dw"), 120, "f64"), (4, (), 120, "f64"),
+                                              (1, ("gnd", "drag", "dw"), 120, "f64"), (1, (), 120, "f64"),
+                                              (1, (), 240, "f64"), (8, ("gnd", "drag", "dw"), 120, "f32")],
                          ids=["multi8_pyb_gnd_drag_dw", "multi4_pyb", "single_pyb_gnd_drag_dw", "single_pyb",
-                              "single_pyb_240hz_runtime_kernel"])
-def test_contact_step_resynced_pyb_flag_kernels(D, aero, freq):
+                              "single_pyb_240hz_runtime_kernel", "multi8_pyb_gnd_drag_dw_f32"])
+def test_contact_step_resynced_pyb_flag_kernels(D, aero, freq, prec):
     """The register-resident contact solve inside the compiled PYB flag-set STEP kernels (the
     integrate tests above run the run-time-flag kernels and their LDS solve), checked locally as
     the integrate tests are: ctrl_freq = pyb_freq makes one env.step() one substep, the GPU is set
@@ -349,7 +350,7 @@ def test_contact_step_resynced_pyb_flag_kernels(D, aero, freq):
             for _ in range(E)]
     for e in range(E):
         envs[e].set_raw_state(raw0[e * D:(e + 1) * D])
-    sim = _sim(n_envs=E, drones_per_env=D, task=task, precision="f64", act=ActionType.RPM,
+    sim = _sim(n_envs=E, drones_per_env=D, task=task, precision=prec, act=ActionType.RPM,
                physics=_physics(aero), autoreset=False, pyb_freq=freq, ctrl_freq=freq)
     errs, low = [], 0
     for t in range(T):
@@ -362,7 +363,13 @@ def test_contact_step_resynced_pyb_flag_kernels(D, aero, freq):
         low += int((r[:, 2] < 0.02).sum())
         errs.append(state_rel_err(g[:, :16], r[:, :16]))
     err = np.array(errs)
-    print(f"\n[parity] contact step resynced D={D} {aero} {freq} Hz: max {err.max():.3e} median {np.median(err):.3e}")
+    print(f"\n[parity] contact step resynced D={D} {aero} {freq} Hz {prec}: max {err.max():.3e} "
+          f"median {np.median(err):.3e}")
     assert low > E * D * T // 4                            # the batch really works the contact
-    assert err.max() <= 1e-12
+    if prec == "f64":
+        assert err.max() <= 1e-12
+    else:
+        # f32: a rim point within f32 rounding of the contact threshold can land on either side
+        # (one such flip: 1.75e-3 in one substep of one drone of 7 680); the median is rounding
+        assert np.median(err) <= 1e-5 and err.max() <= 5e-3
     sim.close()
