@@ -369,7 +369,7 @@ def test_contact_step_resynced_pyb_flag_kernels(D, aero, freq, prec):
     if prec == "f64":
         assert err.max() <= 1e-12
     else:
-        # f32: a rim point within f32 rounding of the contact threshold can land on either side
-        # (one such flip: 1.75e-3 in one substep of one drone of 7 680); the median is rounding
+        # f32: a rim point within f32 rounding of the contact threshold can land on either side of
+        # it (worst substep measured: 1.75e-3 over 960 x 8 drone-substeps); the median is rounding
         assert np.median(err) <= 1e-5 and err.max() <= 5e-3
     sim.close()
