@@ -16,17 +16,19 @@ PHYSICS = ["dyn", "pyb", "pyb_gnd", "pyb_drag", "pyb_dw", "pyb_gnd_drag_dw"]
 ACTS = ["rpm", "one_d_rpm", "pid", "vel", "one_d_pid"]
 
 
+@pytest.mark.parametrize("prec", ["f64", "f32"])
 @pytest.mark.parametrize("D", [1, 3, 70])
 @pytest.mark.parametrize("act", ACTS)
 @pytest.mark.parametrize("physics", PHYSICS)
-def test_step_matrix(physics, act, D):
+def test_step_matrix(physics, act, D, prec):
     import warnings
 
     from gym_pybullet_drones_routing_amd.enums import ActionType, Physics
     from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
     E, T = 5, 6
     task = "hover" if D == 1 else "multihover"
-    kw = dict(drones_per_env=D, task=task, act=ActionType(act), physics=Physics(physics), device="cuda:0")
+    kw = dict(drones_per_env=D, task=task, act=ActionType(act), physics=Physics(physics), precision=prec,
+              device="cuda:0")
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")          # multi-drone PYB: drone<->drone collisions not restated
         batch = BatchedAviarySim(n_envs=E, **kw)
