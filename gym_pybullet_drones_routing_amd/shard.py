@@ -96,8 +96,9 @@ class LearnerHandoff:
     4. terminal rows (``terminal_obs=True``) move only for envs that finished this step, packed
        densely: in "all_gather" mode every rank knows every rank's done count from the gathered
        flags, and one ``all_gather_into_tensor`` of [max count, D, W] per rank runs when any env
-       finished; in "gather" mode each rank with finished envs ``send``s its k rows to the learner,
-       which ``recv``s exactly the counts it read from the gathered flags.  Steps where no env
+       finished; in "gather" mode one ``all_reduce(MAX)`` of a single int gives the step's
+       largest per-rank count and one ``dist.gather`` of [max count, D, W] per rank brings the
+       rows to the learner (collectives only, no point-to-point pairs).  Steps where no env
        finished move no terminal bytes.
 
     ``step`` returns (obs [E, D, W], reward [E], terminated [E], truncated [E], terminal_obs or
