@@ -6,7 +6,7 @@ Cases ('multi' / 'multifly': bench.py's 512 x 8 PYB_GND_DRAG_DW row with U[-1,1]
 'rest' = zero actions of thrust 0.8 hover (every drone resting on the plane after ~0.3 s),
 'fly' = hover actions (no contact), 'noplane' = U[-1,1] with the plane off.  Prints one line
 per case: mean us/step over a timed region of replayed steps and the fraction of low drones.
-Select the library with GPD_LIB (A/B builds)."""
+Select the library with GPD_LIB (A/B builds), the block geometry with GPD_PROBE_DPB (drones per block)."""
 import ctypes
 import math
 import os
@@ -37,6 +37,18 @@ def run(case, E=4096, warm=60, steps=200):
         D = 1
         sim = BatchedAviarySim(n_envs=E, act=ActionType.RPM, physics=Physics.PYB, aero=aero, device="cuda:0")
     g = torch.Generator(device="cuda:0").manual_seed(0)
+    dpb = int(os.environ.get("GPD_PROBE_DPB", "0"))      # drones per block (0: the library's choice)
+    if dpb:
+        sim.close()
+        kw = dict(tuning={"drones_per_block": dpb}, device="cuda:0")
+        if case in ("multi", "multifly"):
+            sim = BatchedAviarySim(n_envs=E, drones_per_env=D, task="multihover", act=ActionType.RPM,
+                                   physics=Physics.PYB_GND_DRAG_DW, initial_xyzs=STAG, **kw)
+        elif case == "multi2pyb":
+            sim = BatchedAviarySim(n_envs=E, drones_per_env=D, task="multihover", act=ActionType.RPM,
+                                   physics=Physics.PYB, **kw)
+        else:
+            sim = BatchedAviarySim(n_envs=E, act=ActionType.RPM, physics=Physics.PYB, aero=aero, **kw)
     n = warm + steps
     if case in ("crash", "noplane", "multi", "multi2pyb"):
         acts = torch.rand((n, E, D, 4), generator=g, device="cuda:0", dtype=torch.float32) * 2 - 1
