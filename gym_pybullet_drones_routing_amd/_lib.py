@@ -26,6 +26,7 @@ GPD_ABI_VERSION = 5
 CTRL_COMPS = 9  # integral_pos_e(3) integral_rpy_e(3) last_rpy(3)
 GPD_TASK_NONE, GPD_TASK_HOVER, GPD_TASK_MULTIHOVER = 0, 1, 2
 GPD_F_GND, GPD_F_DRAG, GPD_F_DW, GPD_F_GEOM_WRENCH, GPD_F_BULLET, GPD_F_NO_PLANE = 1, 2, 4, 8, 16, 32
+GPD_F_NO_DRONE_CONTACT = 64
 GPD_F32, GPD_F64 = 0, 1
 
 # Every symbol include/gpd.h declares (checked by tests/test_lib_symbols.py).

@@ -184,6 +184,13 @@ Consts<R> make_consts(const gpd_sim* s) {
   c.mu = (R)(0.5 * 1.0);     // drone default friction x plane.urdf lateral_friction
   c.plane_half = (R)15.0;    // plane.urdf collision box 30 x 30
   c.resid = (R)1e-7;         // m_leastSquaresResidualThreshold (pybullet)
+  {
+    // drone <-> drone contact (drone_contact, gpd_kernels.h; oracle/bullet_mb.py drone_contact)
+    const double bs = std::sqrt(P.collision_r * P.collision_r + (P.collision_h / 2) * (P.collision_h / 2));
+    const double reach = 2.0 * bs + (double)c.brk;
+    c.dd_reach2 = (R)(reach * reach);
+    c.dd_mu = (R)(0.5 * 0.5);   // drone x drone default friction
+  }
   c.iters = 50;              // m_numIterations (pybullet numSolverIterations)
 #ifdef GPD_DIAG_RESID
   c.resid = (R)GPD_DIAG_RESID;   // diagnostic builds only (e.g. -1: every solve runs c.iters iterations)
@@ -521,7 +528,8 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   if (C.task == GPD_TASK_HOVER && C.drones_per_env != 1)
     return fail(GPD_EINVAL, "gpd_create: HoverAviary is single-drone (drones_per_env must be 1)");
   if (C.precision != GPD_F32 && C.precision != GPD_F64) return fail(GPD_EINVAL, "gpd_create: bad precision");
-  if (C.physics_flags & ~(GPD_F_GND | GPD_F_DRAG | GPD_F_DW | GPD_F_GEOM_WRENCH | GPD_F_BULLET | GPD_F_NO_PLANE))
+  if (C.physics_flags & ~(GPD_F_GND | GPD_F_DRAG | GPD_F_DW | GPD_F_GEOM_WRENCH | GPD_F_BULLET | GPD_F_NO_PLANE |
+                          GPD_F_NO_DRONE_CONTACT))
     return fail(GPD_EINVAL, "gpd_create: unknown physics flag");
   if (params->model < GPD_MODEL_CF2X || params->model > GPD_MODEL_RACE)
     return fail(GPD_EINVAL, "gpd_create: unknown drone model");

@@ -79,7 +79,7 @@ template <> struct PiC<double> { static constexpr double pi = 3.1415926535897932
 
 // ---------------------------------------------------------------- model constants (device memory)
 enum : int { MODEL_CF2X = 0, MODEL_CF2P = 1, MODEL_RACE = 2 };
-enum : int { F_GND = 1, F_DRAG = 2, F_DW = 4, F_GEOM = 8, F_BULLET = 16, F_NO_PLANE = 32 };
+enum : int { F_GND = 1, F_DRAG = 2, F_DW = 4, F_GEOM = 8, F_BULLET = 16, F_NO_PLANE = 32, F_NO_DC = 64 };
 // PF, the physics flags a kernel is compiled for: 0 = plain DYN (the FAST path), a flag set =
 // those terms compiled in (no flag tests, one basic block per substep), kPfRuntime = the terms
 // selected at run time from Consts::flags (every other combination).
@@ -124,6 +124,7 @@ struct Consts {
   R cyl_r, cyl_hh, cyl_zoff;   // collision cylinder (cf2x.urdf:31-35): radius, half length, z offset
   R brk;                       // contact breaking threshold (0.02 x the cylinder's motion disc)
   R slop, erp, mu, plane_half, resid;   // m_linearSlop, m_erp2, combined friction, plane box, residual
+  R dd_reach2, dd_mu;          // drone <-> drone contact: broadphase (2 x bounding sphere + brk)^2, friction
   int iters;                   // m_numIterations
   R init0[10];             // reset template of drone 0 (pos, stored quat, rpy): single-drone envs
   R target0[3];            // task target of drone 0 (single-drone envs: no dependent global load)
@@ -1003,9 +1004,15 @@ __device__ __forceinline__ R contact_low(const Drone<R>& s, const R Rm[9], const
 // Bullet's two-term expansion to ~1e-30).
 // rpm / W / last / k are the caller's loop-carried values: a contact solve parks them in LDS and
 // hands back the reloaded copies (see the contact block below).
-template <typename R, int PF, bool ANGV, int CW = 1>
+// HK: the drone <-> drone contact of multi-drone envs (gpd_kernels.h DcHook), run on the
+// unconstrained velocities before the ground-plane solve; NoDc elsewhere.
+struct NoDc {
+  template <typename R>
+  __device__ void operator()(Drone<R>&, const R*, const Consts<R>&, const DynK<R>&) const {}
+};
+template <typename R, int PF, bool ANGV, int CW = 1, class HK = NoDc>
 __device__ __forceinline__ void bullet_substep(Drone<R>& s, R rpm[4], R W[4], R last[4], R dwsum,
-                                               R q0[4], R d, const Consts<R>& c, DynK<R>& k) {
+                                               R q0[4], R d, const Consts<R>& c, DynK<R>& k, const HK& hk = HK()) {
   R inv, Rm[9];
   readback_unit<R, true, false>(q0[0], q0[1], q0[2], q0[3], d, inv, Rm);
   bool up = true;
@@ -1048,6 +1055,7 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, R rpm[4], R W[4], R 
   s.vx = clampv(s.vx + k.dt * (Fx * k.inv_m - kv * s.vx));
   s.vy = clampv(s.vy + k.dt * (Fy * k.inv_m - kv * s.vy));
   s.vz = clampv(s.vz + k.dt * (Fz * k.inv_m - kv * s.vz));
+  if (!pf_on<PF>(k.flags, F_NO_DC)) hk(s, Rm, c, k);
   // ground-plane contact (solveConstraints, before integrateTransforms); the margin keeps the
   // gate conservative against the candidates' own rounding
   if (!pf_on<PF>(k.flags, F_NO_PLANE)) {
@@ -1144,9 +1152,9 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, R rpm[4], R W[4], R 
 // written before the readback and the two dependency chains interleave.  Lanes with
 // |theta| >= 0.5 (|omega| >= 240 rad/s at 240 Hz: library sin/cos) are redone in a
 // wave-uniform branch at the end.
-template <typename R, int PF, bool ANGV = true, int CW = 1>
+template <typename R, int PF, bool ANGV = true, int CW = 1, class HK = NoDc>
 __device__ __forceinline__ void dyn_substep(Drone<R>& s, R rpm[4], R W[4], R last[4], R dwsum,
-                                            const Consts<R>& c, DynK<R>& k) {
+                                            const Consts<R>& c, DynK<R>& k, const HK& hk = HK()) {
   R q0[4] = {s.qx, s.qy, s.qz, s.qw};
   R d = q0[0] * q0[0] + q0[1] * q0[1] + q0[2] * q0[2] + q0[3] * q0[3];
   // |q| = 1 +- eps for every quaternion _integrateQ produces from a unit one (its update matrix
@@ -1164,7 +1172,7 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, R rpm[4], R W[4], R las
     }
   }
   if (pf_on<PF>(k.flags, F_BULLET)) {
-    bullet_substep<R, PF, ANGV, CW>(s, rpm, W, last, dwsum, q0, d, c, k);
+    bullet_substep<R, PF, ANGV, CW, HK>(s, rpm, W, last, dwsum, q0, d, c, k, hk);
     return;
   }
   R inv, Rm[9];

@@ -262,12 +262,373 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// ---------------------------------------------------------------- drone <-> drone contact (PYB*, D > 1)
+// MultiHoverAviary's drones are colliding Bullet bodies (BaseAviary.py:486-491) stepped together
+// by p.stepSimulation() (:369-370).  Restatement (oracle/bullet_mb.py drone_contact; parity
+// unpinned like the plane's: Bullet's GJK / EPA and its persistent manifold are not restated):
+//   * broadphase: pairs (i, j > i) of an env whose cylinder centres are within
+//     2 x bounding-sphere radius + the breaking threshold;
+//   * one contact per pair: Bullet's margin scheme, the closest points of the margin-shrunk core
+//     cylinders (PAIR_ROUNDS rounds of alternating projection from B's centre) give the normal
+//     (B -> A) and distance core - 2 x margin, with thicker margins for deeper overlaps (up to
+//     ~2 cm), beyond that the least overlap over the centre line and the two axes;
+//   * contacts below the breaking threshold, in (i, j) order, fill the env's D solver slots;
+//   * rows (normal, btPlaneSpace1 friction pair) between two bodies: effective mass
+//     2/m + a_A.I_A^-1 a_A + a_B.I_B^-1 a_B; the plane's rhs rules and cone (mu 0.25); projected
+//     Gauss-Seidel over the env's normal rows, then friction pairs, in slot order; the env stops
+//     at its largest squared residual <= resid or after `iters` iterations.
+// Layout: one LDS column per lane of the block's single wave: the drone columns (centre, axis,
+// pose, velocities, world inverse inertia, velocity deltas) and the env's slots in the columns
+// of its own lanes (slot s of the env whose first lane is b at column b + s), so the lane that
+// owns a slot column solves that row; slots of different envs touch different drones and run
+// together, the slots of one env one after another.  Runs only when the wave's broadphase finds a
+// pair (a ballot), after the unconstrained velocity update and before the ground-plane solve.
+template <typename R>
+__device__ __forceinline__ void cyl_project(R cx, R cy, R cz, R ax, R ay, R az, R r, R hh, R& x, R& y, R& z) {
+  const R dx = x - cx, dy = y - cy, dz = z - cz;
+  const R t = pc_dot(dx, dy, dz, ax, ay, az);
+  const R tc = t > hh ? hh : (t < -hh ? -hh : t);
+  R rx = dx - t * ax, ry = dy - t * ay, rz = dz - t * az;
+  const R rho2 = pc_dot(rx, ry, rz, rx, ry, rz);
+  if (rho2 > r * r) {
+    const R f = r / g_sqrt(rho2);
+    rx = rx * f; ry = ry * f; rz = rz * f;
+  }
+  x = (cx + tc * ax) + rx;
+  y = (cy + tc * ay) + ry;
+  z = (cz + tc * az) + rz;
+}
+template <typename R>
+__device__ __forceinline__ R cyl_extent(R ux, R uy, R uz, R ax, R ay, R az, R r, R hh) {
+  const R ua = pc_dot(ux, uy, uz, ax, ay, az);
+  const R s2 = R(1) - ua * ua;
+  return hh * g_abs(ua) + r * g_sqrt(s2 > R(0) ? s2 : R(0));
+}
+constexpr int kPairRounds = 16;
+// contact of cylinders A (centre ca, axis aa) and B: normal (B -> A), point on B, distance.
+// Bullet's margin scheme over thickening core levels (oracle/bullet_mb.py pair_geometry): the
+// core cylinders (r - m, hh - m) by alternating projection in B-centred coordinates; a level
+// whose cores come within kCoreSep passes to the next margin; deeper overlaps: least overlap over
+// the centre line and the two axes.
+template <typename R>
+__device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], const R cb[3], const R ab[3], R r, R hh,
+                                              R n[3], R pb[3], R& dist) {
+  const R lx = ca[0] - cb[0], ly = ca[1] - cb[1], lz = ca[2] - cb[2];
+  const R margins[4] = {R(0.001), R(0.003), R(0.006), R(0.011)};
+  R qx = R(0), qy = R(0), qz = R(0);
+  for (int lv = 0; lv < 4; ++lv) {
+    const R mg = margins[lv], rc = r - mg, hc = hh - mg;
+    R px = R(0), py = R(0), pz = R(0);
+    qx = R(0); qy = R(0); qz = R(0);
+    for (int it = 0; it < kPairRounds; ++it) {
+      px = qx; py = qy; pz = qz;
+      cyl_project(lx, ly, lz, aa[0], aa[1], aa[2], rc, hc, px, py, pz);
+      qx = px; qy = py; qz = pz;
+      cyl_project(R(0), R(0), R(0), ab[0], ab[1], ab[2], rc, hc, qx, qy, qz);
+    }
+    const R vx = px - qx, vy = py - qy, vz = pz - qz;
+    const R d2 = pc_dot(vx, vy, vz, vx, vy, vz);
+    if (d2 > R(1e-4) * R(1e-4)) {
+      const R dc = g_sqrt(d2);
+      n[0] = vx / dc; n[1] = vy / dc; n[2] = vz / dc;
+      pb[0] = cb[0] + (qx + n[0] * mg); pb[1] = cb[1] + (qy + n[1] * mg); pb[2] = cb[2] + (qz + n[2] * mg);
+      dist = dc - R(2) * mg;
+      return;
+    }
+  }
+  pb[0] = cb[0] + qx; pb[1] = cb[1] + qy; pb[2] = cb[2] + qz;
+  const R c2 = pc_dot(lx, ly, lz, lx, ly, lz);
+  R best = R(0);
+  bool have = false;
+  for (int u = 0; u < 3; ++u) {
+    R ux, uy, uz;
+    if (u == 0) {
+      if (!(c2 > R(1e-24))) continue;
+      const R l = g_sqrt(c2);
+      ux = lx / l; uy = ly / l; uz = lz / l;
+    } else {
+      const R* a = u == 1 ? aa : ab;
+      ux = a[0]; uy = a[1]; uz = a[2];
+    }
+    if (pc_dot(ux, uy, uz, lx, ly, lz) < R(0)) { ux = -ux; uy = -uy; uz = -uz; }
+    const R ov = (cyl_extent(ux, uy, uz, aa[0], aa[1], aa[2], r, hh) + cyl_extent(ux, uy, uz, ab[0], ab[1], ab[2], r, hh)) -
+                 pc_dot(ux, uy, uz, lx, ly, lz);
+    if (!have || ov < best) {
+      have = true;
+      best = ov;
+      n[0] = ux; n[1] = uy; n[2] = uz;
+    }
+  }
+  dist = -best;
+}
+// btPlaneSpace1
+template <typename R>
+__device__ __forceinline__ void plane_space(const R n[3], R p[3], R q[3]) {
+  if (g_abs(n[2]) > R(0.7071067811865475244008443621048490)) {
+    const R a = n[1] * n[1] + n[2] * n[2];
+    const R k = R(1) / g_sqrt(a);
+    p[0] = R(0); p[1] = -n[2] * k; p[2] = n[1] * k;
+    q[0] = a * k; q[1] = -n[0] * p[2]; q[2] = n[0] * p[1];
+  } else {
+    const R a = n[0] * n[0] + n[1] * n[1];
+    const R k = R(1) / g_sqrt(a);
+    p[0] = -n[1] * k; p[1] = n[0] * k; p[2] = R(0);
+    q[0] = -n[2] * p[1]; q[1] = n[2] * p[0]; q[2] = a * k;
+  }
+}
+
+enum { DC_CX, DC_CY, DC_CZ, DC_AX, DC_AY, DC_AZ, DC_PX, DC_PY, DC_PZ, DC_VX, DC_VY, DC_VZ, DC_WX, DC_WY, DC_WZ,
+       DC_I00, DC_I01, DC_I02, DC_I11, DC_I12, DC_I22, DC_DLX, DC_DLY, DC_DLZ, DC_DAX, DC_DAY, DC_DAZ, DC_RES, DC_N };
+template <typename R>
+struct DcLds {
+  R dc[DC_N][kWave];       // drone columns
+  R sc[25][kWave];         // slot columns
+  int sij[2][kWave];       // slot: drone lanes i, j (i = -1: empty)
+  int scnt[kWave], stouch[kWave];
+};
+// one LDS block per instantiation, shared by the broadphase (inlined) and the solve (a call)
+template <typename R>
+__device__ __forceinline__ DcLds<R>& dc_lds() {
+  __shared__ DcLds<R> x;
+  return x;
+}
+// broadphase of lane ln's pairs (ln, j > ln): centres within reach (the centre / axis columns written)
+template <typename R>
+__device__ __forceinline__ bool dc_near(const DcLds<R>& L, const R cc[3], int j, R reach2) {
+  const R ex = cc[0] - L.dc[DC_CX][j], ey = cc[1] - L.dc[DC_CY][j], ez = cc[2] - L.dc[DC_CZ][j];
+  return pc_dot(ex, ey, ez, ex, ey, ez) < reach2;
+}
+// the setup and solve: a call, so that its registers stay out of the substep loop that almost
+// never enters it
+template <typename R>
+__device__ __noinline__ void drone_contact(Drone<R>& s, const R* Rm, const Consts<R>& c, const DynK<R>& k, int ln,
+                                           int base, int D, bool cand) {
+  enum { CX = DC_CX, CY, CZ, AX, AY, AZ, PX, PY, PZ, VX, VY, VZ, WX, WY, WZ, I00, I01, I02, I11, I12, I22,
+         DLX, DLY, DLZ, DAX, DAY, DAZ, RES };
+  enum { RAX, RAY, RAZ, RBX, RBY, RBZ, NX, NY, NZ, T1X, T1Y, T1Z, T2X, T2Y, T2Z, RH0, RH1, RH2, JI0, JI1, JI2, JDN,
+         LM0, LM1, LM2, NSC };
+  static_assert(NSC == 25 && RES == DC_RES, "DcLds layout");
+  DcLds<R>& L = dc_lds<R>();
+  auto& dc = L.dc;
+  auto& sc = L.sc;
+  auto& sij = L.sij;
+  auto& scnt = L.scnt;
+  auto& stouch = L.stouch;
+  const R r = c.cyl_r, hh = c.cyl_hh, zo = c.cyl_zoff;
+  const R ca[3] = {Rm[2], Rm[5], Rm[8]};
+  const R cc[3] = {s.px + ca[0] * zo, s.py + ca[1] * zo, s.pz + ca[2] * zo};
+  const int end = base + D;
+  auto near = [&](int j) { return dc_near(L, cc, j, c.dd_reach2); };
+
+  // ---- setup: drone columns
+  const R q00 = k.ijx * Rm[0], q01 = k.ijy * Rm[1], q02 = k.ijz * Rm[2];
+  const R q10 = k.ijx * Rm[3], q11 = k.ijy * Rm[4], q12 = k.ijz * Rm[5];
+  const R q20 = k.ijx * Rm[6], q21 = k.ijy * Rm[7], q22 = k.ijz * Rm[8];
+  dc[I00][ln] = pc_dot(q00, q01, q02, Rm[0], Rm[1], Rm[2]);
+  dc[I01][ln] = pc_dot(q00, q01, q02, Rm[3], Rm[4], Rm[5]);
+  dc[I02][ln] = pc_dot(q00, q01, q02, Rm[6], Rm[7], Rm[8]);
+  dc[I11][ln] = pc_dot(q10, q11, q12, Rm[3], Rm[4], Rm[5]);
+  dc[I12][ln] = pc_dot(q10, q11, q12, Rm[6], Rm[7], Rm[8]);
+  dc[I22][ln] = pc_dot(q20, q21, q22, Rm[6], Rm[7], Rm[8]);
+  dc[PX][ln] = s.px; dc[PY][ln] = s.py; dc[PZ][ln] = s.pz;
+  dc[VX][ln] = s.vx; dc[VY][ln] = s.vy; dc[VZ][ln] = s.vz;
+  dc[WX][ln] = s.wx; dc[WY][ln] = s.wy; dc[WZ][ln] = s.wz;
+  dc[DLX][ln] = R(0); dc[DLY][ln] = R(0); dc[DLZ][ln] = R(0);
+  dc[DAX][ln] = R(0); dc[DAY][ln] = R(0); dc[DAZ][ln] = R(0);
+  sij[0][ln] = -1;
+  stouch[ln] = 0;
+  // pass 1: this lane's contact count (pairs (ln, j > ln))
+  auto contact = [&](int j, R n[3], R pb[3], R& dist) {
+    const R cb[3] = {dc[CX][j], dc[CY][j], dc[CZ][j]}, ab[3] = {dc[AX][j], dc[AY][j], dc[AZ][j]};
+    pair_geometry(cc, ca, cb, ab, r, hh, n, pb, dist);
+    return dist < c.brk;
+  };
+  int cnt = 0;
+  if (cand) {
+    for (int j = ln + 1; j < end; ++j) {
+      if (!near(j)) continue;
+      R n[3], pb[3], dist;
+      if (contact(j, n, pb, dist)) ++cnt;
+    }
+  }
+  scnt[ln] = cnt;
+  wave_lds_sync();
+  int slot = 0;
+  for (int x = base; x < ln; ++x) slot += scnt[x];
+  // pass 2: the rows of this lane's contacts, into the env's slot columns
+  if (cnt > 0) {
+    for (int j = ln + 1; j < end && slot < D; ++j) {
+      if (!near(j)) continue;
+      R n[3], pb[3], dist;
+      if (!contact(j, n, pb, dist)) continue;
+      const int col = base + slot;
+      ++slot;
+      const R pa[3] = {pb[0] + n[0] * dist, pb[1] + n[1] * dist, pb[2] + n[2] * dist};
+      const R ra[3] = {pa[0] - s.px, pa[1] - s.py, pa[2] - s.pz};
+      const R rb[3] = {pb[0] - dc[PX][j], pb[1] - dc[PY][j], pb[2] - dc[PZ][j]};
+      R t1[3], t2[3];
+      plane_space(n, t1, t2);
+      const R* dirs[3] = {n, t1, t2};
+      const R jb[6] = {dc[I00][j], dc[I01][j], dc[I02][j], dc[I11][j], dc[I12][j], dc[I22][j]};
+      const R ja[6] = {dc[I00][ln], dc[I01][ln], dc[I02][ln], dc[I11][ln], dc[I12][ln], dc[I22][ln]};
+      const R dvx = s.vx - dc[VX][j], dvy = s.vy - dc[VY][j], dvz = s.vz - dc[VZ][j];
+      for (int q = 0; q < 3; ++q) {
+        const R* d = dirs[q];
+        const R aax = ra[1] * d[2] - ra[2] * d[1], aay = ra[2] * d[0] - ra[0] * d[2], aaz = ra[0] * d[1] - ra[1] * d[0];
+        const R abx = rb[1] * d[2] - rb[2] * d[1], aby = rb[2] * d[0] - rb[0] * d[2], abz = rb[0] * d[1] - rb[1] * d[0];
+        const R gax = pc_dot(ja[0], ja[1], ja[2], aax, aay, aaz), gay = pc_dot(ja[1], ja[3], ja[4], aax, aay, aaz),
+                gaz = pc_dot(ja[2], ja[4], ja[5], aax, aay, aaz);
+        const R gbx = pc_dot(jb[0], jb[1], jb[2], abx, aby, abz), gby = pc_dot(jb[1], jb[3], jb[4], abx, aby, abz),
+                gbz = pc_dot(jb[2], jb[4], jb[5], abx, aby, abz);
+        const R jd = (k.inv_m + k.inv_m + pc_dot(aax, aay, aaz, gax, gay, gaz)) + pc_dot(abx, aby, abz, gbx, gby, gbz);
+        const R rel = (pc_dot(d[0], d[1], d[2], dvx, dvy, dvz) + pc_dot(aax, aay, aaz, s.wx, s.wy, s.wz)) -
+                      pc_dot(abx, aby, abz, dc[WX][j], dc[WY][j], dc[WZ][j]);
+        R rhs;
+        if (q == 0) {
+          const R pen = dist + c.slop;
+          rhs = pen > R(0) ? (-rel - pen / k.dt) / jd : (-pen * c.erp / k.dt - rel) / jd;
+          sc[JDN][col] = jd;
+        } else {
+          rhs = -rel / jd;
+        }
+        sc[RH0 + q][col] = rhs;
+        sc[JI0 + q][col] = R(1) / jd;
+        sc[LM0 + q][col] = R(0);
+      }
+      sc[RAX][col] = ra[0]; sc[RAY][col] = ra[1]; sc[RAZ][col] = ra[2];
+      sc[RBX][col] = rb[0]; sc[RBY][col] = rb[1]; sc[RBZ][col] = rb[2];
+      sc[NX][col] = n[0]; sc[NY][col] = n[1]; sc[NZ][col] = n[2];
+      sc[T1X][col] = t1[0]; sc[T1Y][col] = t1[1]; sc[T1Z][col] = t1[2];
+      sc[T2X][col] = t2[0]; sc[T2Y][col] = t2[1]; sc[T2Z][col] = t2[2];
+      sij[0][col] = ln;
+      sij[1][col] = j;
+      stouch[ln] = 1;
+      stouch[j] = 1;
+    }
+  }
+  wave_lds_sync();
+
+  // ---- projected Gauss-Seidel per env
+  const int dl = ln - base;
+  const bool own = sij[0][ln] >= 0;
+  bool envdone = true;
+  for (int x = base; x < end; ++x) envdone = envdone && sij[0][x] < 0;
+  // one row q of the slot in column `col` (the owner lane): J.dv of the two drones
+  auto row = [&](int col, int q, int& i, int& j, R d[3], R a_[3], R b_[3], R ga[3], R gb[3]) {
+    i = sij[0][col];
+    j = sij[1][col];
+    d[0] = sc[NX + 3 * q][col]; d[1] = sc[NY + 3 * q][col]; d[2] = sc[NZ + 3 * q][col];
+    const R ra0 = sc[RAX][col], ra1 = sc[RAY][col], ra2 = sc[RAZ][col];
+    const R rb0 = sc[RBX][col], rb1 = sc[RBY][col], rb2 = sc[RBZ][col];
+    a_[0] = ra1 * d[2] - ra2 * d[1]; a_[1] = ra2 * d[0] - ra0 * d[2]; a_[2] = ra0 * d[1] - ra1 * d[0];
+    b_[0] = rb1 * d[2] - rb2 * d[1]; b_[1] = rb2 * d[0] - rb0 * d[2]; b_[2] = rb0 * d[1] - rb1 * d[0];
+    ga[0] = pc_dot(dc[I00][i], dc[I01][i], dc[I02][i], a_[0], a_[1], a_[2]);
+    ga[1] = pc_dot(dc[I01][i], dc[I11][i], dc[I12][i], a_[0], a_[1], a_[2]);
+    ga[2] = pc_dot(dc[I02][i], dc[I12][i], dc[I22][i], a_[0], a_[1], a_[2]);
+    gb[0] = pc_dot(dc[I00][j], dc[I01][j], dc[I02][j], b_[0], b_[1], b_[2]);
+    gb[1] = pc_dot(dc[I01][j], dc[I11][j], dc[I12][j], b_[0], b_[1], b_[2]);
+    gb[2] = pc_dot(dc[I02][j], dc[I12][j], dc[I22][j], b_[0], b_[1], b_[2]);
+    return (pc_dot(d[0], d[1], d[2], dc[DLX][i] - dc[DLX][j], dc[DLY][i] - dc[DLY][j], dc[DLZ][i] - dc[DLZ][j]) +
+            pc_dot(a_[0], a_[1], a_[2], dc[DAX][i], dc[DAY][i], dc[DAZ][i])) -
+           pc_dot(b_[0], b_[1], b_[2], dc[DAX][j], dc[DAY][j], dc[DAZ][j]);
+  };
+  auto apply = [&](int i, int j, const R d[3], const R ga[3], const R gb[3], R delta) {
+    const R dm = k.inv_m * delta;
+    dc[DLX][i] = dc[DLX][i] + d[0] * dm; dc[DLY][i] = dc[DLY][i] + d[1] * dm; dc[DLZ][i] = dc[DLZ][i] + d[2] * dm;
+    dc[DAX][i] = dc[DAX][i] + ga[0] * delta; dc[DAY][i] = dc[DAY][i] + ga[1] * delta;
+    dc[DAZ][i] = dc[DAZ][i] + ga[2] * delta;
+    dc[DLX][j] = dc[DLX][j] - d[0] * dm; dc[DLY][j] = dc[DLY][j] - d[1] * dm; dc[DLZ][j] = dc[DLZ][j] - d[2] * dm;
+    dc[DAX][j] = dc[DAX][j] - gb[0] * delta; dc[DAY][j] = dc[DAY][j] - gb[1] * delta;
+    dc[DAZ][j] = dc[DAZ][j] - gb[2] * delta;
+  };
+  for (int it = 0; it < c.iters; ++it) {
+    if (__ballot(!envdone) == 0ull) break;
+    R res = R(0);
+    for (int kk = 0; kk < D; ++kk) {                 // normal rows, slot order
+      if (dl == kk && own && !envdone) {
+        int i, j;
+        R d[3], a_[3], b_[3], ga[3], gb[3];
+        const R jv = row(ln, 0, i, j, d, a_, b_, ga, gb);
+        R delta = sc[RH0][ln] - sc[JI0][ln] * jv;
+        const R lam = sc[LM0][ln];
+        const R sum = lam + delta;
+        const bool neg = sum < R(0);
+        delta = neg ? -lam : delta;
+        sc[LM0][ln] = neg ? R(0) : sum;
+        apply(i, j, d, ga, gb, delta);
+        const R rr = delta * sc[JDN][ln];
+        res = g_fmax(res, rr * rr);
+      }
+      wave_lds_sync();
+    }
+    for (int kk = 0; kk < D; ++kk) {                 // friction pairs on the cone
+      if (dl == kk && own && !envdone && sc[LM0][ln] > R(0)) {
+        const R lim = c.dd_mu * sc[LM0][ln];
+        int i, j;
+        R d1v[3], a1[3], b1[3], ga1[3], gb1[3], d2v[3], a2[3], b2[3], ga2[3], gb2[3];
+        const R j1 = row(ln, 1, i, j, d1v, a1, b1, ga1, gb1);
+        const R j2 = row(ln, 2, i, j, d2v, a2, b2, ga2, gb2);
+        const R l1 = sc[LM1][ln], l2 = sc[LM2][ln];
+        R s1 = l1 + (sc[RH1][ln] - sc[JI1][ln] * j1);
+        R s2 = l2 + (sc[RH2][ln] - sc[JI2][ln] * j2);
+        const R m2 = s1 * s1 + s2 * s2;
+        if (m2 > lim * lim) {
+          const R f = lim / g_sqrt(m2);
+          s1 = s1 * f;
+          s2 = s2 * f;
+        }
+        const R e1 = s1 - l1, e2 = s2 - l2;
+        sc[LM1][ln] = s1;
+        sc[LM2][ln] = s2;
+        apply(i, j, d1v, ga1, gb1, e1);
+        apply(i, j, d2v, ga2, gb2, e2);
+        const R rr = e1 + e2;
+        res = g_fmax(res, rr * rr);
+      }
+      wave_lds_sync();
+    }
+    dc[RES][ln] = res;
+    wave_lds_sync();
+    R er = R(0);
+    for (int x = base; x < end; ++x) er = g_fmax(er, dc[RES][x]);
+    envdone = envdone || er <= c.resid;
+    wave_lds_sync();
+  }
+  if (stouch[ln]) {
+    s.vx = s.vx + dc[DLX][ln]; s.vy = s.vy + dc[DLY][ln]; s.vz = s.vz + dc[DLZ][ln];
+    s.wx = s.wx + dc[DAX][ln]; s.wy = s.wy + dc[DAY][ln]; s.wz = s.wz + dc[DAZ][ln];
+  }
+  wave_lds_sync();   // the columns are rewritten by the next substep's call
+}
+// the hook bullet_substep calls (multi-drone envs of one-wave blocks)
+struct DcHook {
+  int tid, base, D;
+  bool active;
+  template <typename R>
+  __device__ __forceinline__ void operator()(Drone<R>& s, const R* Rm, const Consts<R>& c, const DynK<R>& k) const {
+    DcLds<R>& L = dc_lds<R>();
+    const int ln = tid & (kWave - 1);
+    const R zo = c.cyl_zoff;
+    const R cc[3] = {s.px + Rm[2] * zo, s.py + Rm[5] * zo, s.pz + Rm[8] * zo};
+    L.dc[DC_CX][ln] = cc[0]; L.dc[DC_CY][ln] = cc[1]; L.dc[DC_CZ][ln] = cc[2];
+    L.dc[DC_AX][ln] = Rm[2]; L.dc[DC_AY][ln] = Rm[5]; L.dc[DC_AZ][ln] = Rm[8];
+    wave_lds_sync();
+    bool cand = false;
+    if (active)
+      for (int j = ln + 1; j < base + D; ++j) cand = cand || dc_near(L, cc, j, c.dd_reach2);
+    // the common case: no pair of the wave within reach
+    if (GPD_RARE(__ballot(cand) != 0ull)) drone_contact<R>(s, Rm, c, k, ln, base, D, cand);
+    wave_lds_sync();   // the centre columns are rewritten by the next substep
+  }
+};
+
 // One physics substep of every drone of the block, including the readback that precedes it
 // (BaseAviary.py:343-372 loop body).  MULTI: envs have D > 1 drones and may need downwash.
 template <typename R, bool MULTI, int PF, bool ANGV = true>
 __device__ __forceinline__ void substep_block(Drone<R>& s, R rpm[4], R W[4], R last[4],
                                               const Consts<R>& c, DynK<R>& k, R* sx, R* sy, R* sz, int tid,
-                                              int base, int D, DwPairs pairs = DwPairs{0, 0}, R* spair = nullptr) {
+                                              int base, int D, DwPairs pairs = DwPairs{0, 0}, R* spair = nullptr,
+                                              bool active = true) {
   R dw = R(0);
   if (MULTI && pf_on<PF>(k.flags, F_DW)) {
     sx[tid] = s.px; sy[tid] = s.py; sz[tid] = s.pz;
@@ -287,7 +648,8 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, R rpm[4], R W[4], R l
     }
     wave_lds_sync();
   }
-  dyn_substep<R, PF, ANGV>(s, rpm, W, last, dw, c, k);
+  if (MULTI) dyn_substep<R, PF, ANGV, 1, DcHook>(s, rpm, W, last, dw, c, k, DcHook{tid, base, D, active});
+  else dyn_substep<R, PF, ANGV>(s, rpm, W, last, dw, c, k);
 }
 
 // Bytes of dynamic LDS the step kernel needs for its observation tile: the row's columns
@@ -513,7 +875,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
   history_dma();   // diagnostic build: the DMA behind the state loads instead of the first substep
 #endif
   if (dk.nsub > 1) {
-    substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
+    substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, active);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
     GPD_STAMP(1);
@@ -521,9 +883,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
     history_dma();
 #endif
     for (int it = 1; it < dk.nsub - 1; ++it)
-      substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
+      substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, active);
   }
-  substep_block<R, MULTI, PF, true>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair);
+  substep_block<R, MULTI, PF, true>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, active);
 #pragma unroll
   for (int k = 0; k < 4; ++k) last[k] = rpm[k];
 #ifndef GPD_DMA_EARLY
@@ -1344,7 +1706,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_INTEG
     if (t + 2 < n_sub) load4(t + 2, nxt2);
     R W[4];
     rpm_wrench<R, PF>(rpm, dk, c, W);
-    substep_block<R, MULTI, PF>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D);
+    substep_block<R, MULTI, PF>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, DwPairs{0, 0}, nullptr, active);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];
     if (TRAJ && active) {   // TRAJ: the trajectory variant (its readback / Euler registers stay out of the other)

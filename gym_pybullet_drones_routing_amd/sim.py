@@ -21,7 +21,8 @@ _ACTS = {ActionType.RPM: _lib.GPD_ACT_RPM, ActionType.ONE_D_RPM: _lib.GPD_ACT_ON
 PID_ACTS = (ActionType.PID, ActionType.VEL, ActionType.ONE_D_PID)
 _TASKS = {"none": _lib.GPD_TASK_NONE, "hover": _lib.GPD_TASK_HOVER, "multihover": _lib.GPD_TASK_MULTIHOVER}
 _AERO = {"gnd": _lib.GPD_F_GND, "drag": _lib.GPD_F_DRAG, "dw": _lib.GPD_F_DW, "geom": _lib.GPD_F_GEOM_WRENCH,
-         "bullet": _lib.GPD_F_BULLET, "no_plane": _lib.GPD_F_NO_PLANE}
+         "bullet": _lib.GPD_F_BULLET, "no_plane": _lib.GPD_F_NO_PLANE,
+         "no_drone_contact": _lib.GPD_F_NO_DRONE_CONTACT}
 _PHYSICS = {
     Physics.DYN: (),
     Physics.PYB: ("bullet",),
@@ -46,19 +47,21 @@ def physics_flags(physics=Physics.DYN, aero=()):
     the reference's forces (``_physics`` / ``_groundEffect`` / ``_drag`` / ``_downwash``,
     :679-811) to a restated Bullet3 multibody base step (``p.stepSimulation``, :369-370; SURVEY
     §8 f3): default damping, world-frame angular velocity, exponential-map orientation, and the
-    collision cylinder's contact with the ground plane (``plane.urdf``, BaseAviary.py:484).
-    Drone <-> drone collisions are not reproduced, which multi-drone envs report once with a
-    warning.  ``aero`` adds terms by name (``gnd``, ``drag``, ``dw``, ``geom``, ``bullet``,
-    ``no_plane``), e.g. the aero terms on the DYN integrator (BASELINE config 3), or
-    ``no_plane`` for the reference's commented-out plane collision filter (:500-503).
+    collision cylinder's contact with the ground plane (``plane.urdf``, BaseAviary.py:484) and,
+    in envs of several drones, with the env's other drones (every drone is a colliding body,
+    :486-491; envs of more than 64 drones skip it with a warning).  ``aero`` adds terms by name
+    (``gnd``, ``drag``, ``dw``, ``geom``, ``bullet``, ``no_plane``, ``no_drone_contact``), e.g.
+    the aero terms on the DYN integrator (BASELINE config 3), ``no_plane`` for the reference's
+    commented-out plane collision filter (:500-503), or ``no_drone_contact``.
     """
     physics = Physics(physics)
     terms = set(_PHYSICS[physics]) | set(aero)
     unknown = terms - set(_AERO)
     if unknown:
         raise ValueError(f"unknown aero terms {sorted(unknown)}; expected a subset of {sorted(_AERO)}")
-    if "no_plane" in terms and "bullet" not in terms:
-        raise ValueError("'no_plane' applies to the Physics.PYB* modes only (Physics.DYN has no contacts)")
+    for t in ("no_plane", "no_drone_contact"):
+        if t in terms and "bullet" not in terms:
+            raise ValueError(f"'{t}' applies to the Physics.PYB* modes only (Physics.DYN has no contacts)")
     flags = 0
     for t in terms:
         flags |= _AERO[t]
@@ -133,9 +136,10 @@ class BatchedAviarySim:
         cfg.act_type = _ACTS[act]
         cfg.task = _TASKS[task]
         cfg.physics_flags = physics_flags(physics, aero)
-        if cfg.physics_flags & _lib.GPD_F_BULLET and self.drones_per_env > 1:
-            _warn_once("pyb_multi", f"{Physics(physics)}: drone <-> drone collisions are not restated "
-                       "(the ground-plane contact is)")
+        if cfg.physics_flags & _lib.GPD_F_BULLET and self.drones_per_env > 64 \
+                and not cfg.physics_flags & _lib.GPD_F_NO_DRONE_CONTACT:
+            _warn_once("pyb_wide", f"{Physics(physics)}: envs of more than 64 drones skip the drone <-> "
+                       "drone contact (the ground-plane contact applies)")
         cfg.precision = _lib.GPD_F32 if precision == "f32" else _lib.GPD_F64
         cfg.autoreset = 1 if autoreset else 0
         cfg.episode_len_sec = float(episode_len_sec)

@@ -89,6 +89,9 @@ extern "C" {
                                  of _dynamics; implies GEOM_WRENCH */
 #define GPD_F_NO_PLANE 32     /* with GPD_F_BULLET: no drone <-> plane contact (the reference's
                                  commented-out setCollisionFilterPair, BaseAviary.py:500-503) */
+#define GPD_F_NO_DRONE_CONTACT 64 /* with GPD_F_BULLET: no drone <-> drone contact between the drones
+                                 of an env (on by default: every drone is a colliding Bullet body,
+                                 BaseAviary.py:486-491) */
 
 /* precision */
 #define GPD_F32 0

@@ -42,8 +42,10 @@ Ground-plane contact (``p.loadURDF("plane.urdf")``, ``:484``; the drone <-> plan
 at ``:500-503`` is commented out, so the pair collides) is restated as ``plane_contact`` below:
 Bullet's multibody contact constraints solved by projected Gauss-Seidel inside
 ``btMultiBodyConstraintSolver`` between the velocity update and ``integrateTransforms``.  The
-contact set is this restatement's own (see ``plane_contact``); drone <-> drone collisions
-(cylinder vs cylinder, MultiHoverAviary) are not restated.  Bit-level rounding of Bullet's own
+contact set is this restatement's own (see ``plane_contact``).  Drone <-> drone collisions
+(cylinder vs cylinder, MultiHoverAviary's drones, ``:486-491``) are restated as ``drone_contact``:
+one contact per pair from the margin-shrunk cores' closest points, solved with the same rows
+between two moving bodies before the plane solve.  Bit-level rounding of Bullet's own
 operation order (the world <-> base round trips of the link forces, the 6x6 inverse of the
 articulated inertia) is not reproduced either; the restatement is exact in exact arithmetic.
 
@@ -112,6 +114,16 @@ def multibody_step(pos, q_s, vel_w, omega_w, f_base, t_base, f_world, m, inertia
     base COM); ``f_world``: world-frame base force (gravity).  ``cylinder`` = (radius,
     half_height, z_offset) of the collision cylinder turns on the ground-plane contact
     (``plane_contact``); None = free flight.  Returns the new (pos, q_s, vel_w, omega_w)."""
+    q_wb, rot, vel_new, omega_new = multibody_velocity(pos, q_s, vel_w, omega_w, f_base, t_base, f_world, m,
+                                                       inertia, dt, lin_damp, ang_damp, max_vel)
+    return multibody_finish(pos, q_wb, rot, vel_new, omega_new, m, inertia, dt, cylinder)
+
+
+def multibody_velocity(pos, q_s, vel_w, omega_w, f_base, t_base, f_world, m, inertia, dt,
+                       lin_damp=LIN_DAMP, ang_damp=ANG_DAMP, max_vel=MAX_COORD_VEL):
+    """The unconstrained half of ``multibody_step`` (solveExternalForces).  Returns (q_wb, rot,
+    vel_new, omega_new) for ``multibody_finish``; envs of several drones run it for every drone,
+    then ``drone_contact`` over the env, then ``multibody_finish`` per drone."""
     inertia = np.asarray(inertia, dtype=np.float64)
     q_wb = qconj(q_s)                                        # m_baseQuat
     rot = quat_to_mat(q_wb)                                  # rot_from_parent[0]: world -> base
@@ -130,6 +142,12 @@ def multibody_step(pos, q_s, vel_w, omega_w, f_base, t_base, f_world, m, inertia
     vdot = rot.T @ (acc_lin + np.cross(w, v))
     omega_new = np.clip(np.asarray(omega_w, dtype=np.float64) + wdot * dt, -max_vel, max_vel)
     vel_new = np.clip(np.asarray(vel_w, dtype=np.float64) + vdot * dt, -max_vel, max_vel)
+    return q_wb, rot, vel_new, omega_new
+
+
+def multibody_finish(pos, q_wb, rot, vel_new, omega_new, m, inertia, dt, cylinder=None):
+    """The constrained half of ``multibody_step``: the ground-plane contact (solveConstraints)
+    and integrateTransforms.  Returns the new (pos, q_s, vel_w, omega_w)."""
     if cylinder is not None:                                 # solveConstraints, before integrateTransforms
         vel_new, omega_new = plane_contact(pos, rot.T, vel_new, omega_new, m, inertia, dt, *cylinder)
     pos_new = np.asarray(pos, dtype=np.float64) + dt * vel_new
@@ -279,3 +297,204 @@ def plane_contact(pos, rot_bw, vel_w, omega_w, m, inertia, dt, radius, half_heig
             break
     return (np.asarray(vel_w, dtype=np.float64) + rot_bw @ dvl,
             np.asarray(omega_w, dtype=np.float64) + rot_bw @ dva)
+
+
+# ---------------------------------------------------------------------------- drone <-> drone contact
+# MultiHoverAviary's drones are colliding Bullet bodies (BaseAviary.py:486-491, stepped together
+# by :369-370).  Bullet finds a cylinder pair's contact with GJK / EPA and keeps it in a persistent
+# manifold; this restatement's own deterministic contact set (parity unpinned, like the plane's):
+# one point per pair per step from the closest points of the two cylinders' margin-shrunk cores.
+FRICTION_DD = 0.5 * 0.5     # drone x drone combined friction (btCollisionObject default 0.5 each)
+PAIR_ROUNDS = 16            # alternating-projection rounds of the pair's closest points
+CORE_MARGINS = (0.001, 0.003, 0.006, 0.011)   # core shrink per level (the first = the URDF margin)
+CORE_SEP = 1e-4             # core distance below which a level has no well-conditioned normal
+SIMDSQRT12 = 0.7071067811865475244008443621048490
+
+
+def plane_space(n):
+    """btPlaneSpace1: the two friction directions of a contact normal."""
+    if abs(n[2]) > SIMDSQRT12:
+        a = n[1] * n[1] + n[2] * n[2]
+        k = 1.0 / math.sqrt(a)
+        p = np.array([0.0, -n[2] * k, n[1] * k])
+        q = np.array([a * k, -n[0] * p[2], n[0] * p[1]])
+    else:
+        a = n[0] * n[0] + n[1] * n[1]
+        k = 1.0 / math.sqrt(a)
+        p = np.array([-n[1] * k, n[0] * k, 0.0])
+        q = np.array([-n[2] * p[1], n[2] * p[0], a * k])
+    return p, q
+
+
+def cyl_project(c, a, radius, half_height, x):
+    """Closest point of the solid cylinder (centre c, unit axis a) to x."""
+    d = x - c
+    t = float(d @ a)
+    tc = min(max(t, -half_height), half_height)
+    rad = d - t * a
+    rho2 = float(rad @ rad)
+    if rho2 > radius * radius:
+        rad = rad * (radius / math.sqrt(rho2))
+    return c + tc * a + rad
+
+
+def cyl_extent(u, a, radius, half_height):
+    """Half-width of the cylinder (unit axis a) along the unit direction u."""
+    ua = float(u @ a)
+    return half_height * abs(ua) + radius * math.sqrt(max(0.0, 1.0 - ua * ua))
+
+
+def pair_geometry(ca, aa, cb, ab, radius, half_height):
+    """One contact of cylinders A and B: (normal on B pointing to A, point on B, distance;
+    negative = penetration).  Bullet's margin scheme: the closest points of the CORE cylinders
+    (radius and half-height shrunk by a margin m) give the normal and the distance
+    core_distance - 2 m, the point on B's surface is B's core point + m n.  Core closest points by
+    PAIR_ROUNDS rounds of alternating projection from B's centre (in B-centred coordinates);
+    a level whose cores come within CORE_SEP of each other (overlapping or nearly so: no
+    well-conditioned normal) passes to the next, thicker margin (CORE_MARGINS: penetrations up to
+    ~2 cm).  Deeper overlaps: the axis of least overlap among the centre line and the two
+    cylinder axes, at the point the last projections reached (Bullet runs EPA here)."""
+    cl = ca - cb
+    zero = np.zeros(3)
+    for mg in CORE_MARGINS:
+        r, h = radius - mg, half_height - mg
+        xb = zero.copy()
+        for _ in range(PAIR_ROUNDS):
+            pa = cyl_project(cl, aa, r, h, xb)
+            xb = cyl_project(zero, ab, r, h, pa)
+        dv = pa - xb
+        d2 = float(dv @ dv)
+        if d2 > CORE_SEP * CORE_SEP:
+            dc = math.sqrt(d2)
+            n = dv / dc
+            return n, cb + (xb + n * mg), dc - 2.0 * mg
+    cands = []
+    c2 = float(cl @ cl)
+    if c2 > 1e-24:
+        cands.append(cl / math.sqrt(c2))
+    cands += [aa, ab]
+    best, best_ov = None, None
+    for u in cands:
+        u = -u if float(u @ cl) < 0.0 else u
+        ov = cyl_extent(u, aa, radius, half_height) + cyl_extent(u, ab, radius, half_height) - float(u @ cl)
+        if best is None or ov < best_ov:
+            best, best_ov = u, ov
+    return best, cb + xb, -best_ov
+
+
+def drone_contacts(pos, rot_bw, radius, half_height, z_offset):
+    """The env's contacts in solve order: pairs (i, j), i < j, lexicographic, whose cylinders'
+    bounding spheres come within the breaking threshold and whose distance is below it; at most
+    D of them (an env has D solver slots; more simultaneous contacts are dropped)."""
+    D = pos.shape[0]
+    brk = breaking_threshold(radius, half_height)
+    bs = math.sqrt(radius * radius + half_height * half_height)
+    reach = 2.0 * bs + brk
+    axes = [rot_bw[i][:, 2].copy() for i in range(D)]
+    cent = [pos[i] + axes[i] * z_offset for i in range(D)]
+    out = []
+    for i in range(D):
+        for j in range(i + 1, D):
+            dc = cent[i] - cent[j]
+            if not float(dc @ dc) < reach * reach:
+                continue
+            n, pb, dist = pair_geometry(cent[i], axes[i], cent[j], axes[j], radius, half_height)
+            if dist < brk and len(out) < D:
+                out.append((i, j, n, pb, dist))
+    return out
+
+
+def drone_contact(pos, rot_bw, vel_w, omega_w, m, inertia, dt, radius, half_height, z_offset):
+    """Drone <-> drone contact of one env for one ``stepSimulation``: the rows of
+    ``plane_contact`` between two moving bodies, solved before it (between the unconstrained
+    velocity update and the ground-plane solve; Bullet solves both in one island).
+
+    ``pos`` [D, 3] start-of-step positions, ``rot_bw`` [D, 3, 3] body -> world, ``vel_w`` /
+    ``omega_w`` [D, 3] after the unconstrained update.  Per contact (A = i, B = j, normal n from B
+    to A, point on B ``pb``, point on A ``pb + n dist``): rows along n and btPlaneSpace1(n) with
+    arms from each COM, effective mass 2/m + a_A.I_A^-1 a_A + a_B.I_B^-1 a_B (world inverse
+    inertia R diag(1/I) R^T), the plane's rhs rules (speculative / ERP, slop) and friction cone
+    (FRICTION_DD); Gauss-Seidel over the env's normal rows, then its friction pairs, in contact
+    order, until the largest squared residual <= RESIDUAL_THRESHOLD or SOLVER_ITERS.  Returns
+    the new (vel, omega) [D, 3]."""
+    pos = np.asarray(pos, dtype=np.float64)
+    vel = np.array(vel_w, dtype=np.float64)
+    omg = np.array(omega_w, dtype=np.float64)
+    cons = drone_contacts(pos, rot_bw, radius, half_height, z_offset)
+    if not cons:
+        return vel, omg
+    D = pos.shape[0]
+    im = 1.0 / m
+    inv_i = 1.0 / np.asarray(inertia, dtype=np.float64)
+    iw = [rot_bw[i] @ np.diag(inv_i) @ rot_bw[i].T for i in range(D)]
+    rows = []
+    for (i, j, n, pb, dist) in cons:
+        pa = pb + n * dist
+        ra, rb = pa - pos[i], pb - pos[j]
+        t1, t2 = plane_space(n)
+        row = dict(i=i, j=j, d=(n, t1, t2), aa=[], ab=[], ga=[], gb=[], jdi=[], rhs=[], lam=[0.0, 0.0, 0.0])
+        for k, d in enumerate((n, t1, t2)):
+            aa, ab = np.cross(ra, d), np.cross(rb, d)
+            ga, gb = iw[i] @ aa, iw[j] @ ab
+            jd = (2.0 * im + float(aa @ ga)) + float(ab @ gb)
+            rel = float(d @ (vel[i] - vel[j])) + float(aa @ omg[i]) - float(ab @ omg[j])
+            if k == 0:
+                pen = dist + LINEAR_SLOP
+                rhs = (-rel - pen / dt) / jd if pen > 0 else (-pen * CONTACT_ERP / dt - rel) / jd
+                row["jdn"] = jd
+            else:
+                rhs = -rel / jd
+            row["aa"].append(aa); row["ab"].append(ab); row["ga"].append(ga); row["gb"].append(gb)
+            row["jdi"].append(1.0 / jd); row["rhs"].append(rhs)
+        rows.append(row)
+    dl = np.zeros((D, 3))
+    da = np.zeros((D, 3))
+
+    def jv(c, k):
+        i, j = c["i"], c["j"]
+        return float(c["d"][k] @ (dl[i] - dl[j])) + float(c["aa"][k] @ da[i]) - float(c["ab"][k] @ da[j])
+
+    def apply(c, k, delta):
+        i, j = c["i"], c["j"]
+        dl[i] += c["d"][k] * (im * delta)
+        da[i] += c["ga"][k] * delta
+        dl[j] -= c["d"][k] * (im * delta)
+        da[j] -= c["gb"][k] * delta
+
+    for _ in range(SOLVER_ITERS):
+        res = 0.0
+        for c in rows:                                        # normal rows
+            delta = c["rhs"][0] - c["jdi"][0] * jv(c, 0)
+            s = c["lam"][0] + delta
+            if s < 0.0:
+                delta = -c["lam"][0]
+                s = 0.0
+            c["lam"][0] = s
+            apply(c, 0, delta)
+            res = max(res, (delta * c["jdn"]) ** 2)
+        for c in rows:                                        # friction pairs (implicit cone)
+            ln = c["lam"][0]
+            if not ln > 0.0:
+                continue
+            lim = FRICTION_DD * ln
+            s1 = c["lam"][1] + (c["rhs"][1] - c["jdi"][1] * jv(c, 1))
+            s2 = c["lam"][2] + (c["rhs"][2] - c["jdi"][2] * jv(c, 2))
+            m2 = s1 * s1 + s2 * s2
+            if m2 > lim * lim:
+                f = lim / math.sqrt(m2)
+                s1 = s1 * f
+                s2 = s2 * f
+            d1 = s1 - c["lam"][1]
+            d2 = s2 - c["lam"][2]
+            c["lam"][1] = s1
+            c["lam"][2] = s2
+            apply(c, 1, d1)
+            apply(c, 2, d2)
+            res = max(res, (d1 + d2) ** 2)
+        if res <= RESIDUAL_THRESHOLD:
+            break
+    touched = sorted({c["i"] for c in rows} | {c["j"] for c in rows})
+    for i in touched:
+        vel[i] = vel[i] + dl[i]
+        omg[i] = omg[i] + da[i]
+    return vel, omg

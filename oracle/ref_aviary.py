@@ -56,7 +56,7 @@ import math
 import numpy as np
 
 from .bullet_math import euler_from_quat, quat_from_euler, quat_roundtrip, quat_to_mat
-from .bullet_mb import multibody_step
+from .bullet_mb import drone_contact, multibody_finish, multibody_velocity
 from .params import derived
 from .ref_pid import RefDSLPID, pid_action_rpm
 
@@ -78,13 +78,16 @@ class RefAviary:
 
     def __init__(self, model="cf2x", num_drones=1, initial_xyzs=None, initial_rpys=None,
                  pyb_freq=240, ctrl_freq=30, act="rpm", task="hover", aero=(), wrench="dyn",
-                 episode_len_sec=8, integrator="dyn"):
+                 episode_len_sec=8, integrator="dyn", drones_per_env=None):
         if pyb_freq % ctrl_freq != 0:
             raise ValueError("[ERROR] in BaseAviary.__init__(), pyb_freq is not divisible by env_freq.")
         p = derived(model)
         self.P = p
         self.MODEL = model
         self.NUM_DRONES = num_drones
+        # drones that collide with each other under PYB* (consecutive groups): the whole
+        # MultiHoverAviary; raw (task "none") instances default to a batch of one-drone envs
+        self.DRONES_PER_ENV = drones_per_env or (num_drones if task == "multihover" else 1)
         self.PYB_FREQ, self.CTRL_FREQ = pyb_freq, ctrl_freq
         self.PYB_STEPS_PER_CTRL = int(pyb_freq / ctrl_freq)
         self.PYB_TIMESTEP = 1. / pyb_freq
@@ -216,7 +219,7 @@ class RefAviary:
     def _bullet_physics(self, rpm, i):
         """PYB* modes: _physics (:679-711) [+ _groundEffect / _drag / _downwash, :715-811] as
         forces on the links, then one p.stepSimulation() (:369-370) restated by
-        bullet_mb.multibody_step.  Body frame: prop forces (0,0,f_k) at r_k, ground effect
+        bullet_mb (the unconstrained half here; _bullet_step_all finishes it).  Body frame: prop forces (0,0,f_k) at r_k, ground effect
         (0,0,g_k) at r_k, downwash (0,0,dw) and drag R^T (drag_factors * vel) at the COM link."""
         forces = np.array(rpm ** 2) * self.KF
         torques = np.array(rpm ** 2) * self.KM
@@ -240,19 +243,44 @@ class RefAviary:
         if "drag" in self.AERO:
             f_base = f_base + quat_to_mat(self.quat[i, :]).T @ self._drag_force(self.last_clipped_action[i, :], i)
         p = self.P
-        pos, q_s, vel, omega = multibody_step(self._b_pos[i], self._b_quat[i], self._b_vel[i], self._b_angv[i],
-                                              f_base, np.array([tx, ty, z_torque]),
-                                              np.array([0.0, 0.0, -p["G"]]) * self.M, self.M,
-                                              np.array([p["ixx"], p["iyy"], p["izz"]]), self.PYB_TIMESTEP,
-                                              cylinder=None if "no_plane" in self.AERO else
-                                              (p["collision_r"], p["collision_h"] / 2, p["collision_z_offset"]))
-        self._b_pos[i], self._b_quat[i], self._b_vel[i], self._b_angv[i] = pos, q_s, vel, omega
-        self.rpy_rates[i, :] = omega
+        return multibody_velocity(self._b_pos[i], self._b_quat[i], self._b_vel[i], self._b_angv[i],
+                                  f_base, np.array([tx, ty, z_torque]),
+                                  np.array([0.0, 0.0, -p["G"]]) * self.M, self.M,
+                                  np.array([p["ixx"], p["iyy"], p["izz"]]), self.PYB_TIMESTEP)
+
+    def _bullet_step_all(self, rpms):
+        """One p.stepSimulation() of every drone (PYB* modes): the unconstrained velocity update
+        of each drone (_bullet_physics), the drone <-> drone contact over the env (envs of D > 1
+        drones, bullet_mb.drone_contact), then each drone's ground-plane contact and position
+        update (bullet_mb.multibody_finish)."""
+        p = self.P
+        cyl = (p["collision_r"], p["collision_h"] / 2, p["collision_z_offset"])
+        inertia = np.array([p["ixx"], p["iyy"], p["izz"]])
+        mids = [self._bullet_physics(rpms[i, :], i) for i in range(self.NUM_DRONES)]
+        G = self.DRONES_PER_ENV
+        if G > 1 and "no_drone_contact" not in self.AERO:
+            for e0 in range(0, self.NUM_DRONES, G):
+                env = mids[e0:e0 + G]
+                vel, omg = drone_contact(self._b_pos[e0:e0 + G], np.array([m[1].T for m in env]),
+                                         np.array([m[2] for m in env]), np.array([m[3] for m in env]),
+                                         self.M, inertia, self.PYB_TIMESTEP, *cyl)
+                mids[e0:e0 + G] = [(m[0], m[1], vel[i], omg[i]) for i, m in enumerate(env)]
+        for i, (q_wb, rot, vel, omega) in enumerate(mids):
+            pos, q_s, vel, omega = multibody_finish(self._b_pos[i], q_wb, rot, vel, omega, self.M, inertia,
+                                                    self.PYB_TIMESTEP, None if "no_plane" in self.AERO else cyl)
+            self._b_pos[i], self._b_quat[i], self._b_vel[i], self._b_angv[i] = pos, q_s, vel, omega
+            self.rpy_rates[i, :] = omega
+
+    def _substep_all(self, rpms):
+        """One physics substep of every drone (BaseAviary.py:368-370)."""
+        if self.INTEGRATOR == "bullet":
+            return self._bullet_step_all(rpms)
+        for i in range(self.NUM_DRONES):
+            self._dynamics(rpms[i, :], i)
 
     def _dynamics(self, rpm, i):
         """BaseAviary._dynamics (:815-874) (+ optional aero wrench, see module doc)."""
-        if self.INTEGRATOR == "bullet":
-            return self._bullet_physics(rpm, i)
+        assert self.INTEGRATOR != "bullet", "PYB* substeps go through _bullet_step_all"
         pos = self.pos[i, :]
         quat = self.quat[i, :]
         vel = self.vel[i, :]
@@ -373,8 +401,7 @@ class RefAviary:
         for _ in range(self.PYB_STEPS_PER_CTRL):
             if self.PYB_STEPS_PER_CTRL > 1 and not plain_pyb:
                 self._updateAndStoreKinematicInformation()
-            for i in range(self.NUM_DRONES):
-                self._dynamics(clipped_action[i, :], i)
+            self._substep_all(clipped_action)
             self.last_clipped_action = clipped_action
         self._updateAndStoreKinematicInformation()
         obs = self._computeObs()
@@ -392,8 +419,7 @@ class RefAviary:
         rpms = np.asarray(rpms, dtype=np.float64)
         out = []
         for t in range(rpms.shape[0]):
-            for i in range(self.NUM_DRONES):
-                self._dynamics(rpms[t, i, :], i)
+            self._substep_all(rpms[t])
             self.last_clipped_action = rpms[t].copy()
             self._updateAndStoreKinematicInformation()
             if record:
