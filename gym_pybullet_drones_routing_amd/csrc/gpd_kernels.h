@@ -291,7 +291,7 @@ __device__ __forceinline__ void cyl_project(R cx, R cy, R cz, R ax, R ay, R az, 
   R rx = dx - t * ax, ry = dy - t * ay, rz = dz - t * az;
   const R rho2 = pc_dot(rx, ry, rz, rx, ry, rz);
   if (rho2 > r * r) {
-    const R f = r / g_sqrt(rho2);
+    const R f = r * g_rsqrt(rho2);   // Newton-refined: within ~1 ulp of r / sqrt(rho2) (the oracle's)
     rx = rx * f; ry = ry * f; rz = rz * f;
   }
   x = (cx + tc * ax) + rx;
@@ -321,10 +321,13 @@ __device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], cons
     R px = R(0), py = R(0), pz = R(0);
     qx = R(0); qy = R(0); qz = R(0);
     for (int it = 0; it < kPairRounds; ++it) {
+      const R ox = qx, oy = qy, oz = qz;
       px = qx; py = qy; pz = qz;
       cyl_project(lx, ly, lz, aa[0], aa[1], aa[2], rc, hc, px, py, pz);
       qx = px; qy = py; qz = pz;
       cyl_project(R(0), R(0), R(0), ab[0], ab[1], ab[2], rc, hc, qx, qy, qz);
+      const R mx = qx - ox, my = qy - oy, mz = qz - oz;
+      if (pc_dot(mx, my, mz, mx, my, mz) <= R(1e-24)) break;   // B's point moved <= 1e-12 m
     }
     const R vx = px - qx, vy = py - qy, vz = pz - qz;
     const R d2 = pc_dot(vx, vy, vz, vx, vy, vz);
@@ -377,6 +380,9 @@ __device__ __forceinline__ void plane_space(const R n[3], R p[3], R q[3]) {
   }
 }
 
+#ifndef GPD_DC_DIAG
+#define GPD_DC_DIAG 0   // diagnostic builds only (scripts/ab_libs.sh): 1 = no pair solve, 2 = one iteration
+#endif
 enum { DC_CX, DC_CY, DC_CZ, DC_AX, DC_AY, DC_AZ, DC_PX, DC_PY, DC_PZ, DC_VX, DC_VY, DC_VZ, DC_WX, DC_WY, DC_WZ,
        DC_I00, DC_I01, DC_I02, DC_I11, DC_I12, DC_I22, DC_DLX, DC_DLY, DC_DLZ, DC_DAX, DC_DAY, DC_DAZ, DC_RES, DC_N };
 template <typename R>
@@ -392,11 +398,31 @@ __device__ __forceinline__ DcLds<R>& dc_lds() {
   __shared__ DcLds<R> x;
   return x;
 }
-// broadphase of lane ln's pairs (ln, j > ln): centres within reach (the centre / axis columns written)
+// broadphase of lane ln's pairs (ln, j > ln) (the centre / axis columns written): centres within
+// reach, then a separating-axis reject over the two axes and the centre line - separation along
+// any axis bounds the distance from below, so a pair separated by more than the breaking
+// threshold (+ 1e-9 against rounding) has no contact in the oracle either; the test only spares
+// the narrowphase, it decides nothing the oracle decides
 template <typename R>
-__device__ __forceinline__ bool dc_near(const DcLds<R>& L, const R cc[3], int j, R reach2) {
+__device__ __forceinline__ bool dc_near(const DcLds<R>& L, const R cc[3], const R ca[3], int j, const Consts<R>& c) {
   const R ex = cc[0] - L.dc[DC_CX][j], ey = cc[1] - L.dc[DC_CY][j], ez = cc[2] - L.dc[DC_CZ][j];
-  return pc_dot(ex, ey, ez, ex, ey, ez) < reach2;
+  const R e2 = pc_dot(ex, ey, ez, ex, ey, ez);
+  if (!(e2 < c.dd_reach2)) return false;
+  const R bx = L.dc[DC_AX][j], by = L.dc[DC_AY][j], bz = L.dc[DC_AZ][j];
+  const R r = c.cyl_r, hh = c.cyl_hh, lim = c.brk + R(1e-9);
+  const R ab = pc_dot(ca[0], ca[1], ca[2], bx, by, bz);
+  const R s2 = R(1) - ab * ab;
+  const R tilt = hh * g_abs(ab) + r * g_sqrt(s2 > R(0) ? s2 : R(0));   // extent of one along the other's axis
+  if (g_abs(pc_dot(ex, ey, ez, ca[0], ca[1], ca[2])) - (hh + tilt) > lim) return false;
+  if (g_abs(pc_dot(ex, ey, ez, bx, by, bz)) - (hh + tilt) > lim) return false;
+  if (e2 > R(0)) {
+    const R l = g_sqrt(e2);
+    const R ua = pc_dot(ex, ey, ez, ca[0], ca[1], ca[2]) / l, ub = pc_dot(ex, ey, ez, bx, by, bz) / l;
+    const R sa = R(1) - ua * ua, sb = R(1) - ub * ub;
+    const R ext = (hh * g_abs(ua) + r * g_sqrt(sa > R(0) ? sa : R(0))) + (hh * g_abs(ub) + r * g_sqrt(sb > R(0) ? sb : R(0)));
+    if (l - ext > lim) return false;
+  }
+  return true;
 }
 // the setup and solve: a call, so that its registers stay out of the substep loop that almost
 // never enters it
@@ -418,7 +444,7 @@ __device__ __noinline__ void drone_contact(Drone<R>& s, const R* Rm, const Const
   const R ca[3] = {Rm[2], Rm[5], Rm[8]};
   const R cc[3] = {s.px + ca[0] * zo, s.py + ca[1] * zo, s.pz + ca[2] * zo};
   const int end = base + D;
-  auto near = [&](int j) { return dc_near(L, cc, j, c.dd_reach2); };
+  auto near = [&](int j) { return dc_near(L, cc, ca, j, c); };
 
   // ---- setup: drone columns
   const R q00 = k.ijx * Rm[0], q01 = k.ijy * Rm[1], q02 = k.ijz * Rm[2];
@@ -443,12 +469,24 @@ __device__ __noinline__ void drone_contact(Drone<R>& s, const R* Rm, const Const
     pair_geometry(cc, ca, cb, ab, r, hh, n, pb, dist);
     return dist < c.brk;
   };
+  // the first kCache contacts' geometry stays in registers for pass 2 (later ones are recomputed)
+  constexpr int kCache = 2;
+  R cn[kCache][3], cpb[kCache][3], cdist[kCache];
+  int cj[kCache] = {-1, -1};
   int cnt = 0;
   if (cand) {
     for (int j = ln + 1; j < end; ++j) {
       if (!near(j)) continue;
       R n[3], pb[3], dist;
-      if (contact(j, n, pb, dist)) ++cnt;
+      if (contact(j, n, pb, dist)) {
+        if (cnt < kCache) {
+#pragma unroll
+          for (int x = 0; x < 3; ++x) { cn[cnt][x] = n[x]; cpb[cnt][x] = pb[x]; }
+          cdist[cnt] = dist;
+          cj[cnt] = j;
+        }
+        ++cnt;
+      }
     }
   }
   scnt[ln] = cnt;
@@ -457,10 +495,19 @@ __device__ __noinline__ void drone_contact(Drone<R>& s, const R* Rm, const Const
   for (int x = base; x < ln; ++x) slot += scnt[x];
   // pass 2: the rows of this lane's contacts, into the env's slot columns
   if (cnt > 0) {
+    int m = 0;
     for (int j = ln + 1; j < end && slot < D; ++j) {
       if (!near(j)) continue;
       R n[3], pb[3], dist;
-      if (!contact(j, n, pb, dist)) continue;
+      if (m < kCache) {
+        if (cj[m] != j) continue;
+#pragma unroll
+        for (int x = 0; x < 3; ++x) { n[x] = cn[m][x]; pb[x] = cpb[m][x]; }
+        dist = cdist[m];
+      } else if (!contact(j, n, pb, dist)) {
+        continue;
+      }
+      ++m;
       const int col = base + slot;
       ++slot;
       const R pa[3] = {pb[0] + n[0] * dist, pb[1] + n[1] * dist, pb[2] + n[2] * dist};
@@ -508,80 +555,108 @@ __device__ __noinline__ void drone_contact(Drone<R>& s, const R* Rm, const Const
   }
   wave_lds_sync();
 
-  // ---- projected Gauss-Seidel per env
+  // ---- projected Gauss-Seidel per env.  The owner lane of a slot keeps its rows in registers
+  // (directions, a = r x d and g = I^-1 a of both drones, rhs, 1/jacDiag, impulses); only the two
+  // drones' velocity deltas go through LDS.  Rounds run over the slots some env of the wave uses.
   const int dl = ln - base;
-  const bool own = sij[0][ln] >= 0;
+  const int oi = sij[0][ln], oj = sij[1][ln];
+  const bool own = oi >= 0;
   bool envdone = true;
   for (int x = base; x < end; ++x) envdone = envdone && sij[0][x] < 0;
-  // one row q of the slot in column `col` (the owner lane): J.dv of the two drones
-  auto row = [&](int col, int q, int& i, int& j, R d[3], R a_[3], R b_[3], R ga[3], R gb[3]) {
-    i = sij[0][col];
-    j = sij[1][col];
-    d[0] = sc[NX + 3 * q][col]; d[1] = sc[NY + 3 * q][col]; d[2] = sc[NZ + 3 * q][col];
-    const R ra0 = sc[RAX][col], ra1 = sc[RAY][col], ra2 = sc[RAZ][col];
-    const R rb0 = sc[RBX][col], rb1 = sc[RBY][col], rb2 = sc[RBZ][col];
-    a_[0] = ra1 * d[2] - ra2 * d[1]; a_[1] = ra2 * d[0] - ra0 * d[2]; a_[2] = ra0 * d[1] - ra1 * d[0];
-    b_[0] = rb1 * d[2] - rb2 * d[1]; b_[1] = rb2 * d[0] - rb0 * d[2]; b_[2] = rb0 * d[1] - rb1 * d[0];
-    ga[0] = pc_dot(dc[I00][i], dc[I01][i], dc[I02][i], a_[0], a_[1], a_[2]);
-    ga[1] = pc_dot(dc[I01][i], dc[I11][i], dc[I12][i], a_[0], a_[1], a_[2]);
-    ga[2] = pc_dot(dc[I02][i], dc[I12][i], dc[I22][i], a_[0], a_[1], a_[2]);
-    gb[0] = pc_dot(dc[I00][j], dc[I01][j], dc[I02][j], b_[0], b_[1], b_[2]);
-    gb[1] = pc_dot(dc[I01][j], dc[I11][j], dc[I12][j], b_[0], b_[1], b_[2]);
-    gb[2] = pc_dot(dc[I02][j], dc[I12][j], dc[I22][j], b_[0], b_[1], b_[2]);
-    return (pc_dot(d[0], d[1], d[2], dc[DLX][i] - dc[DLX][j], dc[DLY][i] - dc[DLY][j], dc[DLZ][i] - dc[DLZ][j]) +
-            pc_dot(a_[0], a_[1], a_[2], dc[DAX][i], dc[DAY][i], dc[DAZ][i])) -
-           pc_dot(b_[0], b_[1], b_[2], dc[DAX][j], dc[DAY][j], dc[DAZ][j]);
+  int rounds = 0;
+  for (int kk = D - 1; kk >= 0 && rounds == 0; --kk)
+    if (__ballot(own && dl == kk) != 0ull) rounds = kk + 1;
+  R rd[3][3], ra_[3][3], rb_[3][3], rga[3][3], rgb[3][3], rhs[3], jdi[3], lam[3] = {R(0), R(0), R(0)}, jdn = R(0);
+  if (own) {
+    const R ra0 = sc[RAX][ln], ra1 = sc[RAY][ln], ra2 = sc[RAZ][ln];
+    const R rb0 = sc[RBX][ln], rb1 = sc[RBY][ln], rb2 = sc[RBZ][ln];
+    const R ia[6] = {dc[I00][oi], dc[I01][oi], dc[I02][oi], dc[I11][oi], dc[I12][oi], dc[I22][oi]};
+    const R ib[6] = {dc[I00][oj], dc[I01][oj], dc[I02][oj], dc[I11][oj], dc[I12][oj], dc[I22][oj]};
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      R* d = rd[q];
+      d[0] = sc[NX + 3 * q][ln]; d[1] = sc[NY + 3 * q][ln]; d[2] = sc[NZ + 3 * q][ln];
+      R* A = ra_[q];
+      R* B = rb_[q];
+      A[0] = ra1 * d[2] - ra2 * d[1]; A[1] = ra2 * d[0] - ra0 * d[2]; A[2] = ra0 * d[1] - ra1 * d[0];
+      B[0] = rb1 * d[2] - rb2 * d[1]; B[1] = rb2 * d[0] - rb0 * d[2]; B[2] = rb0 * d[1] - rb1 * d[0];
+      rga[q][0] = pc_dot(ia[0], ia[1], ia[2], A[0], A[1], A[2]);
+      rga[q][1] = pc_dot(ia[1], ia[3], ia[4], A[0], A[1], A[2]);
+      rga[q][2] = pc_dot(ia[2], ia[4], ia[5], A[0], A[1], A[2]);
+      rgb[q][0] = pc_dot(ib[0], ib[1], ib[2], B[0], B[1], B[2]);
+      rgb[q][1] = pc_dot(ib[1], ib[3], ib[4], B[0], B[1], B[2]);
+      rgb[q][2] = pc_dot(ib[2], ib[4], ib[5], B[0], B[1], B[2]);
+      rhs[q] = sc[RH0 + q][ln];
+      jdi[q] = sc[JI0 + q][ln];
+    }
+    jdn = sc[JDN][ln];
+  }
+  // the two drones' velocity deltas: loaded together, updated, stored together
+  R vi[6], vj[6];
+  auto load_dv = [&]() {
+#pragma unroll
+    for (int x = 0; x < 6; ++x) { vi[x] = dc[DLX + x][oi]; vj[x] = dc[DLX + x][oj]; }
   };
-  auto apply = [&](int i, int j, const R d[3], const R ga[3], const R gb[3], R delta) {
+  auto store_dv = [&]() {
+#pragma unroll
+    for (int x = 0; x < 6; ++x) { dc[DLX + x][oi] = vi[x]; dc[DLX + x][oj] = vj[x]; }
+  };
+  auto jv = [&](int q) {
+    const R* d = rd[q];
+    return (pc_dot(d[0], d[1], d[2], vi[0] - vj[0], vi[1] - vj[1], vi[2] - vj[2]) +
+            pc_dot(ra_[q][0], ra_[q][1], ra_[q][2], vi[3], vi[4], vi[5])) -
+           pc_dot(rb_[q][0], rb_[q][1], rb_[q][2], vj[3], vj[4], vj[5]);
+  };
+  auto apply = [&](int q, R delta) {
     const R dm = k.inv_m * delta;
-    dc[DLX][i] = dc[DLX][i] + d[0] * dm; dc[DLY][i] = dc[DLY][i] + d[1] * dm; dc[DLZ][i] = dc[DLZ][i] + d[2] * dm;
-    dc[DAX][i] = dc[DAX][i] + ga[0] * delta; dc[DAY][i] = dc[DAY][i] + ga[1] * delta;
-    dc[DAZ][i] = dc[DAZ][i] + ga[2] * delta;
-    dc[DLX][j] = dc[DLX][j] - d[0] * dm; dc[DLY][j] = dc[DLY][j] - d[1] * dm; dc[DLZ][j] = dc[DLZ][j] - d[2] * dm;
-    dc[DAX][j] = dc[DAX][j] - gb[0] * delta; dc[DAY][j] = dc[DAY][j] - gb[1] * delta;
-    dc[DAZ][j] = dc[DAZ][j] - gb[2] * delta;
+    const R* d = rd[q];
+    vi[0] = vi[0] + d[0] * dm; vi[1] = vi[1] + d[1] * dm; vi[2] = vi[2] + d[2] * dm;
+    vi[3] = vi[3] + rga[q][0] * delta; vi[4] = vi[4] + rga[q][1] * delta; vi[5] = vi[5] + rga[q][2] * delta;
+    vj[0] = vj[0] - d[0] * dm; vj[1] = vj[1] - d[1] * dm; vj[2] = vj[2] - d[2] * dm;
+    vj[3] = vj[3] - rgb[q][0] * delta; vj[4] = vj[4] - rgb[q][1] * delta; vj[5] = vj[5] - rgb[q][2] * delta;
   };
-  for (int it = 0; it < c.iters; ++it) {
+#if GPD_DC_DIAG == 2
+  const int iters = 1;   // diagnostic build: one Gauss-Seidel iteration per solve
+#else
+  const int iters = c.iters;
+#endif
+  for (int it = 0; it < iters; ++it) {
     if (__ballot(!envdone) == 0ull) break;
     R res = R(0);
-    for (int kk = 0; kk < D; ++kk) {                 // normal rows, slot order
-      if (dl == kk && own && !envdone) {
-        int i, j;
-        R d[3], a_[3], b_[3], ga[3], gb[3];
-        const R jv = row(ln, 0, i, j, d, a_, b_, ga, gb);
-        R delta = sc[RH0][ln] - sc[JI0][ln] * jv;
-        const R lam = sc[LM0][ln];
-        const R sum = lam + delta;
+    const bool mine = own && !envdone;
+    for (int kk = 0; kk < rounds; ++kk) {            // normal rows, slot order
+      if (mine && dl == kk) {
+        load_dv();
+        R delta = rhs[0] - jdi[0] * jv(0);
+        const R sum = lam[0] + delta;
         const bool neg = sum < R(0);
-        delta = neg ? -lam : delta;
-        sc[LM0][ln] = neg ? R(0) : sum;
-        apply(i, j, d, ga, gb, delta);
-        const R rr = delta * sc[JDN][ln];
+        delta = neg ? -lam[0] : delta;
+        lam[0] = neg ? R(0) : sum;
+        apply(0, delta);
+        store_dv();
+        const R rr = delta * jdn;
         res = g_fmax(res, rr * rr);
       }
       wave_lds_sync();
     }
-    for (int kk = 0; kk < D; ++kk) {                 // friction pairs on the cone
-      if (dl == kk && own && !envdone && sc[LM0][ln] > R(0)) {
-        const R lim = c.dd_mu * sc[LM0][ln];
-        int i, j;
-        R d1v[3], a1[3], b1[3], ga1[3], gb1[3], d2v[3], a2[3], b2[3], ga2[3], gb2[3];
-        const R j1 = row(ln, 1, i, j, d1v, a1, b1, ga1, gb1);
-        const R j2 = row(ln, 2, i, j, d2v, a2, b2, ga2, gb2);
-        const R l1 = sc[LM1][ln], l2 = sc[LM2][ln];
-        R s1 = l1 + (sc[RH1][ln] - sc[JI1][ln] * j1);
-        R s2 = l2 + (sc[RH2][ln] - sc[JI2][ln] * j2);
+    for (int kk = 0; kk < rounds; ++kk) {            // friction pairs on the cone
+      if (mine && dl == kk && lam[0] > R(0)) {
+        load_dv();
+        const R lim = c.dd_mu * lam[0];
+        R s1 = lam[1] + (rhs[1] - jdi[1] * jv(1));
+        R s2 = lam[2] + (rhs[2] - jdi[2] * jv(2));
         const R m2 = s1 * s1 + s2 * s2;
         if (m2 > lim * lim) {
           const R f = lim / g_sqrt(m2);
           s1 = s1 * f;
           s2 = s2 * f;
         }
-        const R e1 = s1 - l1, e2 = s2 - l2;
-        sc[LM1][ln] = s1;
-        sc[LM2][ln] = s2;
-        apply(i, j, d1v, ga1, gb1, e1);
-        apply(i, j, d2v, ga2, gb2, e2);
+        const R e1 = s1 - lam[1], e2 = s2 - lam[2];
+        lam[1] = s1;
+        lam[2] = s2;
+        apply(1, e1);
+        apply(2, e2);
+        store_dv();
         const R rr = e1 + e2;
         res = g_fmax(res, rr * rr);
       }
@@ -614,9 +689,13 @@ struct DcHook {
     L.dc[DC_AX][ln] = Rm[2]; L.dc[DC_AY][ln] = Rm[5]; L.dc[DC_AZ][ln] = Rm[8];
     wave_lds_sync();
     bool cand = false;
+    const R ca[3] = {Rm[2], Rm[5], Rm[8]};
     if (active)
-      for (int j = ln + 1; j < base + D; ++j) cand = cand || dc_near(L, cc, j, c.dd_reach2);
+      for (int j = ln + 1; j < base + D; ++j) cand = cand || dc_near(L, cc, ca, j, c);
     // the common case: no pair of the wave within reach
+#if GPD_DC_DIAG == 1
+    cand = false;   // diagnostic build: broadphase only, no solve
+#endif
     if (GPD_RARE(__ballot(cand) != 0ull)) drone_contact<R>(s, Rm, c, k, ln, base, D, cand);
     wave_lds_sync();   // the centre columns are rewritten by the next substep
   }

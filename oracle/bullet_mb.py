@@ -305,7 +305,7 @@ def plane_contact(pos, rot_bw, vel_w, omega_w, m, inertia, dt, radius, half_heig
 # manifold; this restatement's own deterministic contact set (parity unpinned, like the plane's):
 # one point per pair per step from the closest points of the two cylinders' margin-shrunk cores.
 FRICTION_DD = 0.5 * 0.5     # drone x drone combined friction (btCollisionObject default 0.5 each)
-PAIR_ROUNDS = 16            # alternating-projection rounds of the pair's closest points
+PAIR_ROUNDS = 16            # alternating-projection rounds of the pair's closest points (at most)
 CORE_MARGINS = (0.001, 0.003, 0.006, 0.011)   # core shrink per level (the first = the URDF margin)
 CORE_SEP = 1e-4             # core distance below which a level has no well-conditioned normal
 SIMDSQRT12 = 0.7071067811865475244008443621048490
@@ -360,8 +360,12 @@ def pair_geometry(ca, aa, cb, ab, radius, half_height):
         r, h = radius - mg, half_height - mg
         xb = zero.copy()
         for _ in range(PAIR_ROUNDS):
+            xo = xb
             pa = cyl_project(cl, aa, r, h, xb)
             xb = cyl_project(zero, ab, r, h, pa)
+            mv = xb - xo
+            if float(mv @ mv) <= 1e-24:                     # B's point moved <= 1e-12 m: converged
+                break
         dv = pa - xb
         d2 = float(dv @ dv)
         if d2 > CORE_SEP * CORE_SEP:
