@@ -252,6 +252,10 @@ const void* step_fn_act(bool multi, int flags, bool stream) {
       case F_DW: return (const void*)step_kernel<R, ACT, true, F_DW>;
       case kPfPyb: return (const void*)step_kernel<R, ACT, true, kPfPyb>;   // MultiHoverAviary's default physics
       case kPfPybAll: return (const void*)step_kernel<R, ACT, true, kPfPybAll>;
+      // the same without the drone <-> drone contact (aero "no_drone_contact"): the kernels
+      // compiled without it, as fast as before it existed
+      case kPfPyb | F_NO_DC: return (const void*)step_kernel<R, ACT, true, kPfPyb | F_NO_DC>;
+      case kPfPybAll | F_NO_DC: return (const void*)step_kernel<R, ACT, true, kPfPybAll | F_NO_DC>;
       default: return (const void*)step_kernel<R, ACT, true, kPfRuntime>;
     }
   }

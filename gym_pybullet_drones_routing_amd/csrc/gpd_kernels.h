@@ -381,7 +381,8 @@ __device__ __forceinline__ void plane_space(const R n[3], R p[3], R q[3]) {
 }
 
 #ifndef GPD_DC_DIAG
-#define GPD_DC_DIAG 0   // diagnostic builds only (scripts/ab_libs.sh): 1 = no pair solve, 2 = one iteration
+#define GPD_DC_DIAG 0   // diagnostic builds only (scripts/ab_libs.sh): 1 = no pair solve, 2 = one iteration,
+                        // 3 = no drone contact
 #endif
 enum { DC_CX, DC_CY, DC_CZ, DC_AX, DC_AY, DC_AZ, DC_PX, DC_PY, DC_PZ, DC_VX, DC_VY, DC_VZ, DC_WX, DC_WY, DC_WZ,
        DC_I00, DC_I01, DC_I02, DC_I11, DC_I12, DC_I22, DC_DLX, DC_DLY, DC_DLZ, DC_DAX, DC_DAY, DC_DAZ, DC_RES, DC_N };
@@ -426,39 +427,45 @@ __device__ __forceinline__ bool dc_near(const DcLds<R>& L, const R cc[3], const 
 }
 // the setup and solve: a call, so that its registers stay out of the substep loop that almost
 // never enters it
+#ifndef GPD_DC_INLINE
+#define GPD_DC_INLINE 0   // A/B builds: 1 = the solve inlined at each substep call site
+#endif
+#if GPD_DC_INLINE
+#define GPD_DC_ATTR __forceinline__
+#else
+#define GPD_DC_ATTR __noinline__
+#endif
 template <typename R>
-__device__ __noinline__ void drone_contact(Drone<R>& s, const R* Rm, const Consts<R>& c, const DynK<R>& k, int ln,
-                                           int base, int D, bool cand) {
+__device__ GPD_DC_ATTR void drone_contact(const Consts<R>* cp, R inv_m, R dt, int ln, int base, int D, bool cand) {
   enum { CX = DC_CX, CY, CZ, AX, AY, AZ, PX, PY, PZ, VX, VY, VZ, WX, WY, WZ, I00, I01, I02, I11, I12, I22,
          DLX, DLY, DLZ, DAX, DAY, DAZ, RES };
   enum { RAX, RAY, RAZ, RBX, RBY, RBZ, NX, NY, NZ, T1X, T1Y, T1Z, T2X, T2Y, T2Z, RH0, RH1, RH2, JI0, JI1, JI2, JDN,
          LM0, LM1, LM2, NSC };
   static_assert(NSC == 25 && RES == DC_RES, "DcLds layout");
+#ifdef GPD_CONTACT_STATS
+  const unsigned long long t0 = __builtin_readcyclecounter();
+  unsigned long long t1 = t0, t2 = t0;
+  int n_near = 0;
+#endif
   DcLds<R>& L = dc_lds<R>();
   auto& dc = L.dc;
   auto& sc = L.sc;
   auto& sij = L.sij;
   auto& scnt = L.scnt;
   auto& stouch = L.stouch;
-  const R r = c.cyl_r, hh = c.cyl_hh, zo = c.cyl_zoff;
-  const R ca[3] = {Rm[2], Rm[5], Rm[8]};
-  const R cc[3] = {s.px + ca[0] * zo, s.py + ca[1] * zo, s.pz + ca[2] * zo};
+  // everything comes through LDS (the hook wrote this lane's columns): the call takes no
+  // reference to the caller's registers, so the substep loop that almost never calls keeps them
+  const Consts<R>& c = *cp;
+  const R r = c.cyl_r, hh = c.cyl_hh;
+  const R ca[3] = {dc[AX][ln], dc[AY][ln], dc[AZ][ln]};
+  const R cc[3] = {dc[CX][ln], dc[CY][ln], dc[CZ][ln]};
+  const R spx = dc[PX][ln], spy = dc[PY][ln], spz = dc[PZ][ln];
+  const R svx = dc[VX][ln], svy = dc[VY][ln], svz = dc[VZ][ln];
+  const R swx = dc[WX][ln], swy = dc[WY][ln], swz = dc[WZ][ln];
   const int end = base + D;
   auto near = [&](int j) { return dc_near(L, cc, ca, j, c); };
 
   // ---- setup: drone columns
-  const R q00 = k.ijx * Rm[0], q01 = k.ijy * Rm[1], q02 = k.ijz * Rm[2];
-  const R q10 = k.ijx * Rm[3], q11 = k.ijy * Rm[4], q12 = k.ijz * Rm[5];
-  const R q20 = k.ijx * Rm[6], q21 = k.ijy * Rm[7], q22 = k.ijz * Rm[8];
-  dc[I00][ln] = pc_dot(q00, q01, q02, Rm[0], Rm[1], Rm[2]);
-  dc[I01][ln] = pc_dot(q00, q01, q02, Rm[3], Rm[4], Rm[5]);
-  dc[I02][ln] = pc_dot(q00, q01, q02, Rm[6], Rm[7], Rm[8]);
-  dc[I11][ln] = pc_dot(q10, q11, q12, Rm[3], Rm[4], Rm[5]);
-  dc[I12][ln] = pc_dot(q10, q11, q12, Rm[6], Rm[7], Rm[8]);
-  dc[I22][ln] = pc_dot(q20, q21, q22, Rm[6], Rm[7], Rm[8]);
-  dc[PX][ln] = s.px; dc[PY][ln] = s.py; dc[PZ][ln] = s.pz;
-  dc[VX][ln] = s.vx; dc[VY][ln] = s.vy; dc[VZ][ln] = s.vz;
-  dc[WX][ln] = s.wx; dc[WY][ln] = s.wy; dc[WZ][ln] = s.wz;
   dc[DLX][ln] = R(0); dc[DLY][ln] = R(0); dc[DLZ][ln] = R(0);
   dc[DAX][ln] = R(0); dc[DAY][ln] = R(0); dc[DAZ][ln] = R(0);
   sij[0][ln] = -1;
@@ -477,6 +484,9 @@ __device__ __noinline__ void drone_contact(Drone<R>& s, const R* Rm, const Const
   if (cand) {
     for (int j = ln + 1; j < end; ++j) {
       if (!near(j)) continue;
+#ifdef GPD_CONTACT_STATS
+      ++n_near;
+#endif
       R n[3], pb[3], dist;
       if (contact(j, n, pb, dist)) {
         if (cnt < kCache) {
@@ -491,6 +501,9 @@ __device__ __noinline__ void drone_contact(Drone<R>& s, const R* Rm, const Const
   }
   scnt[ln] = cnt;
   wave_lds_sync();
+#ifdef GPD_CONTACT_STATS
+  t1 = __builtin_readcyclecounter();
+#endif
   int slot = 0;
   for (int x = base; x < ln; ++x) slot += scnt[x];
   // pass 2: the rows of this lane's contacts, into the env's slot columns
@@ -511,14 +524,14 @@ __device__ __noinline__ void drone_contact(Drone<R>& s, const R* Rm, const Const
       const int col = base + slot;
       ++slot;
       const R pa[3] = {pb[0] + n[0] * dist, pb[1] + n[1] * dist, pb[2] + n[2] * dist};
-      const R ra[3] = {pa[0] - s.px, pa[1] - s.py, pa[2] - s.pz};
+      const R ra[3] = {pa[0] - spx, pa[1] - spy, pa[2] - spz};
       const R rb[3] = {pb[0] - dc[PX][j], pb[1] - dc[PY][j], pb[2] - dc[PZ][j]};
       R t1[3], t2[3];
       plane_space(n, t1, t2);
       const R* dirs[3] = {n, t1, t2};
       const R jb[6] = {dc[I00][j], dc[I01][j], dc[I02][j], dc[I11][j], dc[I12][j], dc[I22][j]};
       const R ja[6] = {dc[I00][ln], dc[I01][ln], dc[I02][ln], dc[I11][ln], dc[I12][ln], dc[I22][ln]};
-      const R dvx = s.vx - dc[VX][j], dvy = s.vy - dc[VY][j], dvz = s.vz - dc[VZ][j];
+      const R dvx = svx - dc[VX][j], dvy = svy - dc[VY][j], dvz = svz - dc[VZ][j];
       for (int q = 0; q < 3; ++q) {
         const R* d = dirs[q];
         const R aax = ra[1] * d[2] - ra[2] * d[1], aay = ra[2] * d[0] - ra[0] * d[2], aaz = ra[0] * d[1] - ra[1] * d[0];
@@ -527,13 +540,13 @@ __device__ __noinline__ void drone_contact(Drone<R>& s, const R* Rm, const Const
                 gaz = pc_dot(ja[2], ja[4], ja[5], aax, aay, aaz);
         const R gbx = pc_dot(jb[0], jb[1], jb[2], abx, aby, abz), gby = pc_dot(jb[1], jb[3], jb[4], abx, aby, abz),
                 gbz = pc_dot(jb[2], jb[4], jb[5], abx, aby, abz);
-        const R jd = (k.inv_m + k.inv_m + pc_dot(aax, aay, aaz, gax, gay, gaz)) + pc_dot(abx, aby, abz, gbx, gby, gbz);
-        const R rel = (pc_dot(d[0], d[1], d[2], dvx, dvy, dvz) + pc_dot(aax, aay, aaz, s.wx, s.wy, s.wz)) -
+        const R jd = (inv_m + inv_m + pc_dot(aax, aay, aaz, gax, gay, gaz)) + pc_dot(abx, aby, abz, gbx, gby, gbz);
+        const R rel = (pc_dot(d[0], d[1], d[2], dvx, dvy, dvz) + pc_dot(aax, aay, aaz, swx, swy, swz)) -
                       pc_dot(abx, aby, abz, dc[WX][j], dc[WY][j], dc[WZ][j]);
         R rhs;
         if (q == 0) {
           const R pen = dist + c.slop;
-          rhs = pen > R(0) ? (-rel - pen / k.dt) / jd : (-pen * c.erp / k.dt - rel) / jd;
+          rhs = pen > R(0) ? (-rel - pen / dt) / jd : (-pen * c.erp / dt - rel) / jd;
           sc[JDN][col] = jd;
         } else {
           rhs = -rel / jd;
@@ -555,6 +568,10 @@ __device__ __noinline__ void drone_contact(Drone<R>& s, const R* Rm, const Const
   }
   wave_lds_sync();
 
+#ifdef GPD_CONTACT_STATS
+  t2 = __builtin_readcyclecounter();
+  int it_used = 0;
+#endif
   // ---- projected Gauss-Seidel per env.  The owner lane of a slot keeps its rows in registers
   // (directions, a = r x d and g = I^-1 a of both drones, rhs, 1/jacDiag, impulses); only the two
   // drones' velocity deltas go through LDS.  Rounds run over the slots some env of the wave uses.
@@ -608,7 +625,7 @@ __device__ __noinline__ void drone_contact(Drone<R>& s, const R* Rm, const Const
            pc_dot(rb_[q][0], rb_[q][1], rb_[q][2], vj[3], vj[4], vj[5]);
   };
   auto apply = [&](int q, R delta) {
-    const R dm = k.inv_m * delta;
+    const R dm = inv_m * delta;
     const R* d = rd[q];
     vi[0] = vi[0] + d[0] * dm; vi[1] = vi[1] + d[1] * dm; vi[2] = vi[2] + d[2] * dm;
     vi[3] = vi[3] + rga[q][0] * delta; vi[4] = vi[4] + rga[q][1] * delta; vi[5] = vi[5] + rga[q][2] * delta;
@@ -622,6 +639,9 @@ __device__ __noinline__ void drone_contact(Drone<R>& s, const R* Rm, const Const
 #endif
   for (int it = 0; it < iters; ++it) {
     if (__ballot(!envdone) == 0ull) break;
+#ifdef GPD_CONTACT_STATS
+    it_used = it + 1;
+#endif
     R res = R(0);
     const bool mine = own && !envdone;
     for (int kk = 0; kk < rounds; ++kk) {            // normal rows, slot order
@@ -669,11 +689,26 @@ __device__ __noinline__ void drone_contact(Drone<R>& s, const R* Rm, const Const
     envdone = envdone || er <= c.resid;
     wave_lds_sync();
   }
-  if (stouch[ln]) {
-    s.vx = s.vx + dc[DLX][ln]; s.vy = s.vy + dc[DLY][ln]; s.vz = s.vz + dc[DLZ][ln];
-    s.wx = s.wx + dc[DAX][ln]; s.wy = s.wy + dc[DAY][ln]; s.wz = s.wz + dc[DAZ][ln];
+#ifdef GPD_CONTACT_STATS
+  {
+    const unsigned long long t3 = __builtin_readcyclecounter();
+    unsigned long long nn = 0, ns = 0;
+    for (int x = 0; x < kWave; ++x) ns += (sij[0][x] >= 0);
+    int tot = n_near;
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+    nn = (unsigned long long)tot;
+    if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) {
+      atomicAdd(&g_pc_hist[116], 1ull);
+      atomicAdd(&g_pc_hist[117], t2 - t0);
+      atomicAdd(&g_pc_hist[118], t3 - t2);
+      atomicAdd(&g_pc_hist[119], (unsigned long long)it_used);
+      atomicAdd(&g_pc_hist[123], t1 - t0);
+      atomicAdd(&g_pc_hist[126], ns);
+      atomicAdd(&g_pc_hist[127], nn);
+    }
   }
-  wave_lds_sync();   // the columns are rewritten by the next substep's call
+#endif
+  wave_lds_sync();   // the caller reads the velocity deltas
 }
 // the hook bullet_substep calls (multi-drone envs of one-wave blocks)
 struct DcHook {
@@ -681,6 +716,12 @@ struct DcHook {
   bool active;
   template <typename R>
   __device__ __forceinline__ void operator()(Drone<R>& s, const R* Rm, const Consts<R>& c, const DynK<R>& k) const {
+#if GPD_DC_DIAG == 3
+    return;   // diagnostic build: no drone contact at all (the hook compiled in, its body not)
+#endif
+#ifdef GPD_CONTACT_STATS
+    const unsigned long long tb = __builtin_readcyclecounter();
+#endif
     DcLds<R>& L = dc_lds<R>();
     const int ln = tid & (kWave - 1);
     const R zo = c.cyl_zoff;
@@ -688,6 +729,9 @@ struct DcHook {
     L.dc[DC_CX][ln] = cc[0]; L.dc[DC_CY][ln] = cc[1]; L.dc[DC_CZ][ln] = cc[2];
     L.dc[DC_AX][ln] = Rm[2]; L.dc[DC_AY][ln] = Rm[5]; L.dc[DC_AZ][ln] = Rm[8];
     wave_lds_sync();
+#if GPD_DC_DIAG == 5
+    return;   // diagnostic build: the centre / axis exchange only
+#endif
     bool cand = false;
     const R ca[3] = {Rm[2], Rm[5], Rm[8]};
     if (active)
@@ -696,7 +740,40 @@ struct DcHook {
 #if GPD_DC_DIAG == 1
     cand = false;   // diagnostic build: broadphase only, no solve
 #endif
-    if (GPD_RARE(__ballot(cand) != 0ull)) drone_contact<R>(s, Rm, c, k, ln, base, D, cand);
+#ifdef GPD_CONTACT_STATS
+    {
+      const unsigned long long te = __builtin_readcyclecounter();
+      if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) {
+        atomicAdd(&g_pc_hist[124], 1ull);
+        atomicAdd(&g_pc_hist[125], te - tb);
+      }
+    }
+#endif
+#if GPD_DC_DIAG == 4
+    if (__ballot(cand) != 0ull) s.vx = s.vx + R(0);   // diagnostic build: broadphase, no solve compiled
+#else
+    if (GPD_RARE(__ballot(cand) != 0ull)) {
+      // this lane's columns for the solve: pose, velocities, world inverse inertia R diag(1/I) R^T
+      const R q00 = k.ijx * Rm[0], q01 = k.ijy * Rm[1], q02 = k.ijz * Rm[2];
+      const R q10 = k.ijx * Rm[3], q11 = k.ijy * Rm[4], q12 = k.ijz * Rm[5];
+      const R q20 = k.ijx * Rm[6], q21 = k.ijy * Rm[7], q22 = k.ijz * Rm[8];
+      L.dc[DC_I00][ln] = pc_dot(q00, q01, q02, Rm[0], Rm[1], Rm[2]);
+      L.dc[DC_I01][ln] = pc_dot(q00, q01, q02, Rm[3], Rm[4], Rm[5]);
+      L.dc[DC_I02][ln] = pc_dot(q00, q01, q02, Rm[6], Rm[7], Rm[8]);
+      L.dc[DC_I11][ln] = pc_dot(q10, q11, q12, Rm[3], Rm[4], Rm[5]);
+      L.dc[DC_I12][ln] = pc_dot(q10, q11, q12, Rm[6], Rm[7], Rm[8]);
+      L.dc[DC_I22][ln] = pc_dot(q20, q21, q22, Rm[6], Rm[7], Rm[8]);
+      L.dc[DC_PX][ln] = s.px; L.dc[DC_PY][ln] = s.py; L.dc[DC_PZ][ln] = s.pz;
+      L.dc[DC_VX][ln] = s.vx; L.dc[DC_VY][ln] = s.vy; L.dc[DC_VZ][ln] = s.vz;
+      L.dc[DC_WX][ln] = s.wx; L.dc[DC_WY][ln] = s.wy; L.dc[DC_WZ][ln] = s.wz;
+      wave_lds_sync();
+      drone_contact<R>(&c, k.inv_m, k.dt, ln, base, D, cand);
+      if (L.stouch[ln]) {
+        s.vx = s.vx + L.dc[DC_DLX][ln]; s.vy = s.vy + L.dc[DC_DLY][ln]; s.vz = s.vz + L.dc[DC_DLZ][ln];
+        s.wx = s.wx + L.dc[DC_DAX][ln]; s.wy = s.wy + L.dc[DC_DAY][ln]; s.wz = s.wz + L.dc[DC_DAZ][ln];
+      }
+    }
+#endif
     wave_lds_sync();   // the centre columns are rewritten by the next substep
   }
 };

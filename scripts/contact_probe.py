@@ -23,16 +23,20 @@ from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim  # noqa: E402
 STAG = [[0.15 * math.cos(2 * math.pi * i / 8), 0.15 * math.sin(2 * math.pi * i / 8), 0.5 + 0.1 * i] for i in range(8)]
 
 
+# GPD_PROBE_NODC=1: the multi-drone cases without the drone <-> drone contact
+NODC = ("no_drone_contact",) if os.environ.get("GPD_PROBE_NODC") == "1" else ()
+
+
 def run(case, E=4096, warm=60, steps=200):
     aero = ("no_plane",) if case == "noplane" else ()
     if case in ("multi", "multifly"):    # bench.py's PYB_GND_DRAG_DW row: 512 MultiHover envs x 8 drones, staggered
         E, D = 512, 8
         sim = BatchedAviarySim(n_envs=E, drones_per_env=D, task="multihover", act=ActionType.RPM,
-                               physics=Physics.PYB_GND_DRAG_DW, initial_xyzs=STAG, device="cuda:0")
+                               physics=Physics.PYB_GND_DRAG_DW, initial_xyzs=STAG, device="cuda:0", aero=NODC)
     elif case == "multi2pyb":   # MultiHoverAviary's default: 2 drones, Physics.PYB (examples/learn.py --multiagent)
         E, D = 2048, 2
         sim = BatchedAviarySim(n_envs=E, drones_per_env=D, task="multihover", act=ActionType.RPM,
-                               physics=Physics.PYB, device="cuda:0")
+                               physics=Physics.PYB, device="cuda:0", aero=NODC)
     else:
         D = 1
         sim = BatchedAviarySim(n_envs=E, act=ActionType.RPM, physics=Physics.PYB, aero=aero, device="cuda:0")
@@ -82,6 +86,13 @@ def run(case, E=4096, warm=60, steps=200):
             if h[122]:
                 print(f"   shader cycles: setup {h[120] / it.sum():.0f} per solve, loop {h[121] / h[122]:.0f} per "
                       f"iteration ({h[121] / it.sum():.0f} per solve)", flush=True)
+        if h[124]:
+            print(f"   drone contact: broadphase {h[124]} wave-substeps, {h[125] / h[124]:.0f} cycles each; "
+                  f"solves {h[116]} ({h[116] / h[124]:.3f} of wave-substeps)", flush=True)
+        if h[116]:
+            print(f"   drone contact per solve: setup {h[117] / h[116]:.0f} cycles (pass 1 {h[123] / h[116]:.0f}), "
+                  f"iterations {h[119] / h[116]:.2f} x {h[118] / max(h[119], 1):.0f} cycles, "
+                  f"near pairs {h[127] / h[116]:.2f}, contacts {h[126] / h[116]:.2f}", flush=True)
     sim.close()
 
 
