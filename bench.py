@@ -472,6 +472,75 @@ def other_configs(device, precision, act):
     return out
 
 
+def _policy_mlp(n_in, n_out):
+    """SB3 MlpPolicy's network (examples/learn.py mlp: [64, 64] tanh), random-initialised."""
+    import torch.nn as nn
+    return nn.Sequential(nn.Linear(n_in, 64), nn.Tanh(), nn.Linear(64, 64), nn.Tanh(), nn.Linear(64, n_out))
+
+
+def rollout_leg(device, precision, act, E, K=64, reps=8, store_policy=0):
+    """What an RL caller pays per env.step (the caller: examples/learn.py's PPO rollout, the
+    reference's learn.py:52-94 through SB3): ONE hipGraph of K x (actor and critic MLP forward on
+    the observation, Normal sample, clamp, gpd_step, the rollout-buffer copies) at E envs, against
+    the same graph without gpd_step.  Per step: the whole sequence, the policy part, and their
+    difference = the step's cost inside a rollout (its kernel plus the boundary, with the policy's
+    kernels between consecutive steps instead of another step), by HIP events over graph replays.
+    ``store_policy``: gpd_config::store_policy (0 = the library's choice)."""
+    from gym_pybullet_drones_routing_amd.enums import ActionType
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+    tuning = {"store_policy": store_policy} if store_policy else None
+    sim = BatchedAviarySim(n_envs=E, task="hover", act=ActionType(act), precision=precision, autoreset=True,
+                           device=device, tuning=tuning)
+    W, A = sim.obs_width, sim.act_width
+    torch.manual_seed(0)
+    pi, vf = _policy_mlp(W, A).to(device), _policy_mlp(W, 1).to(device)
+    log_std = torch.zeros(A, device=device)
+    obs = sim.obs.view(E, W)                      # sim-owned, rewritten in place by every step
+    act_buf = torch.zeros((E, 1, A), device=device)
+    buf_obs = torch.zeros((K, E, W), device=device)
+    buf_act = torch.zeros((K, E, A), device=device)
+    buf_val = torch.zeros((K, E), device=device)
+    buf_rew = torch.zeros((K, E), device=device)
+    buf_done = torch.zeros((K, E), device=device)
+
+    def seq(with_step):
+        for t in range(K):
+            mu = pi(obs)
+            v = vf(obs).squeeze(-1)
+            a = mu + log_std.exp() * torch.randn_like(mu)
+            act_buf.copy_(a.clamp(-1.0, 1.0).view(E, 1, A))     # SB3 clips to the Box
+            buf_obs[t].copy_(obs)
+            buf_act[t].copy_(a)
+            buf_val[t].copy_(v)
+            if with_step:
+                sim.step(act_buf)
+            buf_rew[t].copy_(sim.reward)
+            buf_done[t].copy_(torch.logical_or(sim.terminated, sim.truncated))
+    out = {}
+    with torch.no_grad():
+        side = torch.cuda.Stream(device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):             # warm the MLP's library kernels before capture
+            seq(False)
+        torch.cuda.current_stream(device).wait_stream(side)
+        for name, with_step in (("policy_only", False), ("rollout", True)):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                seq(with_step)
+            g.replay()
+            g.replay()
+            us = _event_region_us(device, g.replay, K, min_launches=K * reps)
+            out[name + "_us_per_step"] = us
+            del g
+    out["step_in_rollout_us"] = out["rollout_us_per_step"] - out["policy_only_us_per_step"]
+    out.update({"n_envs": E, "steps_per_graph": K, "store_policy": store_policy or "library default",
+                "what": "one hipGraph of K x (actor + critic 64-64 tanh MLP forward, Normal sample, clamp, gpd_step, "
+                        "rollout-buffer copies) vs the same without gpd_step; step_in_rollout = the difference"})
+    sim.close()
+    torch.cuda.synchronize(device)
+    return out
+
+
 def hbm_copy_gbps(device, n=1 << 28, reps=5):
     """torch copy_ of n float32 (1 GiB, far past the 256 MB Infinity Cache), bytes read + written
     per second: reported beside the HIP ceiling below (torch's copy keeps one load per lane in
@@ -571,6 +640,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-latency-model", action="store_true",
                     help="skip the latency-model leg (its 1- and 16-substep launches share the bench kernel's "
                          "name and grid, so a rocprofv3 trace of the bench kernel leaves it out)")
+    ap.add_argument("--no-rollout", action="store_true",
+                    help="skip the RL-rollout leg (its step launches share the bench kernel's name and grid)")
     ap.add_argument("--mode", default="graph", choices=["native", "graph", "eager"],
                     help="timed region: hipGraph replays (default), a native launch loop (gpd_step_seq), or "
                          "one Python step() call per env.step")
@@ -770,6 +841,8 @@ def run(args):
 
     if rank == 0 and world == 1 and not args.no_latency_model:
         result["roofline"]["latency_model"] = latency_model(device, args.precision, args.act, E, kern_us, nsub)
+    if rank == 0 and world == 1 and not args.no_rollout:
+        result["rollout"] = rollout_leg(device, args.precision, args.act, E)
     if rank == 0 and world == 1 and not args.no_sweep:
         sweep = []
         for e_large in (65536, 1 << 20, 1 << 22):

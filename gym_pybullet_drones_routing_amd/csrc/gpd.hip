@@ -124,6 +124,12 @@ struct gpd_sim {
   bool generic_pf = false;        // the run-time-flag step kernel even where a flag set is compiled in
                                   // (its static LDS + the observation tile would not fit: upload_tables)
   DwPairs dw_pairs{0, 0};         // SimView::dw_pairs
+  // drone <-> drone contact (PYB*, 1 < D <= 64; SimView::dc*): pairs per env, p / P magic, the
+  // [P] pair table, the row store of pairs past a block's first 64 (blocks x stride reals)
+  int dcP = 0, dc_pmagic = 0;
+  int* d_dc_tab = nullptr;
+  void* d_dc_rows = nullptr;
+  long long dc_row_stride = 0;
   double bound_xy;
   std::vector<double> init_tmpl;  // [D][10]
   std::vector<double> target;     // [D][3]
@@ -190,6 +196,13 @@ Consts<R> make_consts(const gpd_sim* s) {
     const double reach = 2.0 * bs + (double)c.brk;
     c.dd_reach2 = (R)(reach * reach);
     c.dd_mu = (R)(0.5 * 0.5);   // drone x drone default friction
+    // FISTA momentum of the narrowphase's rounds (oracle/bullet_mb.py fista_momentum)
+    double t = 1.0;
+    for (int k = 0; k < kPairCold; ++k) {
+      const double tn = (1.0 + std::sqrt(1.0 + 4.0 * t * t)) / 2.0;
+      c.dc_beta[k] = (R)((t - 1.0) / tn);
+      t = tn;
+    }
   }
   c.iters = 50;              // m_numIterations (pybullet numSolverIterations)
 #ifdef GPD_DIAG_RESID
@@ -230,6 +243,11 @@ SimView<R> make_view(const gpd_sim* s) {
   v.nc_magic = s->nc_magic;
   v.dw_pairs = s->dw_pairs;
   v.bound_xy = (R)s->bound_xy;
+  v.dcP = s->dcP;
+  v.dc_pmagic = s->dc_pmagic;
+  v.dc_tab = s->d_dc_tab;
+  v.dc_rows = s->d_dc_rows;
+  v.dc_row_stride = s->dc_row_stride;
   return v;
 }
 
@@ -465,6 +483,8 @@ void free_sim(gpd_sim* s) {
   if (s->d_init) (void)hipFree(s->d_init);
   if (s->d_target) (void)hipFree(s->d_target);
   if (s->d_consts) (void)hipFree(s->d_consts);
+  if (s->d_dc_tab) (void)hipFree(s->d_dc_tab);
+  if (s->d_dc_rows) (void)hipFree(s->d_dc_rows);
   delete s;
 }
 
@@ -532,6 +552,10 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   if (C.task == GPD_TASK_HOVER && C.drones_per_env != 1)
     return fail(GPD_EINVAL, "gpd_create: HoverAviary is single-drone (drones_per_env must be 1)");
   if (C.precision != GPD_F32 && C.precision != GPD_F64) return fail(GPD_EINVAL, "gpd_create: bad precision");
+  if ((C.physics_flags & GPD_F_BULLET) && C.drones_per_env > kWave && !(C.physics_flags & GPD_F_NO_DRONE_CONTACT))
+    return fail(GPD_EUNSUPPORTED,
+                "gpd_create: drone <-> drone contact is implemented for envs of up to 64 drones; pass "
+                "GPD_F_NO_DRONE_CONTACT (aero 'no_drone_contact') for larger PYB* envs");
   if (C.physics_flags & ~(GPD_F_GND | GPD_F_DRAG | GPD_F_DW | GPD_F_GEOM_WRENCH | GPD_F_BULLET | GPD_F_NO_PLANE |
                           GPD_F_NO_DRONE_CONTACT))
     return fail(GPD_EINVAL, "gpd_create: unknown physics flag");
@@ -591,10 +615,8 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     // write-through (sc1) stores for the obs rows (bit 0) and the state (bit 1), default both:
     // measured on one MI355X, 4096 envs 8.60 -> 8.37 us/step and 65536 envs 15.3 -> 13.7 us,
     // large N unchanged (gpd_config::store_policy overrides).  State only while its byte
-    // offsets fit the 32-bit buffer offset.
+    // offsets fit the 32-bit buffer offset (re-applied after the wave-count policies below).
     s->wt = C.store_policy > 0 ? ((C.store_policy - 1) & 3) : 3;
-    const size_t state_bytes = (size_t)kStateComps * s->npad * (C.precision == GPD_F64 ? 8 : 4);
-    if (state_bytes >= 0x7fffffffULL) s->wt &= ~2;
     // bit 2: the step kernels leave last_clipped_action in the ring (store_drone_step) where
     // the step never reads it back: RPM action types (the ring holds the very actions it maps),
     // no drag (the only reader, on the first substep)
@@ -644,6 +666,10 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     // write-through state, store_policy 3; step time 4.93 vs 4.97 us, within the run-to-run spread:
     // profiles/r3/pmc4096, profiles/r3/policy_4096.log)
     if (waves == 3 && C.store_policy <= 0) s->wt = (s->wt & ~1) | 2;
+    // write-through state stores address the whole state through one buffer resource with 32-bit
+    // offsets (store_drone_wt): whatever the policy above chose, never past 2 GiB of state
+    const size_t state_bytes = (size_t)kStateComps * s->npad * (C.precision == GPD_F64 ? 8 : 4);
+    if (state_bytes >= 0x7fffffffULL) s->wt &= ~2;
   }
   if (s->tile_bytes > kLdsBytes) {
     delete s;
@@ -725,6 +751,40 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     free_sim(s);
     (void)hipGetLastError();
     return fail(GPD_ENOMEM, "gpd_create: hipMalloc failed");
+  }
+  if ((C.physics_flags & GPD_F_BULLET) && s->D > 1 && !(C.physics_flags & GPD_F_NO_DRONE_CONTACT)) {
+    // drone <-> drone contact (gpd_kernels.h DcHook / dc_solve): the pair table of an env and the
+    // row store for a block's pairs past its first 64
+    const int D = s->D, P = D * (D - 1) / 2;
+    const int npairs = (s->tpb / D) * P;
+    s->dcP = P;
+    s->dc_pmagic = ((1 << 20) + P - 1) / P;
+    for (int p = 0; p < npairs; ++p)
+      if (((p * s->dc_pmagic) >> 20) != p / P) {
+        free_sim(s);
+        return fail(GPD_EUNSUPPORTED, "gpd_create: drone contact pair layout not supported");
+      }
+    std::vector<int> tab;
+    tab.reserve(P);
+    for (int i = 0; i < D; ++i)
+      for (int j = i + 1; j < D; ++j) tab.push_back(i | (j << 8));   // bullet_mb.drone_contacts' order
+    if (hipMalloc((void**)&s->d_dc_tab, (size_t)P * sizeof(int)) != hipSuccess ||
+        hipMemcpy(s->d_dc_tab, tab.data(), (size_t)P * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+      free_sim(s);
+      (void)hipGetLastError();
+      return fail(GPD_ENOMEM, "gpd_create: drone contact pair table");
+    }
+    if (npairs > kWave) {
+      const int row_reals = s->prec == GPD_F64 ? dc_row_reals<double>() : dc_row_reals<float>();
+      const int chunks = (npairs + kWave - 1) / kWave - 1;
+      s->dc_row_stride = (long long)chunks * kWave * row_reals;
+      const long long blocks = ((long long)s->N + s->tpb - 1) / s->tpb;
+      if (hipMalloc(&s->d_dc_rows, (size_t)(blocks * s->dc_row_stride) * rs) != hipSuccess) {
+        free_sim(s);
+        (void)hipGetLastError();
+        return fail(GPD_ENOMEM, "gpd_create: drone contact row store");
+      }
+    }
   }
   int rc = s->prec == GPD_F64 ? upload_tables<double>(s) : upload_tables<float>(s);
   if (rc != GPD_OK) { free_sim(s); return rc; }

@@ -16,7 +16,10 @@ namespace gpd {
 // ---------------------------------------------------------------- precision-overloaded math
 // A wave-uniform branch that practically never runs: laid out after the hot path, so its code
 // is not fetched into the instruction cache on the launches that skip it.
-#ifdef GPD_NOEXPECT
+#if defined(GPD_NOCOLD)
+#define GPD_RARE(x) ((x) && false)   // diagnostic build: every rare branch compiled out (bounds the
+                                     // instruction-cache gain of moving them out of line)
+#elif defined(GPD_NOEXPECT)
 #define GPD_RARE(x) (x)
 #else
 #define GPD_RARE(x) __builtin_expect((x), 0)
@@ -125,6 +128,7 @@ struct Consts {
   R brk;                       // contact breaking threshold (0.02 x the cylinder's motion disc)
   R slop, erp, mu, plane_half, resid;   // m_linearSlop, m_erp2, combined friction, plane box, residual
   R dd_reach2, dd_mu;          // drone <-> drone contact: broadphase (2 x bounding sphere + brk)^2, friction
+  R dc_beta[8];                // drone <-> drone narrowphase: FISTA momentum weights (bullet_mb.PAIR_BETA)
   int iters;                   // m_numIterations
   R init0[10];             // reset template of drone 0 (pos, stored quat, rpy): single-drone envs
   R target0[3];            // task target of drone 0 (single-drone envs: no dependent global load)
@@ -501,8 +505,14 @@ __device__ __forceinline__ void attitude_decide(R qx, R qy, R qz, R qw, Attitude
     }
   }
 }
-// float32 Euler angles for the float32 observation (the reference casts its float64 angles to
-// float32, BaseRLAviary.py:315); evaluated in float32 from the double-precision arguments.
+// float32 Euler angles for the float32 observation.  The reference computes them in float64
+// (pybullet's getEulerFromQuaternion, BaseAviary.py:518) and casts them (BaseRLAviary.py:313-315):
+// with GPD_OBS_ANGLES_F64 (the default) the f64 sim does the same - double-precision asin / atan2 on
+// the double arguments, then the cast - so the angle columns agree with the reference to the cast
+// of a state that agrees to ~1e-14; the f32 sim (and GPD_OBS_ANGLES_F64=0) evaluates them in float32.
+#ifndef GPD_OBS_ANGLES_F64
+#define GPD_OBS_ANGLES_F64 1
+#endif
 template <typename R>
 __device__ __forceinline__ void obs_euler_f32(const R q[4], const AttitudeArgs<R>& t, float& roll, float& pitch,
                                               float& yaw) {
@@ -510,14 +520,20 @@ __device__ __forceinline__ void obs_euler_f32(const R q[4], const AttitudeArgs<R
   // the regular branch for every lane, the gimbal branches (|sarg| >= 0.99999) as a
   // wave-uniform fix-up
   const R sa = t.sarg < R(-1) ? R(-1) : (t.sarg > R(1) ? R(1) : t.sarg);
-  pitch = asinf((float)sa);
-  roll = atan2f((float)t.a, (float)t.b);
-  yaw = atan2f((float)(R(2) * (x * y + w * z)), (float)(w * w + x * x - y * y - z * z));
+  if (GPD_OBS_ANGLES_F64 && sizeof(R) == 8) {
+    pitch = (float)g_asin(sa);
+    roll = (float)g_atan2(t.a, t.b);
+    yaw = (float)g_atan2(R(2) * (x * y + w * z), w * w + x * x - y * y - z * z);
+  } else {
+    pitch = asinf((float)sa);
+    roll = atan2f((float)t.a, (float)t.b);
+    yaw = atan2f((float)(R(2) * (x * y + w * z)), (float)(w * w + x * x - y * y - z * z));
+  }
   if (GPD_RARE(__ballot(t.gimbal) != 0ull)) {
     if (t.sarg <= R(-0.99999)) {
-      pitch = -1.57079632679489661923f; roll = 0.0f; yaw = 2.0f * atan2f((float)x, (float)-y);
+      pitch = -1.57079632679489661923f; roll = 0.0f; yaw = (float)(R(2) * g_atan2(x, -y));
     } else if (t.sarg >= R(0.99999)) {
-      pitch = 1.57079632679489661923f; roll = 0.0f; yaw = 2.0f * atan2f((float)-x, (float)y);
+      pitch = 1.57079632679489661923f; roll = 0.0f; yaw = (float)(R(2) * g_atan2(-x, y));
     }
   }
 }
@@ -1007,8 +1023,8 @@ __device__ __forceinline__ R contact_low(const Drone<R>& s, const R Rm[9], const
 // HK: the drone <-> drone contact of multi-drone envs (gpd_kernels.h DcHook), run on the
 // unconstrained velocities before the ground-plane solve; NoDc elsewhere.
 struct NoDc {
-  template <typename R>
-  __device__ void operator()(Drone<R>&, const R*, const Consts<R>&, const DynK<R>&) const {}
+  template <typename R, class PK>
+  __device__ void operator()(Drone<R>&, R*, const Consts<R>&, const DynK<R>&, const PK&) const {}
 };
 template <typename R, int PF, bool ANGV, int CW = 1, class HK = NoDc>
 __device__ __forceinline__ void bullet_substep(Drone<R>& s, R rpm[4], R W[4], R last[4], R dwsum,
@@ -1055,7 +1071,57 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, R rpm[4], R W[4], R 
   s.vx = clampv(s.vx + k.dt * (Fx * k.inv_m - kv * s.vx));
   s.vy = clampv(s.vy + k.dt * (Fy * k.inv_m - kv * s.vy));
   s.vz = clampv(s.vz + k.dt * (Fz * k.inv_m - kv * s.vz));
-  if (!pf_on<PF>(k.flags, F_NO_DC)) hk(s, Rm, c, k);
+  // Everything this thread keeps across a contact solve (the caller's constants, RPMs and wrench,
+  // the pose and velocities; for the drone <-> drone call also the basis) goes to per-lane LDS
+  // columns for the solve and comes back after it: the solve's ~200 VGPRs then fit beside the
+  // kernel's own state instead of spilling the row constants into AGPR round trips on the
+  // Gauss-Seidel chain, and across the drone <-> drone call nothing of the substep loop is live,
+  // so the loop's register allocation does not see it.  The reload goes through an opaque lane
+  // offset, so nothing forwards the stored values past the solve; a memory clobber keeps the
+  // stores ahead of it.
+  constexpr int kPark = 15 + 12 + 4 + 12, kParkRm = 9;
+  __shared__ R pk[kPark + kParkRm][kWaveLanes];
+  const int pl = threadIdx.x & (kWaveLanes - 1);
+  auto each = [&](auto&& f) {
+    f(k.dt); f(k.inv_m); f(k.gravity); f(k.jx); f(k.jy); f(k.jz); f(k.ijx); f(k.ijy); f(k.ijz);
+    f(k.hdt); f(k.hdt2); f(k.kf); f(k.km); f(k.L); f(k.Ls2);
+    f(s.px); f(s.py); f(s.pz); f(s.vx); f(s.vy); f(s.vz); f(s.wx); f(s.wy); f(s.wz);
+    f(s.ax); f(s.ay); f(s.az);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f(q0[j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { f(rpm[j]); f(W[j]); f(last[j]); }
+  };
+  auto park = [&]() {
+    int i = 0;
+    each([&](R& x) { pk[i++][pl] = x; });
+    asm volatile("" ::: "memory");
+  };
+  auto unpark = [&]() {
+    int o = pl;
+    asm volatile("" : "+v"(o));
+    int i = 0;
+    each([&](R& x) { x = pk[i++][o]; });
+  };
+  auto park_dc = [&]() {
+    park();
+#pragma unroll
+    for (int j = 0; j < 9; ++j) pk[kPark + j][pl] = Rm[j];
+    asm volatile("" ::: "memory");
+  };
+  auto unpark_dc = [&]() {
+    unpark();
+    int o = pl;
+    asm volatile("" : "+v"(o));
+#pragma unroll
+    for (int j = 0; j < 9; ++j) Rm[j] = pk[kPark + j][o];
+  };
+  if (!pf_on<PF>(k.flags, F_NO_DC)) {
+    // the run-time-flag kernels (a long observation tile may leave no LDS for the parked columns)
+    // call the solve without parking
+    if (PF != kPfRuntime) hk(s, Rm, c, k, ParkFns<decltype(park_dc), decltype(unpark_dc)>{park_dc, unpark_dc});
+    else hk(s, Rm, c, k, NoPark());
+  }
   // ground-plane contact (solveConstraints, before integrateTransforms); the margin keeps the
   // gate conservative against the candidates' own rounding
   if (!pf_on<PF>(k.flags, F_NO_PLANE)) {
@@ -1066,36 +1132,6 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, R rpm[4], R W[4], R 
       if (GPD_RARE(__ballot(low) != 0ull)) {
         if (PF != kPfRuntime) {
 #if GPD_CONTACT_PARK
-          // Everything this thread keeps across the solve (the caller's constants, RPMs and
-          // wrench, the pose and velocities) goes to LDS columns for the iterations and comes
-          // back after them: the solve's ~200 VGPRs then fit beside the kernel's own state
-          // instead of spilling the row constants into AGPR round trips on the Gauss-Seidel chain.
-          // The reload goes through an opaque lane offset, so nothing forwards the stored values
-          // past the solve; a memory clobber keeps the stores ahead of it.
-          constexpr int kPark = 15 + 12 + 4 + 12;
-          __shared__ R pk[kPark][kWaveLanes];
-          const int pl = threadIdx.x & (kWaveLanes - 1);
-          auto each = [&](auto&& f) {
-            f(k.dt); f(k.inv_m); f(k.gravity); f(k.jx); f(k.jy); f(k.jz); f(k.ijx); f(k.ijy); f(k.ijz);
-            f(k.hdt); f(k.hdt2); f(k.kf); f(k.km); f(k.L); f(k.Ls2);
-            f(s.px); f(s.py); f(s.pz); f(s.vx); f(s.vy); f(s.vz); f(s.wx); f(s.wy); f(s.wz);
-            f(s.ax); f(s.ay); f(s.az);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) f(q0[j]);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) { f(rpm[j]); f(W[j]); f(last[j]); }
-          };
-          auto park = [&]() {
-            int i = 0;
-            each([&](R& x) { pk[i++][pl] = x; });
-            asm volatile("" ::: "memory");
-          };
-          auto unpark = [&]() {
-            int o = pl;
-            asm volatile("" : "+v"(o));
-            int i = 0;
-            each([&](R& x) { x = pk[i++][o]; });
-          };
           plane_contact_regs<R>(s, Rm, c, k, ParkFns<decltype(park), decltype(unpark)>{park, unpark});
 #else
           plane_contact_regs<R>(s, Rm, c, k);

@@ -142,6 +142,12 @@ struct SimView {
   int nc_magic;           // floor(t / NC) == (t * nc_magic) >> 16 for 0 <= t < 64 (host-checked)
   DwPairs dw_pairs;       // downwash pair split (n = 0: one lane per drone loops over its env)
   R bound_xy;             // 1.5 (Hover) or 2.0 (MultiHover)
+  // drone <-> drone contact (PYB*, D > 1; DcPairs): pairs per env D(D-1)/2 (0 = off), p / P magic,
+  // the [P] pair table, the per-block row store for pairs past the first 64 of a block
+  int dcP, dc_pmagic;
+  const int* dc_tab;
+  void* dc_rows;
+  long long dc_row_stride;   // row-store reals per block
 };
 
 template <typename R>
@@ -266,23 +272,32 @@ __device__ __forceinline__ void wave_lds_sync() {
 // MultiHoverAviary's drones are colliding Bullet bodies (BaseAviary.py:486-491) stepped together
 // by p.stepSimulation() (:369-370).  Restatement (oracle/bullet_mb.py drone_contact; parity
 // unpinned like the plane's: Bullet's GJK / EPA and its persistent manifold are not restated):
-//   * broadphase: pairs (i, j > i) of an env whose cylinder centres are within
-//     2 x bounding-sphere radius + the breaking threshold;
+//   * broadphase (pair_near): pairs (i, j > i) of an env whose bounding spheres come within the
+//     breaking threshold and that no separating axis (the two cylinder axes, the centre line)
+//     keeps farther apart than it;
 //   * one contact per pair: Bullet's margin scheme, the closest points of the margin-shrunk core
-//     cylinders (PAIR_ROUNDS rounds of alternating projection from B's centre) give the normal
-//     (B -> A) and distance core - 2 x margin, with thicker margins for deeper overlaps (up to
-//     ~2 cm), beyond that the least overlap over the centre line and the two axes;
-//   * contacts below the breaking threshold, in (i, j) order, fill the env's D solver slots;
+//     cylinders by kPairCold rounds of FISTA-accelerated alternating projection from B's centre
+//     (a fixed count: the result is a continuous function of the poses) give the normal (B -> A)
+//     and distance core - 2 x margin, with thicker margins for deeper overlaps (up to ~2 cm),
+//     beyond that the least overlap over the centre line and the two axes;
+//   * EVERY pair whose distance is below the breaking threshold is a contact (up to D(D-1)/2 per
+//     env), solved in (i, j) order;
 //   * rows (normal, btPlaneSpace1 friction pair) between two bodies: effective mass
 //     2/m + a_A.I_A^-1 a_A + a_B.I_B^-1 a_B; the plane's rhs rules and cone (mu 0.25); projected
-//     Gauss-Seidel over the env's normal rows, then friction pairs, in slot order; the env stops
+//     Gauss-Seidel over the env's normal rows, then friction pairs, in contact order; the env stops
 //     at its largest squared residual <= resid or after `iters` iterations.
-// Layout: one LDS column per lane of the block's single wave: the drone columns (centre, axis,
-// pose, velocities, world inverse inertia, velocity deltas) and the env's slots in the columns
-// of its own lanes (slot s of the env whose first lane is b at column b + s), so the lane that
-// owns a slot column solves that row; slots of different envs touch different drones and run
-// together, the slots of one env one after another.  Runs only when the wave's broadphase finds a
-// pair (a ballot), after the unconstrained velocity update and before the ground-plane solve.
+// GPU layout.  The pairs of a block's whole envs are numbered p = env * P + q (P = D(D-1)/2, q the
+// (i, j) index of bullet_mb.drone_contacts' order) and lane ln handles pairs ln, ln + 64, ... (chunk
+// ch = p / 64).  The hot part (DcHook, every substep): the drones' centre / axis columns into LDS,
+// the broadphase of every pair (the sphere test; the separating-axis tests only for pairs in
+// reach), one ballot per chunk.  A wave with a pair in reach calls dc_solve (rare): the narrowphase
+// of its near pairs in parallel over lanes, each contact's rows set up by the lane of its pair -
+// chunk 0 in that lane's registers, later chunks in a per-block global row store - then the
+// Gauss-Seidel sweeps: round r solves the r-th contact of every env at once (contacts of different
+// envs touch different drones), the drones' velocity deltas in LDS.  When no env of the wave has
+// more than one contact (every two-drone env, most waves of 8-drone envs) the owner lane keeps its
+// two drones' deltas in registers for the whole solve and the sweep needs no LDS at all.
+constexpr int kPairCold = 8;   // oracle/bullet_mb.py PAIR_COLD
 template <typename R>
 __device__ __forceinline__ void cyl_project(R cx, R cy, R cz, R ax, R ay, R az, R r, R hh, R& x, R& y, R& z) {
   const R dx = x - cx, dy = y - cy, dz = z - cz;
@@ -299,47 +314,44 @@ __device__ __forceinline__ void cyl_project(R cx, R cy, R cz, R ax, R ay, R az, 
   z = (cz + tc * az) + rz;
 }
 template <typename R>
-__device__ __forceinline__ R cyl_extent(R ux, R uy, R uz, R ax, R ay, R az, R r, R hh) {
-  const R ua = pc_dot(ux, uy, uz, ax, ay, az);
+__device__ __forceinline__ R cyl_extent_cos(R ua, R r, R hh) {
   const R s2 = R(1) - ua * ua;
   return hh * g_abs(ua) + r * g_sqrt(s2 > R(0) ? s2 : R(0));
 }
-constexpr int kPairRounds = 16;
-// contact of cylinders A (centre ca, axis aa) and B: normal (B -> A), point on B, distance.
-// Bullet's margin scheme over thickening core levels (oracle/bullet_mb.py pair_geometry): the
-// core cylinders (r - m, hh - m) by alternating projection in B-centred coordinates; a level
-// whose cores come within kCoreSep passes to the next margin; deeper overlaps: least overlap over
-// the centre line and the two axes.
+// contact of cylinders A (centre ca, axis aa) and B: normal (B -> A), point on B, distance
+// (oracle/bullet_mb.py pair_geometry).  beta: FISTA's momentum weights (Consts::dc_beta).
 template <typename R>
 __device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], const R cb[3], const R ab[3], R r, R hh,
-                                              R n[3], R pb[3], R& dist) {
+                                              const R* beta, R n[3], R pb[3], R& dist) {
   const R lx = ca[0] - cb[0], ly = ca[1] - cb[1], lz = ca[2] - cb[2];
   const R margins[4] = {R(0.001), R(0.003), R(0.006), R(0.011)};
-  R qx = R(0), qy = R(0), qz = R(0);
+  R yx = R(0), yy = R(0), yz = R(0);
   for (int lv = 0; lv < 4; ++lv) {
     const R mg = margins[lv], rc = r - mg, hc = hh - mg;
-    R px = R(0), py = R(0), pz = R(0);
-    qx = R(0); qy = R(0); qz = R(0);
-    for (int it = 0; it < kPairRounds; ++it) {
-      const R ox = qx, oy = qy, oz = qz;
-      px = qx; py = qy; pz = qz;
+    yx = R(0); yy = R(0); yz = R(0);
+    R zx = R(0), zy = R(0), zz = R(0);
+#pragma unroll
+    for (int it = 0; it < kPairCold; ++it) {
+      R px = zx, py = zy, pz = zz;
       cyl_project(lx, ly, lz, aa[0], aa[1], aa[2], rc, hc, px, py, pz);
-      qx = px; qy = py; qz = pz;
-      cyl_project(R(0), R(0), R(0), ab[0], ab[1], ab[2], rc, hc, qx, qy, qz);
-      const R mx = qx - ox, my = qy - oy, mz = qz - oz;
-      if (pc_dot(mx, my, mz, mx, my, mz) <= R(1e-24)) break;   // B's point moved <= 1e-12 m
+      cyl_project(R(0), R(0), R(0), ab[0], ab[1], ab[2], rc, hc, px, py, pz);
+      const R b = beta[it];
+      zx = px + b * (px - yx); zy = py + b * (py - yy); zz = pz + b * (pz - yz);
+      yx = px; yy = py; yz = pz;
     }
-    const R vx = px - qx, vy = py - qy, vz = pz - qz;
+    R ax = yx, ay = yy, az = yz;
+    cyl_project(lx, ly, lz, aa[0], aa[1], aa[2], rc, hc, ax, ay, az);
+    const R vx = ax - yx, vy = ay - yy, vz = az - yz;
     const R d2 = pc_dot(vx, vy, vz, vx, vy, vz);
     if (d2 > R(1e-4) * R(1e-4)) {
       const R dc = g_sqrt(d2);
       n[0] = vx / dc; n[1] = vy / dc; n[2] = vz / dc;
-      pb[0] = cb[0] + (qx + n[0] * mg); pb[1] = cb[1] + (qy + n[1] * mg); pb[2] = cb[2] + (qz + n[2] * mg);
+      pb[0] = cb[0] + (yx + n[0] * mg); pb[1] = cb[1] + (yy + n[1] * mg); pb[2] = cb[2] + (yz + n[2] * mg);
       dist = dc - R(2) * mg;
       return;
     }
   }
-  pb[0] = cb[0] + qx; pb[1] = cb[1] + qy; pb[2] = cb[2] + qz;
+  pb[0] = cb[0] + yx; pb[1] = cb[1] + yy; pb[2] = cb[2] + yz;
   const R c2 = pc_dot(lx, ly, lz, lx, ly, lz);
   R best = R(0);
   bool have = false;
@@ -354,7 +366,8 @@ __device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], cons
       ux = a[0]; uy = a[1]; uz = a[2];
     }
     if (pc_dot(ux, uy, uz, lx, ly, lz) < R(0)) { ux = -ux; uy = -uy; uz = -uz; }
-    const R ov = (cyl_extent(ux, uy, uz, aa[0], aa[1], aa[2], r, hh) + cyl_extent(ux, uy, uz, ab[0], ab[1], ab[2], r, hh)) -
+    const R ov = (cyl_extent_cos(pc_dot(ux, uy, uz, aa[0], aa[1], aa[2]), r, hh) +
+                  cyl_extent_cos(pc_dot(ux, uy, uz, ab[0], ab[1], ab[2]), r, hh)) -
                  pc_dot(ux, uy, uz, lx, ly, lz);
     if (!have || ov < best) {
       have = true;
@@ -381,52 +394,238 @@ __device__ __forceinline__ void plane_space(const R n[3], R p[3], R q[3]) {
 }
 
 #ifndef GPD_DC_DIAG
-#define GPD_DC_DIAG 0   // diagnostic builds only (scripts/ab_libs.sh): 1 = no pair solve, 2 = one iteration,
-                        // 3 = no drone contact
+#define GPD_DC_DIAG 0   // diagnostic builds only: 1 = broadphase only (no solve compiled),
+                        // 3 = no drone contact, 6 = the solve compiled but never entered
 #endif
 enum { DC_CX, DC_CY, DC_CZ, DC_AX, DC_AY, DC_AZ, DC_PX, DC_PY, DC_PZ, DC_VX, DC_VY, DC_VZ, DC_WX, DC_WY, DC_WZ,
-       DC_I00, DC_I01, DC_I02, DC_I11, DC_I12, DC_I22, DC_DLX, DC_DLY, DC_DLZ, DC_DAX, DC_DAY, DC_DAZ, DC_RES, DC_N };
+       DC_I00, DC_I01, DC_I02, DC_I11, DC_I12, DC_I22, DC_DLX, DC_DLY, DC_DLZ, DC_DAX, DC_DAY, DC_DAZ, DC_N };
+constexpr int kDcChunks = 32;   // pair chunks of a block: <= 64 (D-1) / 2 / 64 + 1 for D <= 64
 template <typename R>
 struct DcLds {
-  R dc[DC_N][kWave];       // drone columns
-  R sc[25][kWave];         // slot columns
-  int sij[2][kWave];       // slot: drone lanes i, j (i = -1: empty)
-  int scnt[kWave], stouch[kWave];
+  R dc[DC_N][kWave];                  // drone columns
+  unsigned long long nearw[kDcChunks], contw[kDcChunks];   // pairs in reach / in contact, by chunk
+  R eres[kWave];                      // per env: this iteration's largest squared residual
+  int edone[kWave], ecnt[kWave];      // per env: solve finished, contacts
+  int stouch[kWave];                  // drone in a contact
 };
-// one LDS block per instantiation, shared by the broadphase (inlined) and the solve (a call)
+// one LDS block per instantiation, shared by the hook (inlined) and the solve (a call)
 template <typename R>
 __device__ __forceinline__ DcLds<R>& dc_lds() {
   __shared__ DcLds<R> x;
   return x;
 }
-// broadphase of lane ln's pairs (ln, j > ln) (the centre / axis columns written): centres within
-// reach, then a separating-axis reject over the two axes and the centre line - separation along
-// any axis bounds the distance from below, so a pair separated by more than the breaking
-// threshold (+ 1e-9 against rounding) has no contact in the oracle either; the test only spares
-// the narrowphase, it decides nothing the oracle decides
-template <typename R>
-__device__ __forceinline__ bool dc_near(const DcLds<R>& L, const R cc[3], const R ca[3], int j, const Consts<R>& c) {
-  const R ex = cc[0] - L.dc[DC_CX][j], ey = cc[1] - L.dc[DC_CY][j], ez = cc[2] - L.dc[DC_CZ][j];
-  const R e2 = pc_dot(ex, ey, ez, ex, ey, ez);
-  if (!(e2 < c.dd_reach2)) return false;
-  const R bx = L.dc[DC_AX][j], by = L.dc[DC_AY][j], bz = L.dc[DC_AZ][j];
-  const R r = c.cyl_r, hh = c.cyl_hh, lim = c.brk + R(1e-9);
-  const R ab = pc_dot(ca[0], ca[1], ca[2], bx, by, bz);
-  const R s2 = R(1) - ab * ab;
-  const R tilt = hh * g_abs(ab) + r * g_sqrt(s2 > R(0) ? s2 : R(0));   // extent of one along the other's axis
-  if (g_abs(pc_dot(ex, ey, ez, ca[0], ca[1], ca[2])) - (hh + tilt) > lim) return false;
-  if (g_abs(pc_dot(ex, ey, ez, bx, by, bz)) - (hh + tilt) > lim) return false;
-  if (e2 > R(0)) {
-    const R l = g_sqrt(e2);
-    const R ua = pc_dot(ex, ey, ez, ca[0], ca[1], ca[2]) / l, ub = pc_dot(ex, ey, ez, bx, by, bz) / l;
-    const R sa = R(1) - ua * ua, sb = R(1) - ub * ub;
-    const R ext = (hh * g_abs(ua) + r * g_sqrt(sa > R(0) ? sa : R(0))) + (hh * g_abs(ub) + r * g_sqrt(sb > R(0) ? sb : R(0)));
-    if (l - ext > lim) return false;
-  }
-  return true;
+// the per-block layout a kernel hands to the hook (its prologue computes it once)
+struct DcPairs {
+  int npairs, P, D, nch;   // pairs of the block's whole envs, per env, drones per env, chunks
+  int pij[4];              // chunks 0..3: this lane's pair as (lane i) | (lane j) << 8, -1 = none
+  int pmagic;              // p / P == (p * pmagic) >> 20 for p < npairs (host-checked)
+  const int* tab;          // [P] pair q -> i | j << 8 (env-local drones), for chunks >= 4
+  void* rows;              // this block's row store (chunks >= 1), or null
+};
+__device__ __forceinline__ DcPairs dc_pairs_none() {
+  DcPairs dp;
+  dp.npairs = dp.P = dp.nch = dp.pmagic = 0;
+  dp.D = 1;
+  dp.pij[0] = dp.pij[1] = dp.pij[2] = dp.pij[3] = -1;
+  dp.tab = nullptr;
+  dp.rows = nullptr;
+  return dp;
 }
+// whether a kernel of flag set PF runs the drone <-> drone contact (multi-drone PYB* envs)
+template <bool MULTI, int PF>
+__device__ __forceinline__ bool dc_enabled(int flags) {
+  return MULTI && pf_on<PF>(flags, F_BULLET) && !pf_on<PF>(flags, F_NO_DC);
+}
+__device__ __forceinline__ int dc_pair_lanes(const DcPairs& dp, int p);
+// this lane's pair of chunk ch (registers for chunks 0..3, selects rather than a dynamic index)
+__device__ __forceinline__ int dc_pair_of(const DcPairs& dp, int ch, int p) {
+  if (ch >= 4) return dc_pair_lanes(dp, p);
+  return ch == 0 ? dp.pij[0] : (ch == 1 ? dp.pij[1] : (ch == 2 ? dp.pij[2] : dp.pij[3]));
+}
+__device__ __forceinline__ int dc_pair_lanes(const DcPairs& dp, int p) {
+  const int e = (p * dp.pmagic) >> 20;
+  const int t = dp.tab[p - e * dp.P];
+  return ((t & 255) + e * dp.D) | (((t >> 8) + e * dp.D) << 8);
+}
+template <typename R>
+__device__ __forceinline__ DcPairs dc_pairs_for(const SimView<R>& v, int tid, int nact) {
+  DcPairs dp;
+  dp.P = v.dcP;
+  dp.D = v.D;
+  dp.npairs = v.dcP > 0 ? (nact / v.D) * v.dcP : 0;
+  dp.nch = (dp.npairs + kWave - 1) / kWave;
+  dp.pmagic = v.dc_pmagic;
+  dp.tab = v.dc_tab;
+  dp.rows = v.dc_rows ? (void*)((R*)v.dc_rows + (long long)blockIdx.x * v.dc_row_stride) : nullptr;
+#pragma unroll
+  for (int ch = 0; ch < 4; ++ch) {
+    const int p = tid + kWave * ch;
+    dp.pij[ch] = p < dp.npairs ? dc_pair_lanes(dp, p) : -1;
+  }
+  return dp;
+}
+// broadphase of the pair (i, j) (oracle/bullet_mb.py pair_near): the sphere test, then the
+// separating-axis rejects; the centre / axis columns written
+template <typename R>
+__device__ __forceinline__ bool dc_near(const DcLds<R>& L, int i, int j, const Consts<R>& c) {
+  const R ex = L.dc[DC_CX][i] - L.dc[DC_CX][j], ey = L.dc[DC_CY][i] - L.dc[DC_CY][j],
+          ez = L.dc[DC_CZ][i] - L.dc[DC_CZ][j];
+  const R e2 = pc_dot(ex, ey, ez, ex, ey, ez);
+  if (GPD_RARE(e2 < c.dd_reach2)) {
+    const R ax = L.dc[DC_AX][i], ay = L.dc[DC_AY][i], az = L.dc[DC_AZ][i];
+    const R bx = L.dc[DC_AX][j], by = L.dc[DC_AY][j], bz = L.dc[DC_AZ][j];
+    const R r = c.cyl_r, hh = c.cyl_hh, lim = c.brk + R(1e-9);
+    const R tilt = cyl_extent_cos(pc_dot(ax, ay, az, bx, by, bz), r, hh);   // one along the other's axis
+    const R ea = pc_dot(ex, ey, ez, ax, ay, az), eb = pc_dot(ex, ey, ez, bx, by, bz);
+    if (g_abs(ea) - (hh + tilt) > lim) return false;
+    if (g_abs(eb) - (hh + tilt) > lim) return false;
+    if (e2 > R(0)) {
+      const R l = g_sqrt(e2);
+      const R ext = cyl_extent_cos(ea / l, r, hh) + cyl_extent_cos(eb / l, r, hh);
+      if (l - ext > lim) return false;
+    }
+    return true;
+  }
+  return false;
+}
+// a contact's rows: directions (n, t1, t2), arms x direction for A (= i) and B (= j), I_w^-1 of
+// those, rhs, 1/jacDiag, the normal row's jacDiag, impulses
+template <typename R>
+struct DcRow {
+  R d[3][3], A[3][3], B[3][3], gA[3][3], gB[3][3], rhs[3], jdi[3], jdn, lam[3];
+  int i, j, env, rank;
+};
+template <typename R>
+__device__ __forceinline__ void dc_row_setup(const DcLds<R>& L, int i, int j, const R n[3], const R pb[3], R dist,
+                                             const Consts<R>& c, R inv_m, R idt, DcRow<R>& w) {
+  const R pa[3] = {pb[0] + n[0] * dist, pb[1] + n[1] * dist, pb[2] + n[2] * dist};
+  const R ra[3] = {pa[0] - L.dc[DC_PX][i], pa[1] - L.dc[DC_PY][i], pa[2] - L.dc[DC_PZ][i]};
+  const R rb[3] = {pb[0] - L.dc[DC_PX][j], pb[1] - L.dc[DC_PY][j], pb[2] - L.dc[DC_PZ][j]};
+  R t1[3], t2[3];
+  plane_space(n, t1, t2);
+  const R ia[6] = {L.dc[DC_I00][i], L.dc[DC_I01][i], L.dc[DC_I02][i], L.dc[DC_I11][i], L.dc[DC_I12][i], L.dc[DC_I22][i]};
+  const R ib[6] = {L.dc[DC_I00][j], L.dc[DC_I01][j], L.dc[DC_I02][j], L.dc[DC_I11][j], L.dc[DC_I12][j], L.dc[DC_I22][j]};
+  const R dvx = L.dc[DC_VX][i] - L.dc[DC_VX][j], dvy = L.dc[DC_VY][i] - L.dc[DC_VY][j], dvz = L.dc[DC_VZ][i] - L.dc[DC_VZ][j];
+  const R wa[3] = {L.dc[DC_WX][i], L.dc[DC_WY][i], L.dc[DC_WZ][i]};
+  const R wb[3] = {L.dc[DC_WX][j], L.dc[DC_WY][j], L.dc[DC_WZ][j]};
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const R* d = q == 0 ? n : (q == 1 ? t1 : t2);
+    w.d[q][0] = d[0]; w.d[q][1] = d[1]; w.d[q][2] = d[2];
+    R* A = w.A[q];
+    R* B = w.B[q];
+    A[0] = ra[1] * d[2] - ra[2] * d[1]; A[1] = ra[2] * d[0] - ra[0] * d[2]; A[2] = ra[0] * d[1] - ra[1] * d[0];
+    B[0] = rb[1] * d[2] - rb[2] * d[1]; B[1] = rb[2] * d[0] - rb[0] * d[2]; B[2] = rb[0] * d[1] - rb[1] * d[0];
+    w.gA[q][0] = pc_dot(ia[0], ia[1], ia[2], A[0], A[1], A[2]);
+    w.gA[q][1] = pc_dot(ia[1], ia[3], ia[4], A[0], A[1], A[2]);
+    w.gA[q][2] = pc_dot(ia[2], ia[4], ia[5], A[0], A[1], A[2]);
+    w.gB[q][0] = pc_dot(ib[0], ib[1], ib[2], B[0], B[1], B[2]);
+    w.gB[q][1] = pc_dot(ib[1], ib[3], ib[4], B[0], B[1], B[2]);
+    w.gB[q][2] = pc_dot(ib[2], ib[4], ib[5], B[0], B[1], B[2]);
+    const R jd = (inv_m + inv_m + pc_dot(A[0], A[1], A[2], w.gA[q][0], w.gA[q][1], w.gA[q][2])) +
+                 pc_dot(B[0], B[1], B[2], w.gB[q][0], w.gB[q][1], w.gB[q][2]);
+    const R rel = (pc_dot(d[0], d[1], d[2], dvx, dvy, dvz) + pc_dot(A[0], A[1], A[2], wa[0], wa[1], wa[2])) -
+                  pc_dot(B[0], B[1], B[2], wb[0], wb[1], wb[2]);
+    // 1/jd and x/dt as Newton-refined reciprocals (jd >= 2/m > 0): ~1 ulp from the quotients
+    const R inv = g_rcp(jd);
+    if (q == 0) {
+      const R pen = dist + c.slop;
+      w.rhs[0] = pen > R(0) ? (-rel - pen * idt) * inv : (-pen * c.erp * idt - rel) * inv;
+      w.jdn = jd;
+    } else {
+      w.rhs[q] = -rel * inv;
+    }
+    w.jdi[q] = inv;
+    w.lam[q] = R(0);
+  }
+  w.i = i;
+  w.j = j;
+}
+// the rows' Jacobian products and impulse application (vi / vj: the two drones' deltas, linear
+// then angular)
+template <typename R>
+__device__ __forceinline__ R dc_jv(const DcRow<R>& w, int q, const R vi[6], const R vj[6]) {
+  return (pc_dot(w.d[q][0], w.d[q][1], w.d[q][2], vi[0] - vj[0], vi[1] - vj[1], vi[2] - vj[2]) +
+          pc_dot(w.A[q][0], w.A[q][1], w.A[q][2], vi[3], vi[4], vi[5])) -
+         pc_dot(w.B[q][0], w.B[q][1], w.B[q][2], vj[3], vj[4], vj[5]);
+}
+template <typename R>
+__device__ __forceinline__ void dc_apply(const DcRow<R>& w, int q, R delta, R inv_m, R vi[6], R vj[6]) {
+  const R dm = inv_m * delta;
+  vi[0] = vi[0] + w.d[q][0] * dm; vi[1] = vi[1] + w.d[q][1] * dm; vi[2] = vi[2] + w.d[q][2] * dm;
+  vi[3] = vi[3] + w.gA[q][0] * delta; vi[4] = vi[4] + w.gA[q][1] * delta; vi[5] = vi[5] + w.gA[q][2] * delta;
+  vj[0] = vj[0] - w.d[q][0] * dm; vj[1] = vj[1] - w.d[q][1] * dm; vj[2] = vj[2] - w.d[q][2] * dm;
+  vj[3] = vj[3] - w.gB[q][0] * delta; vj[4] = vj[4] - w.gB[q][1] * delta; vj[5] = vj[5] - w.gB[q][2] * delta;
+}
+// one normal row (bullet_mb.drone_contact's normal loop); returns the row's squared residual
+template <typename R>
+__device__ __forceinline__ R dc_normal(DcRow<R>& w, R inv_m, R vi[6], R vj[6]) {
+  R delta = w.rhs[0] - w.jdi[0] * dc_jv(w, 0, vi, vj);
+  const R sum = w.lam[0] + delta;
+  const bool neg = sum < R(0);
+  delta = neg ? -w.lam[0] : delta;
+  w.lam[0] = neg ? R(0) : sum;
+  dc_apply(w, 0, delta, inv_m, vi, vj);
+  const R rr = delta * w.jdn;
+  return rr * rr;
+}
+// one friction pair on the cone (only while the normal impulse is positive); squared residual
+template <typename R>
+__device__ __forceinline__ R dc_friction(DcRow<R>& w, R mu, R inv_m, R vi[6], R vj[6]) {
+  if (!(w.lam[0] > R(0))) return R(0);
+  const R lim = mu * w.lam[0];
+  R s1 = w.lam[1] + (w.rhs[1] - w.jdi[1] * dc_jv(w, 1, vi, vj));
+  R s2 = w.lam[2] + (w.rhs[2] - w.jdi[2] * dc_jv(w, 2, vi, vj));
+  const R m2 = s1 * s1 + s2 * s2;
+  if (m2 > lim * lim) {
+    const R f = lim * g_rsqrt(m2);
+    s1 = s1 * f;
+    s2 = s2 * f;
+  }
+  const R e1 = s1 - w.lam[1], e2 = s2 - w.lam[2];
+  w.lam[1] = s1;
+  w.lam[2] = s2;
+  dc_apply(w, 1, e1, inv_m, vi, vj);
+  dc_apply(w, 2, e2, inv_m, vi, vj);
+  const R rr = e1 + e2;
+  return rr * rr;
+}
+// bits set in words[] over [lo, hi)
+__device__ __forceinline__ int popc_range(const unsigned long long* words, int lo, int hi) {
+  int n = 0;
+  for (int w = lo >> 6; w < ((hi + 63) >> 6); ++w) {
+    unsigned long long m = words[w];
+    const int b0 = w << 6;
+    if (lo > b0) m &= ~0ull << (lo - b0);
+    if (hi < b0 + 64) m &= (1ull << (hi - b0)) - 1ull;
+    n += __popcll(m);
+  }
+  return n;
+}
+// the row store: per chunk, element x of lane ln at chunk[x * 64 + ln] (55 reals), then the four
+// ints (i, j, env, rank) at ints[k * 64 + ln] behind them
+template <typename R>
+__device__ __forceinline__ void dc_row_store(R* chunk, int ln, const DcRow<R>& w) {
+  const R* src = &w.d[0][0];
+#pragma unroll
+  for (int x = 0; x < 55; ++x) chunk[x * kWave + ln] = src[x];
+  int* di = reinterpret_cast<int*>(chunk + 55 * kWave);
+  di[ln] = w.i; di[kWave + ln] = w.j; di[2 * kWave + ln] = w.env; di[3 * kWave + ln] = w.rank;
+}
+template <typename R>
+__device__ __forceinline__ void dc_row_load(const R* chunk, int ln, DcRow<R>& w) {
+  R* dst = &w.d[0][0];
+#pragma unroll
+  for (int x = 0; x < 55; ++x) dst[x] = chunk[x * kWave + ln];
+  const int* si = reinterpret_cast<const int*>(chunk + 55 * kWave);
+  w.i = si[ln]; w.j = si[kWave + ln]; w.env = si[2 * kWave + ln]; w.rank = si[3 * kWave + ln];
+}
+// R elements of one row in the store: 55 reals + 4 ints, column-major over the chunk's 64 lanes
+template <typename R>
+__host__ __device__ constexpr int dc_row_reals() { return 55 + (4 * 4 + (int)sizeof(R) - 1) / (int)sizeof(R); }
+
 // the setup and solve: a call, so that its registers stay out of the substep loop that almost
-// never enters it
+// never enters it (the caller parks its own values in LDS around it: bullet_substep)
 #ifndef GPD_DC_INLINE
 #define GPD_DC_INLINE 0   // A/B builds: 1 = the solve inlined at each substep call site
 #endif
@@ -436,286 +635,169 @@ __device__ __forceinline__ bool dc_near(const DcLds<R>& L, const R cc[3], const 
 #define GPD_DC_ATTR __noinline__
 #endif
 template <typename R>
-__device__ GPD_DC_ATTR void drone_contact(const Consts<R>* cp, R inv_m, R dt, int ln, int base, int D, bool cand) {
-  enum { CX = DC_CX, CY, CZ, AX, AY, AZ, PX, PY, PZ, VX, VY, VZ, WX, WY, WZ, I00, I01, I02, I11, I12, I22,
-         DLX, DLY, DLZ, DAX, DAY, DAZ, RES };
-  enum { RAX, RAY, RAZ, RBX, RBY, RBZ, NX, NY, NZ, T1X, T1Y, T1Z, T2X, T2Y, T2Z, RH0, RH1, RH2, JI0, JI1, JI2, JDN,
-         LM0, LM1, LM2, NSC };
-  static_assert(NSC == 25 && RES == DC_RES, "DcLds layout");
+__device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln, DcPairs dp) {
 #ifdef GPD_CONTACT_STATS
   const unsigned long long t0 = __builtin_readcyclecounter();
   unsigned long long t1 = t0, t2 = t0;
   int n_near = 0;
 #endif
   DcLds<R>& L = dc_lds<R>();
-  auto& dc = L.dc;
-  auto& sc = L.sc;
-  auto& sij = L.sij;
-  auto& scnt = L.scnt;
-  auto& stouch = L.stouch;
-  // everything comes through LDS (the hook wrote this lane's columns): the call takes no
-  // reference to the caller's registers, so the substep loop that almost never calls keeps them
   const Consts<R>& c = *cp;
-  const R r = c.cyl_r, hh = c.cyl_hh;
-  const R ca[3] = {dc[AX][ln], dc[AY][ln], dc[AZ][ln]};
-  const R cc[3] = {dc[CX][ln], dc[CY][ln], dc[CZ][ln]};
-  const R spx = dc[PX][ln], spy = dc[PY][ln], spz = dc[PZ][ln];
-  const R svx = dc[VX][ln], svy = dc[VY][ln], svz = dc[VZ][ln];
-  const R swx = dc[WX][ln], swy = dc[WY][ln], swz = dc[WZ][ln];
-  const int end = base + D;
-  auto near = [&](int j) { return dc_near(L, cc, ca, j, c); };
-
-  // ---- setup: drone columns
-  dc[DLX][ln] = R(0); dc[DLY][ln] = R(0); dc[DLZ][ln] = R(0);
-  dc[DAX][ln] = R(0); dc[DAY][ln] = R(0); dc[DAZ][ln] = R(0);
-  sij[0][ln] = -1;
-  stouch[ln] = 0;
-  // pass 1: this lane's contact count (pairs (ln, j > ln))
-  auto contact = [&](int j, R n[3], R pb[3], R& dist) {
-    const R cb[3] = {dc[CX][j], dc[CY][j], dc[CZ][j]}, ab[3] = {dc[AX][j], dc[AY][j], dc[AZ][j]};
-    pair_geometry(cc, ca, cb, ab, r, hh, n, pb, dist);
-    return dist < c.brk;
-  };
-  // the first kCache contacts' geometry stays in registers for pass 2 (later ones are recomputed)
-  constexpr int kCache = 2;
-  R cn[kCache][3], cpb[kCache][3], cdist[kCache];
-  int cj[kCache] = {-1, -1};
-  int cnt = 0;
-  if (cand) {
-    for (int j = ln + 1; j < end; ++j) {
-      if (!near(j)) continue;
+  const R idt = g_rcp(dt);
+  const int nenv = dp.P > 0 ? dp.npairs / dp.P : 0;
+  L.dc[DC_DLX][ln] = R(0); L.dc[DC_DLY][ln] = R(0); L.dc[DC_DLZ][ln] = R(0);
+  L.dc[DC_DAX][ln] = R(0); L.dc[DC_DAY][ln] = R(0); L.dc[DC_DAZ][ln] = R(0);
+  L.stouch[ln] = 0;
+  // ---- narrowphase of the pairs in reach (in parallel over lanes), rows by the pair's lane
+  DcRow<R> w0;
+  bool have0 = false;
+  w0.i = w0.j = 0;
+  R* rows = reinterpret_cast<R*>(dp.rows);
+  constexpr int kRowR = dc_row_reals<R>();
+  for (int ch = 0; ch < dp.nch; ++ch) {
+    const unsigned long long nw = L.nearw[ch];
+    bool con = false;
+    if (nw != 0) {
+      const int p = ln + kWave * ch;
+      if ((nw >> ln) & 1ull) {
 #ifdef GPD_CONTACT_STATS
-      ++n_near;
+        ++n_near;
 #endif
-      R n[3], pb[3], dist;
-      if (contact(j, n, pb, dist)) {
-        if (cnt < kCache) {
-#pragma unroll
-          for (int x = 0; x < 3; ++x) { cn[cnt][x] = n[x]; cpb[cnt][x] = pb[x]; }
-          cdist[cnt] = dist;
-          cj[cnt] = j;
+        const int pij = dc_pair_of(dp, ch, p);
+        const int i = pij & 255, j = pij >> 8;
+        const R ca[3] = {L.dc[DC_CX][i], L.dc[DC_CY][i], L.dc[DC_CZ][i]}, aa[3] = {L.dc[DC_AX][i], L.dc[DC_AY][i], L.dc[DC_AZ][i]};
+        const R cb[3] = {L.dc[DC_CX][j], L.dc[DC_CY][j], L.dc[DC_CZ][j]}, ab[3] = {L.dc[DC_AX][j], L.dc[DC_AY][j], L.dc[DC_AZ][j]};
+        R n[3], pb[3], dist;
+        pair_geometry(ca, aa, cb, ab, c.cyl_r, c.cyl_hh, c.dc_beta, n, pb, dist);
+        con = dist < c.brk;
+        if (con) {
+          DcRow<R> w;
+          dc_row_setup(L, i, j, n, pb, dist, c, inv_m, idt, w);
+          w.env = (p * dp.pmagic) >> 20;
+          if (ch == 0) {
+            w0 = w;
+            have0 = true;
+          } else {
+            dc_row_store(rows + (long long)(ch - 1) * kWave * kRowR, ln, w);
+          }
+          L.stouch[i] = 1;
+          L.stouch[j] = 1;
         }
-        ++cnt;
       }
     }
+    const unsigned long long cw = __ballot(con);
+    if (ln == 0) L.contw[ch] = cw;
   }
-  scnt[ln] = cnt;
   wave_lds_sync();
 #ifdef GPD_CONTACT_STATS
   t1 = __builtin_readcyclecounter();
 #endif
-  int slot = 0;
-  for (int x = base; x < ln; ++x) slot += scnt[x];
-  // pass 2: the rows of this lane's contacts, into the env's slot columns
-  if (cnt > 0) {
-    int m = 0;
-    for (int j = ln + 1; j < end && slot < D; ++j) {
-      if (!near(j)) continue;
-      R n[3], pb[3], dist;
-      if (m < kCache) {
-        if (cj[m] != j) continue;
-#pragma unroll
-        for (int x = 0; x < 3; ++x) { n[x] = cn[m][x]; pb[x] = cpb[m][x]; }
-        dist = cdist[m];
-      } else if (!contact(j, n, pb, dist)) {
-        continue;
-      }
-      ++m;
-      const int col = base + slot;
-      ++slot;
-      const R pa[3] = {pb[0] + n[0] * dist, pb[1] + n[1] * dist, pb[2] + n[2] * dist};
-      const R ra[3] = {pa[0] - spx, pa[1] - spy, pa[2] - spz};
-      const R rb[3] = {pb[0] - dc[PX][j], pb[1] - dc[PY][j], pb[2] - dc[PZ][j]};
-      R t1[3], t2[3];
-      plane_space(n, t1, t2);
-      const R* dirs[3] = {n, t1, t2};
-      const R jb[6] = {dc[I00][j], dc[I01][j], dc[I02][j], dc[I11][j], dc[I12][j], dc[I22][j]};
-      const R ja[6] = {dc[I00][ln], dc[I01][ln], dc[I02][ln], dc[I11][ln], dc[I12][ln], dc[I22][ln]};
-      const R dvx = svx - dc[VX][j], dvy = svy - dc[VY][j], dvz = svz - dc[VZ][j];
-      for (int q = 0; q < 3; ++q) {
-        const R* d = dirs[q];
-        const R aax = ra[1] * d[2] - ra[2] * d[1], aay = ra[2] * d[0] - ra[0] * d[2], aaz = ra[0] * d[1] - ra[1] * d[0];
-        const R abx = rb[1] * d[2] - rb[2] * d[1], aby = rb[2] * d[0] - rb[0] * d[2], abz = rb[0] * d[1] - rb[1] * d[0];
-        const R gax = pc_dot(ja[0], ja[1], ja[2], aax, aay, aaz), gay = pc_dot(ja[1], ja[3], ja[4], aax, aay, aaz),
-                gaz = pc_dot(ja[2], ja[4], ja[5], aax, aay, aaz);
-        const R gbx = pc_dot(jb[0], jb[1], jb[2], abx, aby, abz), gby = pc_dot(jb[1], jb[3], jb[4], abx, aby, abz),
-                gbz = pc_dot(jb[2], jb[4], jb[5], abx, aby, abz);
-        const R jd = (inv_m + inv_m + pc_dot(aax, aay, aaz, gax, gay, gaz)) + pc_dot(abx, aby, abz, gbx, gby, gbz);
-        const R rel = (pc_dot(d[0], d[1], d[2], dvx, dvy, dvz) + pc_dot(aax, aay, aaz, swx, swy, swz)) -
-                      pc_dot(abx, aby, abz, dc[WX][j], dc[WY][j], dc[WZ][j]);
-        R rhs;
-        if (q == 0) {
-          const R pen = dist + c.slop;
-          rhs = pen > R(0) ? (-rel - pen / dt) / jd : (-pen * c.erp / dt - rel) / jd;
-          sc[JDN][col] = jd;
-        } else {
-          rhs = -rel / jd;
-        }
-        sc[RH0 + q][col] = rhs;
-        sc[JI0 + q][col] = R(1) / jd;
-        sc[LM0 + q][col] = R(0);
-      }
-      sc[RAX][col] = ra[0]; sc[RAY][col] = ra[1]; sc[RAZ][col] = ra[2];
-      sc[RBX][col] = rb[0]; sc[RBY][col] = rb[1]; sc[RBZ][col] = rb[2];
-      sc[NX][col] = n[0]; sc[NY][col] = n[1]; sc[NZ][col] = n[2];
-      sc[T1X][col] = t1[0]; sc[T1Y][col] = t1[1]; sc[T1Z][col] = t1[2];
-      sc[T2X][col] = t2[0]; sc[T2Y][col] = t2[1]; sc[T2Z][col] = t2[2];
-      sij[0][col] = ln;
-      sij[1][col] = j;
-      stouch[ln] = 1;
-      stouch[j] = 1;
-    }
+  // contacts per env, each contact's rank within its env (the (i, j) order)
+  int rounds = 0;
+  for (int e = 0; e < nenv; ++e) {
+    const int k = popc_range(L.contw, e * dp.P, (e + 1) * dp.P);
+    rounds = k > rounds ? k : rounds;
   }
-  wave_lds_sync();
-
+  if (have0) w0.rank = popc_range(L.contw, w0.env * dp.P, ln);
+  for (int ch = 1; ch < dp.nch; ++ch) {
+    if (((L.contw[ch] >> ln) & 1ull) == 0) continue;
+    int* ri = reinterpret_cast<int*>(rows + (long long)(ch - 1) * kWave * kRowR + 55 * kWave);
+    ri[3 * kWave + ln] = popc_range(L.contw, ri[2 * kWave + ln] * dp.P, ln + kWave * ch);
+  }
+  const R mu = c.dd_mu, resid = c.resid;
+  const int iters = c.iters;
 #ifdef GPD_CONTACT_STATS
   t2 = __builtin_readcyclecounter();
   int it_used = 0;
 #endif
-  // ---- projected Gauss-Seidel per env.  The owner lane of a slot keeps its rows in registers
-  // (directions, a = r x d and g = I^-1 a of both drones, rhs, 1/jacDiag, impulses); only the two
-  // drones' velocity deltas go through LDS.  Rounds run over the slots some env of the wave uses.
-  const int dl = ln - base;
-  const int oi = sij[0][ln], oj = sij[1][ln];
-  const bool own = oi >= 0;
-  bool envdone = true;
-  for (int x = base; x < end; ++x) envdone = envdone && sij[0][x] < 0;
-  int rounds = 0;
-  for (int kk = D - 1; kk >= 0 && rounds == 0; --kk)
-    if (__ballot(own && dl == kk) != 0ull) rounds = kk + 1;
-  R rd[3][3], ra_[3][3], rb_[3][3], rga[3][3], rgb[3][3], rhs[3], jdi[3], lam[3] = {R(0), R(0), R(0)}, jdn = R(0);
-  if (own) {
-    const R ra0 = sc[RAX][ln], ra1 = sc[RAY][ln], ra2 = sc[RAZ][ln];
-    const R rb0 = sc[RBX][ln], rb1 = sc[RBY][ln], rb2 = sc[RBZ][ln];
-    const R ia[6] = {dc[I00][oi], dc[I01][oi], dc[I02][oi], dc[I11][oi], dc[I12][oi], dc[I22][oi]};
-    const R ib[6] = {dc[I00][oj], dc[I01][oj], dc[I02][oj], dc[I11][oj], dc[I12][oj], dc[I22][oj]};
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      R* d = rd[q];
-      d[0] = sc[NX + 3 * q][ln]; d[1] = sc[NY + 3 * q][ln]; d[2] = sc[NZ + 3 * q][ln];
-      R* A = ra_[q];
-      R* B = rb_[q];
-      A[0] = ra1 * d[2] - ra2 * d[1]; A[1] = ra2 * d[0] - ra0 * d[2]; A[2] = ra0 * d[1] - ra1 * d[0];
-      B[0] = rb1 * d[2] - rb2 * d[1]; B[1] = rb2 * d[0] - rb0 * d[2]; B[2] = rb0 * d[1] - rb1 * d[0];
-      rga[q][0] = pc_dot(ia[0], ia[1], ia[2], A[0], A[1], A[2]);
-      rga[q][1] = pc_dot(ia[1], ia[3], ia[4], A[0], A[1], A[2]);
-      rga[q][2] = pc_dot(ia[2], ia[4], ia[5], A[0], A[1], A[2]);
-      rgb[q][0] = pc_dot(ib[0], ib[1], ib[2], B[0], B[1], B[2]);
-      rgb[q][1] = pc_dot(ib[1], ib[3], ib[4], B[0], B[1], B[2]);
-      rgb[q][2] = pc_dot(ib[2], ib[4], ib[5], B[0], B[1], B[2]);
-      rhs[q] = sc[RH0 + q][ln];
-      jdi[q] = sc[JI0 + q][ln];
-    }
-    jdn = sc[JDN][ln];
-  }
-  // the two drones' velocity deltas: loaded together, updated, stored together
-  R vi[6], vj[6];
-  auto load_dv = [&]() {
-#pragma unroll
-    for (int x = 0; x < 6; ++x) { vi[x] = dc[DLX + x][oi]; vj[x] = dc[DLX + x][oj]; }
-  };
-  auto store_dv = [&]() {
-#pragma unroll
-    for (int x = 0; x < 6; ++x) { dc[DLX + x][oi] = vi[x]; dc[DLX + x][oj] = vj[x]; }
-  };
-  auto jv = [&](int q) {
-    const R* d = rd[q];
-    return (pc_dot(d[0], d[1], d[2], vi[0] - vj[0], vi[1] - vj[1], vi[2] - vj[2]) +
-            pc_dot(ra_[q][0], ra_[q][1], ra_[q][2], vi[3], vi[4], vi[5])) -
-           pc_dot(rb_[q][0], rb_[q][1], rb_[q][2], vj[3], vj[4], vj[5]);
-  };
-  auto apply = [&](int q, R delta) {
-    const R dm = inv_m * delta;
-    const R* d = rd[q];
-    vi[0] = vi[0] + d[0] * dm; vi[1] = vi[1] + d[1] * dm; vi[2] = vi[2] + d[2] * dm;
-    vi[3] = vi[3] + rga[q][0] * delta; vi[4] = vi[4] + rga[q][1] * delta; vi[5] = vi[5] + rga[q][2] * delta;
-    vj[0] = vj[0] - d[0] * dm; vj[1] = vj[1] - d[1] * dm; vj[2] = vj[2] - d[2] * dm;
-    vj[3] = vj[3] - rgb[q][0] * delta; vj[4] = vj[4] - rgb[q][1] * delta; vj[5] = vj[5] - rgb[q][2] * delta;
-  };
-#if GPD_DC_DIAG == 2
-  const int iters = 1;   // diagnostic build: one Gauss-Seidel iteration per solve
-#else
-  const int iters = c.iters;
-#endif
-  for (int it = 0; it < iters; ++it) {
-    if (__ballot(!envdone) == 0ull) break;
+  if (rounds <= 1 && dp.nch <= 1) {
+    // ---- every env has at most one contact: its lane owns both drones' deltas
+    R vi[6] = {R(0), R(0), R(0), R(0), R(0), R(0)}, vj[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+    bool done = !have0;
+    for (int it = 0; it < iters; ++it) {
+      if (__ballot(!done) == 0ull) break;
 #ifdef GPD_CONTACT_STATS
-    it_used = it + 1;
+      it_used = it + 1;
 #endif
-    R res = R(0);
-    const bool mine = own && !envdone;
-    for (int kk = 0; kk < rounds; ++kk) {            // normal rows, slot order
-      if (mine && dl == kk) {
-        load_dv();
-        R delta = rhs[0] - jdi[0] * jv(0);
-        const R sum = lam[0] + delta;
-        const bool neg = sum < R(0);
-        delta = neg ? -lam[0] : delta;
-        lam[0] = neg ? R(0) : sum;
-        apply(0, delta);
-        store_dv();
-        const R rr = delta * jdn;
-        res = g_fmax(res, rr * rr);
+      if (!done) {
+        R res = dc_normal(w0, inv_m, vi, vj);
+        res = g_fmax(res, dc_friction(w0, mu, inv_m, vi, vj));
+        done = res <= resid;
       }
-      wave_lds_sync();
     }
-    for (int kk = 0; kk < rounds; ++kk) {            // friction pairs on the cone
-      if (mine && dl == kk && lam[0] > R(0)) {
-        load_dv();
-        const R lim = c.dd_mu * lam[0];
-        R s1 = lam[1] + (rhs[1] - jdi[1] * jv(1));
-        R s2 = lam[2] + (rhs[2] - jdi[2] * jv(2));
-        const R m2 = s1 * s1 + s2 * s2;
-        if (m2 > lim * lim) {
-          const R f = lim / g_sqrt(m2);
-          s1 = s1 * f;
-          s2 = s2 * f;
+    if (have0) {
+      L.dc[DC_DLX][w0.i] = vi[0]; L.dc[DC_DLY][w0.i] = vi[1]; L.dc[DC_DLZ][w0.i] = vi[2];
+      L.dc[DC_DAX][w0.i] = vi[3]; L.dc[DC_DAY][w0.i] = vi[4]; L.dc[DC_DAZ][w0.i] = vi[5];
+      L.dc[DC_DLX][w0.j] = vj[0]; L.dc[DC_DLY][w0.j] = vj[1]; L.dc[DC_DLZ][w0.j] = vj[2];
+      L.dc[DC_DAX][w0.j] = vj[3]; L.dc[DC_DAY][w0.j] = vj[4]; L.dc[DC_DAZ][w0.j] = vj[5];
+    }
+  } else {
+    // ---- general case: round r solves the r-th contact of every env; deltas through LDS
+    if (ln < nenv) L.edone[ln] = popc_range(L.contw, ln * dp.P, (ln + 1) * dp.P) == 0;
+    wave_lds_sync();
+    R vi[6], vj[6];
+    auto visit = [&](DcRow<R>& w, bool friction) {
+      if (L.edone[w.env]) return;
+#pragma unroll
+      for (int x = 0; x < 6; ++x) { vi[x] = L.dc[DC_DLX + x][w.i]; vj[x] = L.dc[DC_DLX + x][w.j]; }
+      const R rr = friction ? dc_friction(w, mu, inv_m, vi, vj) : dc_normal(w, inv_m, vi, vj);
+#pragma unroll
+      for (int x = 0; x < 6; ++x) { L.dc[DC_DLX + x][w.i] = vi[x]; L.dc[DC_DLX + x][w.j] = vj[x]; }
+      L.eres[w.env] = g_fmax(L.eres[w.env], rr);   // one row of an env per round: no race
+    };
+    for (int it = 0; it < iters; ++it) {
+      if (__ballot(ln < nenv && !L.edone[ln]) == 0ull) break;
+#ifdef GPD_CONTACT_STATS
+      it_used = it + 1;
+#endif
+      if (ln < nenv) L.eres[ln] = R(0);
+      wave_lds_sync();
+      for (int ph = 0; ph < 2; ++ph) {              // normal rows, then friction pairs
+        for (int r = 0; r < rounds; ++r) {
+          if (have0 && w0.rank == r) visit(w0, ph == 1);
+          for (int ch = 1; ch < dp.nch; ++ch) {
+            if (((L.contw[ch] >> ln) & 1ull) == 0) continue;
+            R* chunk = rows + (long long)(ch - 1) * kWave * kRowR;
+            DcRow<R> w;
+            dc_row_load(chunk, ln, w);
+            if (w.rank != r) continue;
+            visit(w, ph == 1);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) chunk[(52 + q) * kWave + ln] = w.lam[q];
+          }
+          wave_lds_sync();
         }
-        const R e1 = s1 - lam[1], e2 = s2 - lam[2];
-        lam[1] = s1;
-        lam[2] = s2;
-        apply(1, e1);
-        apply(2, e2);
-        store_dv();
-        const R rr = e1 + e2;
-        res = g_fmax(res, rr * rr);
       }
+      if (ln < nenv && !L.edone[ln]) L.edone[ln] = L.eres[ln] <= resid;
       wave_lds_sync();
     }
-    dc[RES][ln] = res;
-    wave_lds_sync();
-    R er = R(0);
-    for (int x = base; x < end; ++x) er = g_fmax(er, dc[RES][x]);
-    envdone = envdone || er <= c.resid;
-    wave_lds_sync();
   }
 #ifdef GPD_CONTACT_STATS
   {
     const unsigned long long t3 = __builtin_readcyclecounter();
-    unsigned long long nn = 0, ns = 0;
-    for (int x = 0; x < kWave; ++x) ns += (sij[0][x] >= 0);
-    int tot = n_near;
-    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
-    nn = (unsigned long long)tot;
+    int tot = n_near, nc = have0 ? 1 : 0;
+    for (int o = 32; o > 0; o >>= 1) { tot += __shfl_xor(tot, o); nc += __shfl_xor(nc, o); }
     if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) {
       atomicAdd(&g_pc_hist[116], 1ull);
       atomicAdd(&g_pc_hist[117], t2 - t0);
       atomicAdd(&g_pc_hist[118], t3 - t2);
       atomicAdd(&g_pc_hist[119], (unsigned long long)it_used);
       atomicAdd(&g_pc_hist[123], t1 - t0);
-      atomicAdd(&g_pc_hist[126], ns);
-      atomicAdd(&g_pc_hist[127], nn);
+      atomicAdd(&g_pc_hist[126], (unsigned long long)nc);
+      atomicAdd(&g_pc_hist[127], (unsigned long long)tot);
     }
   }
 #endif
   wave_lds_sync();   // the caller reads the velocity deltas
 }
-// the hook bullet_substep calls (multi-drone envs of one-wave blocks)
+// the hook bullet_substep calls (multi-drone envs of one-wave blocks): pk parks the caller's
+// values in LDS around the solve (bullet_substep), so nothing of the substep loop is live across
+// the call and the loop's own register allocation does not see the solve
 struct DcHook {
-  int tid, base, D;
-  bool active;
-  template <typename R>
-  __device__ __forceinline__ void operator()(Drone<R>& s, const R* Rm, const Consts<R>& c, const DynK<R>& k) const {
+  int tid;
+  DcPairs dp;
+  template <typename R, class PK>
+  __device__ __forceinline__ void operator()(Drone<R>& s, R* Rm, const Consts<R>& c, const DynK<R>& k, const PK& pk) const {
 #if GPD_DC_DIAG == 3
     return;   // diagnostic build: no drone contact at all (the hook compiled in, its body not)
 #endif
@@ -723,23 +805,24 @@ struct DcHook {
     const unsigned long long tb = __builtin_readcyclecounter();
 #endif
     DcLds<R>& L = dc_lds<R>();
+    const DcPairs& P = dp;
     const int ln = tid & (kWave - 1);
     const R zo = c.cyl_zoff;
-    const R cc[3] = {s.px + Rm[2] * zo, s.py + Rm[5] * zo, s.pz + Rm[8] * zo};
-    L.dc[DC_CX][ln] = cc[0]; L.dc[DC_CY][ln] = cc[1]; L.dc[DC_CZ][ln] = cc[2];
+    L.dc[DC_CX][ln] = s.px + Rm[2] * zo; L.dc[DC_CY][ln] = s.py + Rm[5] * zo; L.dc[DC_CZ][ln] = s.pz + Rm[8] * zo;
     L.dc[DC_AX][ln] = Rm[2]; L.dc[DC_AY][ln] = Rm[5]; L.dc[DC_AZ][ln] = Rm[8];
     wave_lds_sync();
-#if GPD_DC_DIAG == 5
-    return;   // diagnostic build: the centre / axis exchange only
-#endif
-    bool cand = false;
-    const R ca[3] = {Rm[2], Rm[5], Rm[8]};
-    if (active)
-      for (int j = ln + 1; j < base + D; ++j) cand = cand || dc_near(L, cc, ca, j, c);
-    // the common case: no pair of the wave within reach
-#if GPD_DC_DIAG == 1
-    cand = false;   // diagnostic build: broadphase only, no solve
-#endif
+    bool any = false;
+    for (int ch = 0; ch < P.nch; ++ch) {
+      const int p = ln + kWave * ch;
+      bool near = false;
+      if (p < P.npairs) {
+        const int pij = dc_pair_of(P, ch, p);
+        near = dc_near(L, pij & 255, pij >> 8, c);
+      }
+      const unsigned long long w = __ballot(near);
+      if (ln == 0) L.nearw[ch] = w;
+      any = any || w != 0ull;
+    }
 #ifdef GPD_CONTACT_STATS
     {
       const unsigned long long te = __builtin_readcyclecounter();
@@ -749,10 +832,12 @@ struct DcHook {
       }
     }
 #endif
-#if GPD_DC_DIAG == 4
-    if (__ballot(cand) != 0ull) s.vx = s.vx + R(0);   // diagnostic build: broadphase, no solve compiled
-#else
-    if (GPD_RARE(__ballot(cand) != 0ull)) {
+#if GPD_DC_DIAG == 1
+    any = false;   // diagnostic build: broadphase only, no solve
+#elif GPD_DC_DIAG == 6
+    any = any && (k.flags & (1 << 29)) != 0;   // diagnostic build: the solve compiled, never entered
+#endif
+    if (GPD_RARE(any)) {
       // this lane's columns for the solve: pose, velocities, world inverse inertia R diag(1/I) R^T
       const R q00 = k.ijx * Rm[0], q01 = k.ijy * Rm[1], q02 = k.ijz * Rm[2];
       const R q10 = k.ijx * Rm[3], q11 = k.ijy * Rm[4], q12 = k.ijz * Rm[5];
@@ -766,14 +851,17 @@ struct DcHook {
       L.dc[DC_PX][ln] = s.px; L.dc[DC_PY][ln] = s.py; L.dc[DC_PZ][ln] = s.pz;
       L.dc[DC_VX][ln] = s.vx; L.dc[DC_VY][ln] = s.vy; L.dc[DC_VZ][ln] = s.vz;
       L.dc[DC_WX][ln] = s.wx; L.dc[DC_WY][ln] = s.wy; L.dc[DC_WZ][ln] = s.wz;
+      const R inv_m = k.inv_m, dt = k.dt;
+      const DcPairs dpc = P;
       wave_lds_sync();
-      drone_contact<R>(&c, k.inv_m, k.dt, ln, base, D, cand);
+      pk.park();
+      dc_solve<R>(&c, inv_m, dt, ln, dpc);
+      pk.unpark();
       if (L.stouch[ln]) {
         s.vx = s.vx + L.dc[DC_DLX][ln]; s.vy = s.vy + L.dc[DC_DLY][ln]; s.vz = s.vz + L.dc[DC_DLZ][ln];
         s.wx = s.wx + L.dc[DC_DAX][ln]; s.wy = s.wy + L.dc[DC_DAY][ln]; s.wz = s.wz + L.dc[DC_DAZ][ln];
       }
     }
-#endif
     wave_lds_sync();   // the centre columns are rewritten by the next substep
   }
 };
@@ -783,8 +871,7 @@ struct DcHook {
 template <typename R, bool MULTI, int PF, bool ANGV = true>
 __device__ __forceinline__ void substep_block(Drone<R>& s, R rpm[4], R W[4], R last[4],
                                               const Consts<R>& c, DynK<R>& k, R* sx, R* sy, R* sz, int tid,
-                                              int base, int D, DwPairs pairs = DwPairs{0, 0}, R* spair = nullptr,
-                                              bool active = true) {
+                                              int base, int D, DwPairs pairs, R* spair, const DcPairs& dcp) {
   R dw = R(0);
   if (MULTI && pf_on<PF>(k.flags, F_DW)) {
     sx[tid] = s.px; sy[tid] = s.py; sz[tid] = s.pz;
@@ -804,7 +891,7 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, R rpm[4], R W[4], R l
     }
     wave_lds_sync();
   }
-  if (MULTI) dyn_substep<R, PF, ANGV, 1, DcHook>(s, rpm, W, last, dw, c, k, DcHook{tid, base, D, active});
+  if (MULTI) dyn_substep<R, PF, ANGV, 1, DcHook>(s, rpm, W, last, dw, c, k, DcHook{tid, dcp});
   else dyn_substep<R, PF, ANGV>(s, rpm, W, last, dw, c, k);
 }
 
@@ -955,6 +1042,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
   const long long nn = active ? n : n0;
   const long long e = MULTI ? nn / D : nn;
   const bool drag = pf_on<PF>(c.flags, F_DRAG);
+  // drone <-> drone contact: the block's pair layout (the pair table loads go out with the state's)
+  const DcPairs dcp = dc_enabled<MULTI, PF>(c.flags) ? dc_pairs_for(v, tid, nact) : dc_pairs_none();
 
   Drone<R> s;
   R last[4];
@@ -1031,7 +1120,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
   history_dma();   // diagnostic build: the DMA behind the state loads instead of the first substep
 #endif
   if (dk.nsub > 1) {
-    substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, active);
+    substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, dcp);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
     GPD_STAMP(1);
@@ -1039,9 +1128,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
     history_dma();
 #endif
     for (int it = 1; it < dk.nsub - 1; ++it)
-      substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, active);
+      substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, dcp);
   }
-  substep_block<R, MULTI, PF, true>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, active);
+  substep_block<R, MULTI, PF, true>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, dcp);
 #pragma unroll
   for (int k = 0; k < 4; ++k) last[k] = rpm[k];
 #ifndef GPD_DMA_EARLY
@@ -1822,11 +1911,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_INTEG
   const bool active = tid < v.tpb && n < v.N;
   const long long nn = active ? n : (long long)blockIdx.x * v.tpb;   // the block's first drone (step_kernel)
   (void)d;
+  const long long nleft = v.N - (long long)blockIdx.x * v.tpb;
+  const int nact = (int)(nleft < v.tpb ? nleft : v.tpb);
   Drone<R> s;
   R last[4];
   load_drone<R, STREAM>(v, nn, s, last, true);
   const long long N = v.N;
   DynK<R> dk = dyn_consts(c);
+  const DcPairs dcp = dc_enabled<MULTI, PF>(c.flags) ? dc_pairs_for(v, tid, nact) : dc_pairs_none();
   // RPMs are loaded two substeps ahead of their use (substeps t+1 and t+2 in flight while t
   // integrates): more bytes in flight per wave for the HBM stream.  A drone's 4 RPMs are one
   // aligned 4*sizeof(R)-byte vector (rows of the [T][N][4] tensor).
@@ -1862,7 +1954,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_INTEG
     if (t + 2 < n_sub) load4(t + 2, nxt2);
     R W[4];
     rpm_wrench<R, PF>(rpm, dk, c, W);
-    substep_block<R, MULTI, PF>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, DwPairs{0, 0}, nullptr, active);
+    substep_block<R, MULTI, PF>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, DwPairs{0, 0}, nullptr, dcp);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];
     if (TRAJ && active) {   // TRAJ: the trajectory variant (its readback / Euler registers stay out of the other)

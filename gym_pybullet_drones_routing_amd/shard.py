@@ -93,13 +93,17 @@ class LearnerHandoff:
        ``mode="gather"`` (one learner: ``dist.gather`` to rank 0, G x prefix bytes land there
        only) or ``mode="all_gather"`` (data-parallel learners: ``all_gather_into_tensor``, the
        batch lands on every rank);
-    4. terminal rows (``terminal_obs=True``) move only for envs that finished this step, packed
-       densely: in "all_gather" mode every rank knows every rank's done count from the gathered
-       flags, and one ``all_gather_into_tensor`` of [max count, D, W] per rank runs when any env
-       finished; in "gather" mode one ``all_reduce(MAX)`` of a single int gives the step's
-       largest per-rank count and one ``dist.gather`` of [max count, D, W] per rank brings the
-       rows to the learner (collectives only, no point-to-point pairs).  Steps where no env
-       finished move no terminal bytes.
+    4. terminal rows (``terminal_obs=True``): every rank compacts the rows of its envs that
+       finished this step on the device (a prefix sum over its done flags, ``index_copy_``) into
+       a fixed block of ``terminal_capacity`` rows (default: the shard's env count, so it never
+       overflows), and that block goes the prefix's way (``gather`` / ``all_gather_into_tensor``);
+       the receiving ranks place row j of rank r at rank r's j-th finished env, again from the
+       gathered flags on the device.  Every size is fixed, so a step issues its collectives without
+       waiting for the device: no ``.item()`` / ``.tolist()`` / boolean indexing anywhere (round
+       3 sized the terminal exchange from the done counts, two host syncs per step, each longer
+       than the ~5 us step itself).  A smaller ``terminal_capacity`` moves fewer bytes; a step
+       whose finished envs exceed it on some rank drops their rows and raises the
+       ``overflowed()`` flag (a device tensor the caller reads when it synchronises anyway).
 
     ``step`` returns (obs [E, D, W], reward [E], terminated [E], truncated [E], terminal_obs or
     None) - freshly allocated tensors, so a caller may keep them across steps - on the learner
@@ -111,7 +115,7 @@ class LearnerHandoff:
     MODES = ("all_gather", "gather")
 
     def __init__(self, sim, global_envs, learner_rank=0, terminal_obs=True, mode="all_gather",
-                 force_collectives=False):
+                 force_collectives=False, terminal_capacity=None):
         if mode not in self.MODES:
             raise ValueError(f"mode must be one of {self.MODES}")
         self.sim = sim
@@ -135,6 +139,16 @@ class LearnerHandoff:
         self.pack_all = torch.empty((self.world * self.nbytes,), dtype=torch.uint8, device=dev)
         D, A = sim.drones_per_env, sim.act_width
         self.local_actions = torch.empty((self.count, D, A), dtype=torch.float32, device=dev)
+        C = self.count if terminal_capacity is None else int(terminal_capacity)
+        if not 1 <= C <= self.count:
+            raise ValueError(f"terminal_capacity must be in [1, {self.count}]")
+        self.capacity = C
+        W = sim.obs_width
+        # the compacted block (+ one scratch row that the envs still running write to) and the
+        # gathered blocks of every rank
+        self._tblock = torch.zeros((C + 1, D * W), dtype=torch.float32, device=dev)
+        self._trows = torch.zeros((self.world * C, D * W), dtype=torch.float32, device=dev)
+        self._overflow = torch.zeros((), dtype=torch.bool, device=dev)
         self.terminal_bytes = 0     # terminal-row bytes received by the learner so far (all steps)
         self.steps = 0
 
@@ -151,6 +165,11 @@ class LearnerHandoff:
         "all_gather", on the learner for "gather")."""
         return (self.global_envs * self.sim.drones_per_env * self.sim.act_width * 4,
                 self.world * self.nbytes)
+
+    def overflowed(self):
+        """True when some step's finished envs exceeded ``terminal_capacity`` on some rank (their
+        terminal rows were not delivered).  Reads a device flag: a host synchronisation."""
+        return bool(self._overflow)
 
     def stats(self):
         """Bytes per step of each part of the hand-off (learner side), averaged over the steps."""
@@ -212,65 +231,54 @@ class LearnerHandoff:
         off, n = self.layout[name]
         return self.sim.out_pack[off:off + n].view(dtype).reshape(shape)
 
+    def _exchange_rows(self):
+        """The compacted terminal blocks [C, D*W] of every rank -> self._trows (receiving ranks)."""
+        local = self._tblock[:self.capacity]
+        if not self._coll:
+            self._trows.copy_(local)
+            return
+        if self.mode == "all_gather":
+            if self._gloo:
+                host = [torch.empty(tuple(local.shape), dtype=torch.float32) for _ in range(self.world)]
+                dist.all_gather(host, local.cpu())
+                self._trows.copy_(torch.cat(host))
+            else:
+                dist.all_gather_into_tensor(self._trows, local)
+        else:
+            if self._gloo:
+                host = [torch.empty(tuple(local.shape), dtype=torch.float32) for _ in range(self.world)] \
+                    if self.is_learner else None
+                dist.gather(local.cpu(), host, dst=self.learner)
+                if self.is_learner:
+                    self._trows.copy_(torch.cat(host))
+            else:
+                parts = list(self._trows.view(self.world, self.capacity, -1).unbind(0)) if self.is_learner else None
+                dist.gather(local, parts, dst=self.learner)
+
     def _terminal_rows(self, te, tr):
         """Terminal rows of the envs that finished this step ([G*E, D, W], zero elsewhere) on the
-        ranks that receive; None elsewhere.  te / tr: gathered flags (receiving ranks)."""
+        ranks that receive; None elsewhere.  te / tr: gathered flags (receiving ranks).  Fixed
+        sizes and device-side indices only: nothing here waits for the device."""
         G, E, D, W = self.world, self.count, self.sim.drones_per_env, self.sim.obs_width
+        C = self.capacity
         ldone = (self._local("terminated", torch.uint8, (E,)) | self._local("truncated", torch.uint8, (E,))).bool()
         lrows = self._local("terminal_obs", torch.float32, (E, D * W))
-        done_all = (te | tr).bool().reshape(G, E) if self.receives else None
-        out = torch.zeros((G * E, D, W), dtype=torch.float32, device=self.device) if self.receives else None
-        if self.mode == "all_gather" or not self._coll:
-            counts = done_all.sum(1).tolist()             # host sync: sizes the exchange
-            kmax = max(counts)
-            if kmax == 0:
-                return out
-            buf = torch.zeros((kmax, D * W), dtype=torch.float32, device=self.device)
-            k = counts[self.rank]
-            if k:
-                buf[:k] = lrows[ldone]
-            if self._coll:
-                rows = torch.empty((G * kmax, D * W), dtype=torch.float32, device=self.device)
-                if self._gloo:
-                    host = [torch.empty((kmax, D * W), dtype=torch.float32) for _ in range(G)]
-                    dist.all_gather(host, buf.cpu())
-                    rows.copy_(torch.cat(host))
-                else:
-                    dist.all_gather_into_tensor(rows, buf)
-            else:
-                rows = buf
-            # row j of rank r's block -> global env r*E + (its j-th finished env)
-            within = done_all.to(torch.int64).cumsum(1) - 1
-            src = (torch.arange(G, device=self.device)[:, None] * kmax + within)[done_all]
-            out.view(G * E, D * W)[done_all.reshape(-1)] = rows[src]
-            self.terminal_bytes += G * kmax * D * W * 4
-            return out
-        # "gather": the largest per-rank count by one all_reduce(MAX) of a single int, then one
-        # dist.gather of [kmax, D*W] blocks to the learner (collectives only: no point-to-point
-        # pairs to set up; every rank pads its block to the common count)
-        k = int(ldone.sum().item())                       # host sync: this rank's count
-        kt = torch.tensor([k], dtype=torch.int64, device="cpu" if self._gloo else self.device)
-        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
-        kmax = int(kt.item())
-        if kmax == 0:
-            return out
-        buf = torch.zeros((kmax, D * W), dtype=torch.float32, device=self.device)
-        if k:
-            buf[:k] = lrows[ldone]
-        if self._gloo:
-            host = [torch.empty((kmax, D * W), dtype=torch.float32) for _ in range(G)] if self.is_learner else None
-            dist.gather(buf.cpu(), host, dst=self.learner)
-            rows = torch.cat(host).to(self.device) if self.is_learner else None
-        else:
-            rows = torch.empty((G * kmax, D * W), dtype=torch.float32, device=self.device) if self.is_learner else None
-            dist.gather(buf, list(rows.view(G, kmax, D * W).unbind(0)) if self.is_learner else None, dst=self.learner)
-        if not self.is_learner:
+        # compaction: the j-th finished env's row -> block row j; the others -> the scratch row C
+        j = torch.cumsum(ldone.to(torch.int64), 0) - 1
+        dst = torch.where(ldone & (j < C), j, torch.full_like(j, C))
+        self._tblock.index_copy_(0, dst, lrows)
+        self._exchange_rows()
+        self.terminal_bytes += G * C * D * W * 4
+        if not self.receives:
             return None
-        within = done_all.to(torch.int64).cumsum(1) - 1
-        src = (torch.arange(G, device=self.device)[:, None] * kmax + within)[done_all]
-        out.view(G * E, D * W)[done_all.reshape(-1)] = rows[src]
-        self.terminal_bytes += G * kmax * D * W * 4
-        return out
+        done_all = (te | tr).bool().reshape(G, E)
+        within = torch.cumsum(done_all.to(torch.int64), 1) - 1
+        src = torch.arange(G, device=self.device)[:, None] * C + within.clamp(0, C - 1)
+        keep = done_all & (within < C)
+        self._overflow |= (done_all & (within >= C)).any()
+        rows = self._trows.index_select(0, src.reshape(-1))
+        out = torch.where(keep.reshape(-1, 1), rows, torch.zeros((), dtype=rows.dtype, device=self.device))
+        return out.view(G * E, D, W)
 
     def _views(self):
         """The learner's global batch, reassembled from the gathered packs (rank order)."""

@@ -49,7 +49,7 @@ def physics_flags(physics=Physics.DYN, aero=()):
     §8 f3): default damping, world-frame angular velocity, exponential-map orientation, and the
     collision cylinder's contact with the ground plane (``plane.urdf``, BaseAviary.py:484) and,
     in envs of several drones, with the env's other drones (every drone is a colliding body,
-    :486-491; envs of more than 64 drones skip it with a warning).  ``aero`` adds terms by name
+    :486-491; envs of more than 64 drones raise NotImplementedError unless ``no_drone_contact``).  ``aero`` adds terms by name
     (``gnd``, ``drag``, ``dw``, ``geom``, ``bullet``, ``no_plane``, ``no_drone_contact``), e.g.
     the aero terms on the DYN integrator (BASELINE config 3), ``no_plane`` for the reference's
     commented-out plane collision filter (:500-503), or ``no_drone_contact``.
@@ -138,8 +138,11 @@ class BatchedAviarySim:
         cfg.physics_flags = physics_flags(physics, aero)
         if cfg.physics_flags & _lib.GPD_F_BULLET and self.drones_per_env > 64 \
                 and not cfg.physics_flags & _lib.GPD_F_NO_DRONE_CONTACT:
-            _warn_once("pyb_wide", f"{Physics(physics)}: envs of more than 64 drones skip the drone <-> "
-                       "drone contact (the ground-plane contact applies)")
+            # a physics term is never dropped silently: the multi-wave kernels do not restate it
+            raise NotImplementedError(
+                f"{Physics(physics)} with {self.drones_per_env} drones per env: the drone <-> drone contact is "
+                "implemented for envs of up to 64 drones; pass aero=('no_drone_contact',) to run larger "
+                "PYB* envs without it")
         cfg.precision = _lib.GPD_F32 if precision == "f32" else _lib.GPD_F64
         cfg.autoreset = 1 if autoreset else 0
         cfg.episode_len_sec = float(episode_len_sec)

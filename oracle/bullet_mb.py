@@ -44,8 +44,8 @@ Bullet's multibody contact constraints solved by projected Gauss-Seidel inside
 ``btMultiBodyConstraintSolver`` between the velocity update and ``integrateTransforms``.  The
 contact set is this restatement's own (see ``plane_contact``).  Drone <-> drone collisions
 (cylinder vs cylinder, MultiHoverAviary's drones, ``:486-491``) are restated as ``drone_contact``:
-one contact per pair from the margin-shrunk cores' closest points, solved with the same rows
-between two moving bodies before the plane solve.  Bit-level rounding of Bullet's own
+one contact per pair (every pair in contact, no cap) from the margin-shrunk cores' closest points
+(FISTA-accelerated alternating projection from B's centre), solved with the same rows between two moving bodies before the plane solve.  Bit-level rounding of Bullet's own
 operation order (the world <-> base round trips of the link forces, the 6x6 inverse of the
 articulated inertia) is not reproduced either; the restatement is exact in exact arithmetic.
 
@@ -303,12 +303,32 @@ def plane_contact(pos, rot_bw, vel_w, omega_w, m, inertia, dt, radius, half_heig
 # MultiHoverAviary's drones are colliding Bullet bodies (BaseAviary.py:486-491, stepped together
 # by :369-370).  Bullet finds a cylinder pair's contact with GJK / EPA and keeps it in a persistent
 # manifold; this restatement's own deterministic contact set (parity unpinned, like the plane's):
-# one point per pair per step from the closest points of the two cylinders' margin-shrunk cores.
+# one point per pair per step from the closest points of the two cylinders' margin-shrunk cores,
+# found by a fixed number of FISTA-accelerated alternating-projection rounds from B's centre.
+# (Continuing a pair from its previous substep's point, as Bullet's persistent manifold does with
+# its points, was measured and rejected: on flat faces every point of the overlap is a fixed point
+# of the projections, so the single contact point drifts with the bodies and tips a drone resting
+# on another one over - DESIGN.md §2.3.)
 FRICTION_DD = 0.5 * 0.5     # drone x drone combined friction (btCollisionObject default 0.5 each)
-PAIR_ROUNDS = 16            # alternating-projection rounds of the pair's closest points (at most)
+PAIR_COLD = 8               # accelerated alternating-projection rounds from B's centre
 CORE_MARGINS = (0.001, 0.003, 0.006, 0.011)   # core shrink per level (the first = the URDF margin)
 CORE_SEP = 1e-4             # core distance below which a level has no well-conditioned normal
+SAT_SLACK = 1e-9            # the broadphase's separating-axis reject keeps this much against rounding
 SIMDSQRT12 = 0.7071067811865475244008443621048490
+
+
+def fista_momentum(k):
+    """FISTA's momentum weights beta_0..beta_{k-1}: t_0 = 1, t_{i+1} = (1 + sqrt(1 + 4 t_i^2)) / 2,
+    beta_i = (t_i - 1) / t_{i+1} (beta_0 = 0)."""
+    out, t = [], 1.0
+    for _ in range(k):
+        tn = (1.0 + math.sqrt(1.0 + 4.0 * t * t)) / 2.0
+        out.append((t - 1.0) / tn)
+        t = tn
+    return tuple(out)
+
+
+PAIR_BETA = fista_momentum(PAIR_COLD)
 
 
 def plane_space(n):
@@ -344,34 +364,71 @@ def cyl_extent(u, a, radius, half_height):
     return half_height * abs(ua) + radius * math.sqrt(max(0.0, 1.0 - ua * ua))
 
 
+def pair_near(ci, ai, cj, aj, radius, half_height, brk):
+    """Broadphase of the pair (i, j): bounding spheres within the breaking threshold, and no
+    separating axis among the two cylinder axes and the centre line with a separation above it
+    (+ SAT_SLACK).  Separation along any axis bounds the distance from below, so the reject
+    never drops a pair whose distance is below the threshold."""
+    bs = math.sqrt(radius * radius + half_height * half_height)
+    reach = 2.0 * bs + brk
+    e = ci - cj
+    e2 = float(e @ e)
+    if not e2 < reach * reach:
+        return False
+    lim = brk + SAT_SLACK
+    ab = float(ai @ aj)
+    tilt = half_height * abs(ab) + radius * math.sqrt(max(0.0, 1.0 - ab * ab))
+    if abs(float(e @ ai)) - (half_height + tilt) > lim:
+        return False
+    if abs(float(e @ aj)) - (half_height + tilt) > lim:
+        return False
+    if e2 > 0.0:
+        ln = math.sqrt(e2)
+        ua, ub = float(e @ ai) / ln, float(e @ aj) / ln
+        ext = cyl_extent_cos(ua, radius, half_height) + cyl_extent_cos(ub, radius, half_height)
+        if ln - ext > lim:
+            return False
+    return True
+
+
+def cyl_extent_cos(ua, radius, half_height):
+    """cyl_extent for a direction whose cosine with the axis is ua."""
+    return half_height * abs(ua) + radius * math.sqrt(max(0.0, 1.0 - ua * ua))
+
+
 def pair_geometry(ca, aa, cb, ab, radius, half_height):
     """One contact of cylinders A and B: (normal on B pointing to A, point on B, distance;
-    negative = penetration).  Bullet's margin scheme: the closest points of the CORE cylinders
-    (radius and half-height shrunk by a margin m) give the normal and the distance
-    core_distance - 2 m, the point on B's surface is B's core point + m n.  Core closest points by
-    PAIR_ROUNDS rounds of alternating projection from B's centre (in B-centred coordinates);
-    a level whose cores come within CORE_SEP of each other (overlapping or nearly so: no
-    well-conditioned normal) passes to the next, thicker margin (CORE_MARGINS: penetrations up to
-    ~2 cm).  Deeper overlaps: the axis of least overlap among the centre line and the two
-    cylinder axes, at the point the last projections reached (Bullet runs EPA here)."""
+    negative = penetration).  Bullet's margin scheme:
+    the closest points of the CORE cylinders (radius and half-height shrunk by a margin m) give
+    the normal and the distance core_distance - 2 m; the point on B's surface is B's core point +
+    m n.  Core points by PAIR_COLD rounds of alternating projection in B-centred coordinates from
+    B's centre with FISTA momentum (y' = P_B(P_A(z)), z = y' + beta (y' - y)) - a fixed count, no
+    convergence test, so the result is a continuous function of the poses (16 plain rounds, round
+    3's choice, left up to 2 mm of distance error on tilted face-to-face pairs where the plain
+    rounds creep at cos^2 of the faces' angle; 8 accelerated ones reach the same accuracy, 16 ten
+    times better) - then the point of A's core closest to B's.  A level whose cores come within CORE_SEP of each
+    other (overlapping or nearly so: no well-conditioned normal) passes to the next, thicker
+    margin (CORE_MARGINS: penetrations up to ~2 cm).  Deeper overlaps: the axis of least overlap
+    among the centre line and the two cylinder axes, at the point the last level reached (Bullet
+    runs EPA here)."""
     cl = ca - cb
     zero = np.zeros(3)
+    y = zero
     for mg in CORE_MARGINS:
         r, h = radius - mg, half_height - mg
-        xb = zero.copy()
-        for _ in range(PAIR_ROUNDS):
-            xo = xb
-            pa = cyl_project(cl, aa, r, h, xb)
-            xb = cyl_project(zero, ab, r, h, pa)
-            mv = xb - xo
-            if float(mv @ mv) <= 1e-24:                     # B's point moved <= 1e-12 m: converged
-                break
-        dv = pa - xb
+        y = zero.copy()
+        z = zero.copy()
+        for beta in PAIR_BETA:
+            yn = cyl_project(zero, ab, r, h, cyl_project(cl, aa, r, h, z))
+            z = yn + beta * (yn - y)
+            y = yn
+        pa = cyl_project(cl, aa, r, h, y)
+        dv = pa - y
         d2 = float(dv @ dv)
         if d2 > CORE_SEP * CORE_SEP:
             dc = math.sqrt(d2)
             n = dv / dc
-            return n, cb + (xb + n * mg), dc - 2.0 * mg
+            return n, cb + (y + n * mg), dc - 2.0 * mg
     cands = []
     c2 = float(cl @ cl)
     if c2 > 1e-24:
@@ -383,27 +440,24 @@ def pair_geometry(ca, aa, cb, ab, radius, half_height):
         ov = cyl_extent(u, aa, radius, half_height) + cyl_extent(u, ab, radius, half_height) - float(u @ cl)
         if best is None or ov < best_ov:
             best, best_ov = u, ov
-    return best, cb + xb, -best_ov
+    return best, cb + y, -best_ov
 
 
 def drone_contacts(pos, rot_bw, radius, half_height, z_offset):
-    """The env's contacts in solve order: pairs (i, j), i < j, lexicographic, whose cylinders'
-    bounding spheres come within the breaking threshold and whose distance is below it; at most
-    D of them (an env has D solver slots; more simultaneous contacts are dropped)."""
+    """The env's contacts in solve order: pairs (i, j), i < j, lexicographic, that pass the
+    broadphase (``pair_near``) and whose distance is below the breaking threshold - every such
+    pair, however many (up to D (D - 1) / 2; round 3 kept at most D)."""
     D = pos.shape[0]
     brk = breaking_threshold(radius, half_height)
-    bs = math.sqrt(radius * radius + half_height * half_height)
-    reach = 2.0 * bs + brk
     axes = [rot_bw[i][:, 2].copy() for i in range(D)]
     cent = [pos[i] + axes[i] * z_offset for i in range(D)]
     out = []
     for i in range(D):
         for j in range(i + 1, D):
-            dc = cent[i] - cent[j]
-            if not float(dc @ dc) < reach * reach:
+            if not pair_near(cent[i], axes[i], cent[j], axes[j], radius, half_height, brk):
                 continue
             n, pb, dist = pair_geometry(cent[i], axes[i], cent[j], axes[j], radius, half_height)
-            if dist < brk and len(out) < D:
+            if dist < brk:
                 out.append((i, j, n, pb, dist))
     return out
 
@@ -411,7 +465,11 @@ def drone_contacts(pos, rot_bw, radius, half_height, z_offset):
 def drone_contact(pos, rot_bw, vel_w, omega_w, m, inertia, dt, radius, half_height, z_offset):
     """Drone <-> drone contact of one env for one ``stepSimulation``: the rows of
     ``plane_contact`` between two moving bodies, solved before it (between the unconstrained
-    velocity update and the ground-plane solve; Bullet solves both in one island).
+    velocity update and the ground-plane solve).  Known deviation: Bullet solves the pair and
+    plane rows of an island in one Gauss-Seidel loop; here the pair solve runs first and each
+    drone's plane solve after it, so a drone resting on another that rests on the plane settles
+    over substeps rather than within one solve (tests/test_oracle_drone_contact.py pins the
+    stacked-on-the-plane case).
 
     ``pos`` [D, 3] start-of-step positions, ``rot_bw`` [D, 3, 3] body -> world, ``vel_w`` /
     ``omega_w`` [D, 3] after the unconstrained update.  Per contact (A = i, B = j, normal n from B

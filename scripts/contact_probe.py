@@ -27,7 +27,7 @@ STAG = [[0.15 * math.cos(2 * math.pi * i / 8), 0.15 * math.sin(2 * math.pi * i /
 NODC = ("no_drone_contact",) if os.environ.get("GPD_PROBE_NODC") == "1" else ()
 
 
-def run(case, E=4096, warm=60, steps=200):
+def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.environ.get("PROBE_STEPS", 200))):
     aero = ("no_plane",) if case == "noplane" else ()
     if case in ("multi", "multifly"):    # bench.py's PYB_GND_DRAG_DW row: 512 MultiHover envs x 8 drones, staggered
         E, D = 512, 8

@@ -110,14 +110,15 @@ class _PackedOracleShard:
             self._put(name, getattr(self.o, name))
 
 
-def _handoff_worker(rank, world, port, E, T, q, mode, force, ack):
+def _handoff_worker(rank, world, port, E, T, q, mode, force, ack, cap=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from gym_pybullet_drones_routing_amd.shard import LearnerHandoff, env_shard
         _, count = env_shard(E, rank, world)
-        h = LearnerHandoff(_PackedOracleShard(count, task="hover"), E, mode=mode, force_collectives=force)
+        h = LearnerHandoff(_PackedOracleShard(count, task="hover"), E, mode=mode, force_collectives=force,
+                           terminal_capacity=cap)
         rng = np.random.default_rng(1)
         acts = rng.uniform(-1, 1, (T, E, 1, 4)).astype(np.float32)
         acts[:, :2] *= 0.05                          # long-lived envs beside ones that end early
@@ -135,31 +136,34 @@ def _handoff_worker(rank, world, port, E, T, q, mode, force, ack):
                 outs.append(tuple(x.numpy().copy() for x in r))
                 prev = (r, outs[-1])
         if rank == 0:
-            q.put((outs, h.bytes_per_step(), h.stats()))
+            q.put((outs, h.bytes_per_step(), h.stats(), h.overflowed()))
             ack.wait(120)          # stay alive until the parent has read the whole message
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mode,force", [(2, "all_gather", False), (2, "gather", False),
-                                              (1, "all_gather", True), (1, "gather", True),
-                                              (1, "all_gather", False)])
-def test_learner_handoff_gloo_matches_one_process(world, mode, force):
+@pytest.mark.parametrize("world,mode,force,cap", [(2, "all_gather", False, None), (2, "gather", False, None),
+                                                  (1, "all_gather", True, None), (1, "gather", True, None),
+                                                  (1, "all_gather", False, None), (2, "gather", False, 1),
+                                                  (2, "all_gather", False, 2)])
+def test_learner_handoff_gloo_matches_one_process(world, mode, force, cap):
     """Rank-0 learner scatters actions, shards step, the output-pack prefixes are gathered (or
-    all-gathered) and the finished envs' terminal rows follow: the learner's batch (incl.
-    terminal rows after auto-resets) equals one process stepping all envs.  World size 1 with
-    and without forced collectives (the one-rank shortcut must still return fresh tensors)."""
+    all-gathered) and the finished envs' terminal rows follow in fixed-size compacted blocks: the
+    learner's batch (incl. terminal rows after auto-resets) equals one process stepping all envs.
+    World size 1 with and without forced collectives (the one-rank shortcut must still return
+    fresh tensors).  With a terminal_capacity below the shard size, the first `cap` finished envs
+    of a rank per step are delivered and the overflow flag says whether any were not."""
     from oracle.c_oracle import COracle
     E, T = 8, 40
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ack = ctx.Event()
     port = _free_port()
-    procs = [ctx.Process(target=_handoff_worker, args=(r, world, port, E, T, q, mode, force, ack))
+    procs = [ctx.Process(target=_handoff_worker, args=(r, world, port, E, T, q, mode, force, ack, cap))
              for r in range(world)]
     for p in procs:
         p.start()
-    outs, (act_bytes, pack_bytes), stats = q.get(timeout=300)
+    outs, (act_bytes, pack_bytes), stats, overflowed = q.get(timeout=300)
     ack.set()
     for p in procs:
         p.join(timeout=120)
@@ -170,7 +174,9 @@ def test_learner_handoff_gloo_matches_one_process(world, mode, force):
     rng = np.random.default_rng(1)
     acts = rng.uniform(-1, 1, (T, E, 1, 4)).astype(np.float32)
     acts[:, :2] *= 0.05
-    n_done, row_bytes = 0, 0
+    n_done, any_over = 0, False
+    per = E // world
+    C = per if cap is None else cap
     for t in range(T):
         o, r, te, tr = ref.step(acts[t])
         obs, rew, gte, gtr, tobs = outs[t + 1]
@@ -180,16 +186,18 @@ def test_learner_handoff_gloo_matches_one_process(world, mode, force):
         np.testing.assert_array_equal(gtr.astype(bool), tr)
         done = te | tr
         n_done += int(done.sum())
-        np.testing.assert_array_equal(tobs[done], ref.terminal_obs[done])
-        assert not tobs[~done].any()                  # only finished envs' rows are sent
-        row_bytes += int(done.sum()) * 72 * 4
+        # the first C finished envs of each rank arrive; with the default capacity, all of them
+        first = np.zeros_like(done)
+        for rk in range(world):
+            idx = np.flatnonzero(done[rk * per:(rk + 1) * per])
+            first[rk * per + idx[:C]] = True
+            any_over |= len(idx) > C
+        np.testing.assert_array_equal(tobs[first], ref.terminal_obs[first])
+        assert not tobs[~first].any()                 # only (delivered) finished envs' rows
     assert n_done > 0
-    # terminal bytes: exactly the finished rows with one rank; with several, every rank's block is
-    # padded to the step's largest count
-    if world == 1:
-        assert stats["terminal_bytes_avg"] * T == row_bytes
-    else:
-        assert row_bytes <= stats["terminal_bytes_avg"] * T <= world * row_bytes
+    assert overflowed == any_over and (cap is not None or not any_over)
+    # terminal bytes: a fixed block of C rows per rank and step (no host sync sizes it)
+    assert stats["terminal_bytes_avg"] == world * C * 72 * 4
 
 
 def _prefix_bytes(e):

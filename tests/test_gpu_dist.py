@@ -29,7 +29,7 @@ def _actions(E, T, D, A, seed):
     return acts
 
 
-def _worker(rank, world, port, kw, E, T, q, backend="gloo", mode="all_gather", ack=None):
+def _worker(rank, world, port, kw, E, T, q, backend="gloo", mode="all_gather", ack=None, sync_check=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     extra = {"device_id": torch.device("cuda:0")} if backend == "nccl" else {}
@@ -44,12 +44,20 @@ def _worker(rank, world, port, kw, E, T, q, backend="gloo", mode="all_gather", a
         if backend == "nccl":
             assert dist.get_backend() == "nccl"
         acts = _actions(E, T, sim.drones_per_env, sim.act_width, 5)
+        acts_dev = torch.from_numpy(acts).cuda()
         o0 = h.reset()
         outs = [o0.cpu().numpy() if rank == 0 else None]
+        keep = []
         for t in range(T):
-            r = h.step(torch.from_numpy(acts[t]).cuda() if rank == 0 else None)
+            if sync_check and t == 2:
+                torch.cuda.synchronize()
+                torch.cuda.set_sync_debug_mode("error")   # steady state: no host synchronisation at all
+            r = h.step(acts_dev[t] if rank == 0 else None)
             if rank == 0:
-                outs.append(tuple(x.cpu().numpy() for x in r))
+                keep.append(r)
+        torch.cuda.set_sync_debug_mode("default")
+        for r in keep:
+            outs.append(tuple(x.cpu().numpy() for x in r))
         sim.close()
         if rank == 0:
             q.put(outs)
@@ -83,12 +91,12 @@ def _collect(q, procs, limit=150, ack=None):
     return outs
 
 
-def _run(kw, E, T, world, backend, mode):
+def _run(kw, E, T, world, backend, mode, sync_check=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ack = ctx.Event()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, kw, E, T, q, backend, mode, ack))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kw, E, T, q, backend, mode, ack, sync_check))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -135,8 +143,10 @@ def test_handoff_rccl_one_rank(mode):
     """The RCCL code path of the hand-off (backend "nccl" = RCCL on ROCm) on the one-GPU box:
     a one-rank group with the collectives forced on, so that dist.scatter, the prefix
     gather / all_gather_into_tensor and the terminal-row all-gather of uint8 / float32 device
-    tensors really execute on RCCL.  Bit-identical to one sim stepping the same envs."""
+    tensors really execute on RCCL.  Bit-identical to one sim stepping the same envs.  Steady-state
+    steps run under torch.cuda.set_sync_debug_mode("error"): the hand-off never waits for the
+    device (fixed-size compacted terminal blocks, device-side indices)."""
     kw = dict(task="hover")
     E, T = 64, 260
-    outs = _run(kw, E, T, 1, "nccl", mode)
+    outs = _run(kw, E, T, 1, "nccl", mode, sync_check=True)
     _check_against_one_sim(outs, kw, E, T)

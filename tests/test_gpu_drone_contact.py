@@ -5,8 +5,11 @@ p.stepSimulation at :369-370).  The restatement (oracle/bullet_mb.py drone_conta
 drone_contact) is this repository's own contact set and solver order: parity unpinned against
 pybullet, like the ground-plane contact.  These tests pin the HIP path to the oracle:
   * resynced substeps (integrate kernel, run-time flags) over head-on, glancing, stacked, tilted,
-    resting-overlap and far-apart pairs, and a four-drone pile-up: f64 max <= 1e-10 per substep;
-    f32 median <= 1e-5;
+    resting-overlap and far-apart pairs, a four-drone pile-up, three-drone envs (64 % 3 != 0: a
+    block's last lanes idle), a four-drone pile with six simultaneous contacts (more than the
+    env's D) and eight-drone 2 x 2 x 2 stacks in 64-drone blocks (pairs past a block's first 64
+    go through the row store, several contacts per env through the LDS rounds): f64 max <= 1e-10
+    per substep; f32 median <= 1e-6, max <= 1e-3;
   * resynced control steps through the Physics.PYB flag-set step kernel (MultiHover layout);
   * physics: the pair's linear momentum is unchanged by the contact, the head-on pair stops
     short of interpenetration, and ``no_drone_contact`` lets the drones pass through each other.
@@ -59,21 +62,77 @@ def _pileup():
     return raw
 
 
+def _triples():
+    """Three-drone envs (D = 3): a head-on pair beside a free drone, and a three-way collision."""
+    raw = np.zeros((6, 20))
+    raw[0:3, 0:3] = [[0, 0, 1.0], [0.2, 0, 1.0], [0.1, 0.5, 1.0]]
+    raw[0:3, 7:10] = [[1, 0, 0], [-1, 0, 0], [0, 0, 0]]
+    for k, a in enumerate(np.arange(3) * 2 * np.pi / 3):
+        raw[3 + k, 0:3] = [0.075 * np.cos(a), 0.075 * np.sin(a), 1.0 + 0.003 * k]
+        raw[3 + k, 7:10] = [-0.5 * np.cos(a), -0.5 * np.sin(a), 0]
+    raw[:, 6] = 1.0
+    raw[:, 16:20] = HOVER
+    return raw
+
+
+def _pile6():
+    """Four drones with six contacts: a touching triangle and a fourth drone falling onto all three."""
+    from oracle.params import derived
+    hh = derived("cf2x")["collision_h"] / 2
+    raw = np.zeros((4, 20))
+    tri = [[0, 0, 1.0], [0.1195, 0, 1.0], [0.05975, 0.1035, 1.0]]
+    raw[0:3, 0:3] = tri
+    raw[3, 0:3] = np.mean(tri, axis=0) + [0, 0, 2 * hh - 0.0005]
+    raw[3, 7:10] = [0, 0, -0.6]
+    raw[0:3, 7:10] = [[-0.1, -0.05, 0], [0.1, -0.05, 0], [0, 0.1, 0.05]]
+    raw[:, 6] = 1.0
+    raw[:, 16:20] = HOVER
+    return raw
+
+
+def _cube(rng):
+    """Eight drones as a 2 x 2 x 2 stack squeezed together (12+ contacts in one env)."""
+    from oracle.params import derived
+    hh = derived("cf2x")["collision_h"] / 2
+    raw = np.zeros((8, 20))
+    for k in range(8):
+        raw[k, 0:3] = [0.1195 * (k & 1), 0.1195 * ((k >> 1) & 1), 1.0 + (2 * hh - 0.0005) * (k >> 2)]
+        raw[k, 7:10] = -0.3 * (raw[k, 0:3] - [0.06, 0.06, 1.0 + hh]) + rng.uniform(-0.05, 0.05, 3)
+        raw[k, 10:13] = rng.uniform(-1, 1, 3)
+        raw[k, 13:16] = raw[k, 10:13]
+    raw[:, 6] = 1.0
+    raw[:, 16:20] = HOVER
+    return raw
+
+
 def _pyb():
     from gym_pybullet_drones_routing_amd.enums import Physics
     return Physics.PYB
 
 
+def _cases(D):
+    rng = np.random.default_rng(D)
+    if D == 2:
+        return _scenarios(), None
+    if D == 3:
+        return _triples(), None
+    if D == 4:
+        return np.concatenate([_pileup(), _pileup()[::-1].copy(), _pile6()]), None
+    # D = 8: eight stacks in one 64-drone block (224 pairs: three row-store chunks)
+    return np.concatenate([_cube(rng) for _ in range(8)]), {"drones_per_block": 64}
+
+
 @pytest.mark.parametrize("prec", ["f64", "f32"])
-@pytest.mark.parametrize("D", [2, 4])
+@pytest.mark.parametrize("D", [2, 3, 4, 8])
 def test_drone_contact_resynced(prec, D):
-    raw0 = _scenarios() if D == 2 else np.concatenate([_pileup(), _pileup()[::-1].copy()])
+    raw0, tuning = _cases(D)
     n = raw0.shape[0]
     T = 40
     rpms = np.full((T, n, 4), HOVER)
     env = RefAviary(num_drones=n, task="none", integrator="bullet", aero=("no_plane",), drones_per_env=D)
     env.set_raw_state(raw0)
-    sim = _sim(n_envs=n // D, drones_per_env=D, task="none", precision=prec, physics=_pyb(), aero=("no_plane",))
+    sim = _sim(n_envs=n // D, drones_per_env=D, task="none", precision=prec, physics=_pyb(), aero=("no_plane",),
+               tuning=tuning)
     err = resynced_substep_errors(sim, env, rpms)
     sep = np.linalg.norm(env._b_pos[0] - env._b_pos[1])
     print(f"\n[parity] drone contact D={D} {prec}: max {err.max():.3e} median {np.median(err):.3e} "
@@ -81,29 +140,43 @@ def test_drone_contact_resynced(prec, D):
     if prec == "f64":
         assert err.max() <= 1e-10
     else:
-        assert np.median(err) <= 1e-5 and err.max() <= 5e-2
+        assert np.median(err) <= 1e-6 and err.max() <= 1e-3
     sim.close()
 
 
-def test_drone_contact_step_kernel_resynced():
-    """The Physics.PYB flag-set step kernel (MultiHoverAviary's default physics, D = 2)."""
+def test_drone_contact_counts_beyond_d():
+    """The six-contact pile and the eight-drone stacks really hold more simultaneous contacts than
+    their env's D (no slot cap in the oracle either)."""
+    from oracle.bullet_math import quat_to_mat
+    from oracle.bullet_mb import drone_contacts
+    from oracle.params import derived
+    p = derived("cf2x")
+    for raw, D in ((_pile6(), 4), (_cube(np.random.default_rng(8)), 8)):
+        rot = np.array([quat_to_mat(q) for q in raw[:, 3:7]])
+        cons = drone_contacts(raw[:, 0:3], rot, p["collision_r"], p["collision_h"] / 2, p["collision_z_offset"])
+        assert len(cons) > D
+
+
+@pytest.mark.parametrize("D", [2, 3, 4])
+def test_drone_contact_step_kernel_resynced(D):
+    """The Physics.PYB flag-set step kernel (MultiHoverAviary's default physics; the parked call)."""
     from gym_pybullet_drones_routing_amd.enums import ActionType
-    raw0 = _scenarios()
+    raw0 = {2: _scenarios, 3: _triples, 4: _pile6}[D]()
     n = raw0.shape[0]
-    env = RefAviary(num_drones=n, task="none", integrator="bullet", act="rpm", drones_per_env=2)
+    env = RefAviary(num_drones=n, task="none", integrator="bullet", act="rpm", drones_per_env=D)
     env.set_raw_state(raw0)
-    sim = _sim(n_envs=n // 2, drones_per_env=2, task="none", precision="f64", physics=_pyb(), act=ActionType.RPM)
+    sim = _sim(n_envs=n // D, drones_per_env=D, task="none", precision="f64", physics=_pyb(), act=ActionType.RPM)
     sim.reset()
     rng = np.random.default_rng(5)
     errs = []
     for t in range(12):
         a = rng.uniform(-0.2, 0.2, (n, 4)).astype(np.float32)
         sim.set_raw_state(oracle_raw(env))
-        sim.step(torch.from_numpy(a.reshape(n // 2, 2, 4)).cuda())
+        sim.step(torch.from_numpy(a.reshape(n // D, D, 4)).cuda())
         env.step(a)
         errs.append(state_rel_err(sim.raw_state().cpu().numpy()[None, :, :16], oracle_raw(env)[None, :, :16])[0])
     err = np.array(errs)
-    print(f"\n[parity] drone contact, PYB step kernel: max {err.max():.3e}")
+    print(f"\n[parity] drone contact, PYB step kernel D={D}: max {err.max():.3e}")
     assert err.max() <= 1e-10
     sim.close()
 

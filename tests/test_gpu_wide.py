@@ -110,6 +110,14 @@ def test_wide_one_d_pid_matches_numpy_oracle():
     sim.close()
 
 
+def test_wide_pyb_requires_opt_out_of_drone_contact():
+    """Envs of more than 64 drones run the multi-wave kernels, which do not restate the drone <->
+    drone contact: under Physics.PYB* that is an error, not a silently dropped physics term."""
+    from gym_pybullet_drones_routing_amd.enums import Physics
+    with pytest.raises(NotImplementedError, match="no_drone_contact"):
+        _sim(n_envs=1, drones_per_env=65, task="multihover", physics=Physics.PYB)
+
+
 def test_wide_pyb_contact_resynced():
     """Physics.PYB in an env of 80 drones crashing into the plane: the waves take turns in the
     contact solve's LDS rows; resynced per-substep parity as in test_gpu_bullet.py."""
@@ -122,7 +130,9 @@ def test_wide_pyb_contact_resynced():
     rpms = _rpms(rng, T, D, scale=0.5) * 0.6
     env = RefAviary(num_drones=D, task="none", integrator="bullet")
     env.set_raw_state(raw0)
-    sim = _sim(n_envs=1, drones_per_env=D, task="none", physics=Physics.PYB)
+    # the oracle env steps its 80 drones independently (drones_per_env 1): no drone <-> drone
+    # contact on either side (the multi-wave kernels do not restate it)
+    sim = _sim(n_envs=1, drones_per_env=D, task="none", physics=Physics.PYB, aero=("no_drone_contact",))
     err = resynced_substep_errors(sim, env, rpms)
     print(f"\n[wide] PYB contact resynced D=80: max {err.max():.3e}")
     assert (oracle_raw(env)[:, 2] < 0.02).sum() > D // 4

@@ -4,7 +4,8 @@ import math
 
 import numpy as np
 
-from oracle.bullet_mb import (LINEAR_SLOP, breaking_threshold, drone_contact, drone_contacts, pair_geometry, plane_space)
+from oracle.bullet_mb import (CORE_MARGINS, LINEAR_SLOP, PAIR_BETA, PAIR_COLD, breaking_threshold, cyl_project, drone_contact,
+                              drone_contacts, pair_geometry, pair_near, plane_space)
 from oracle.bullet_math import quat_from_euler, quat_to_mat
 from oracle.params import derived
 
@@ -85,19 +86,119 @@ def test_far_and_separating_pairs_unchanged():
     assert np.array_equal(v, vel)
 
 
-def test_contact_order_and_slot_cap():
+def _rot(rpys):
+    return np.array([quat_to_mat(quat_from_euler(np.array(r, dtype=np.float64))) for r in rpys])
+
+
+def test_contact_order_and_no_cap():
     # five drones stacked tightly: 4 adjacent contacts (+ none at two levels apart), in (i, j) order
     pos = np.array([[0, 0, 1.0 + 0.0245 * k] for k in range(5)])
     rot = np.array([np.eye(3)] * 5)
     cons = drone_contacts(pos, rot, R_, HH, ZO)
     assert [(c[0], c[1]) for c in cons] == [(0, 1), (1, 2), (2, 3), (3, 4)]
-    # a three-drone cluster all within the threshold: 3 pairs fit the 3 slots; four mutually
-    # touching drones (6 pairs) keep the first 4
-    tri = np.array([[0, 0, 1.0], [0.12, 0, 1.0], [0.06, 0.1039, 1.0]])
-    assert len(drone_contacts(tri, rot[:3], R_, HH, ZO)) == 3
-    quad = np.array([[0, 0, 1.0], [0.0, 0, 1.0245], [0.0, 0, 1.049], [0.0, 0, 1.0735]])
-    quad[:, 0] += [0, 0.001, 0.002, 0.003]
+    # four drones, six contacts (more than the env's D): a touching triangle with a fourth drone
+    # resting on all three - every pair is kept
+    tri = [[0, 0, 1.0], [0.1195, 0, 1.0], [0.05975, 0.1035, 1.0]]
+    top = np.mean(tri, axis=0) + [0, 0, 2 * HH - 0.0005]
+    quad = np.array(tri + [top])
     cons = drone_contacts(quad, rot[:4], R_, HH, ZO)
-    assert len(cons) == 3 or len(cons) == 4
+    assert [(c[0], c[1]) for c in cons] == [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)]
+    # eight drones as a 2 x 2 x 2 stack: 12 face / side contacts plus the rims of the layers' diagonals
+    cube = np.array([[0.1195 * (k & 1), 0.1195 * ((k >> 1) & 1), 1.0 + (2 * HH - 0.0005) * (k >> 2)] for k in range(8)])
+    cons = drone_contacts(cube, np.array([np.eye(3)] * 8), R_, HH, ZO)
+    assert len(cons) >= 12 and all(c[4] < breaking_threshold(R_, HH) for c in cons)
     assert breaking_threshold(R_, HH) < 0.002
-    assert math.isfinite(cons[0][4])
+
+
+def test_six_contacts_in_a_four_drone_pile_conserve_momentum():
+    tri = [[0, 0, 1.0], [0.1195, 0, 1.0], [0.05975, 0.1035, 1.0]]
+    top = np.mean(tri, axis=0) + [0, 0, 2 * HH - 0.0005]
+    pos = np.array(tri + [top])
+    rng = np.random.default_rng(7)
+    vel = rng.uniform(-0.5, 0.5, (4, 3))
+    vel[3] = [0, 0, -0.8]
+    omg = rng.uniform(-1, 1, (4, 3))
+    v, w = _solve(pos, [(0, 0, 0)] * 4, vel, omg)
+    np.testing.assert_allclose(v.sum(0), vel.sum(0), atol=1e-12)
+    assert v[3, 2] > -0.8 + 0.1                 # the top drone is held up by the three below
+
+
+def test_broadphase_never_drops_a_contact():
+    """pair_near's separating-axis reject bounds the distance from below: every pair it rejects
+    is farther apart than the breaking threshold (random poses around contact range)."""
+    rng = np.random.default_rng(11)
+    brk = breaking_threshold(R_, HH)
+    rejected = 0
+    for _ in range(3000):
+        ci = np.zeros(3)
+        cj = rng.normal(size=3) * [0.08, 0.08, 0.03]
+        ai, aj = _rot([rng.uniform(-0.6, 0.6, 3), rng.uniform(-0.6, 0.6, 3)])[:, :, 2]
+        if pair_near(ci, ai, cj, aj, R_, HH, brk):
+            continue
+        rejected += 1
+        # the true distance by many plain alternating-projection rounds (monotone, from above)
+        y = np.zeros(3)
+        for _ in range(400):
+            y = cyl_project(np.zeros(3), aj, R_, HH, cyl_project(ci - cj, ai, R_, HH, y))
+        d = np.linalg.norm(cyl_project(ci - cj, ai, R_, HH, y) - y)
+        assert d > brk - 1e-6
+    assert rejected > 100
+
+
+def test_narrowphase_is_fixed_round_accelerated_projection():
+    """FISTA's momentum weights and the narrowphase's fixed round count: no convergence test, so
+    the result is a continuous function of the poses; and it reaches the accuracy of round 3's 16
+    plain rounds on a tilted face-to-face pair where those creep."""
+    assert len(PAIR_BETA) == PAIR_COLD and PAIR_BETA[0] == 0.0 and all(0 < b < 1 for b in PAIR_BETA[1:])
+    ca, cb = np.array([0.0, 0.0, 1.0]), np.array([0.121, 0.002, 1.001])
+    aa, ab = _rot([(0.1, 0.2, 0.0), (-0.15, 0.05, 0.3)])[:, :, 2]
+    n0, pb0, d0 = pair_geometry(ca, aa, cb, ab, R_, HH)
+    n1, pb1, d1 = pair_geometry(ca + 1e-12, aa, cb, ab, R_, HH)
+    assert abs(d1 - d0) < 1e-10 and np.abs(pb1 - pb0).max() < 1e-10
+    # accuracy against many plain rounds over random tilted pairs 1 mm+ apart: micrometre-level
+    # (on the contacts recorded from crashing 2- and 8-drone envs - scripts/dc_narrowphase_stats.py -
+    # the 8 accelerated rounds match round 3's 16 plain ones: p90 1.4e-4 vs 1.2e-4 m, DESIGN.md §2.3)
+    rng = np.random.default_rng(5)
+    mg = CORE_MARGINS[0]
+
+    def plain(ca, aa, ab, k):
+        y = np.zeros(3)
+        for _ in range(k):
+            y = cyl_project(np.zeros(3), ab, R_ - mg, HH - mg, cyl_project(ca, aa, R_ - mg, HH - mg, y))
+        return np.linalg.norm(cyl_project(ca, aa, R_ - mg, HH - mg, y) - y) - 2 * mg
+    e8, e16 = [], []
+    for _ in range(60):
+        ca = np.array([rng.uniform(-0.12, 0.12), rng.uniform(-0.12, 0.12), rng.uniform(0.028, 0.04)])
+        aa, ab = _rot([rng.uniform(-0.4, 0.4, 3), rng.uniform(-0.4, 0.4, 3)])[:, :, 2]
+        d_true = plain(ca, aa, ab, 4000)
+        if d_true < 1e-3:
+            continue
+        e8.append(pair_geometry(ca, aa, np.zeros(3), ab, R_, HH)[2] - d_true)
+        e16.append(plain(ca, aa, ab, 16) - d_true)
+    print(f"\n[narrowphase] distance error median / max: 8 FISTA {np.median(e8):.2e} / {max(e8):.2e} m, "
+          f"16 plain {np.median(e16):.2e} / {max(e16):.2e} m")
+    assert min(e8) > -1e-12 and np.median(e8) < 1e-6 and max(e8) <= max(e16) + 1e-3
+
+
+def test_stacked_on_the_plane_sequential_split():
+    """Known deviation: pair rows first, the plane rows after, instead of one
+    island solve.  A level drone dropped onto another resting on the plane: every substep the pair
+    solve hands the bottom drone part of the top one's downward velocity, the plane solve then
+    removes it from the bottom drone only, so the top one sinks into the bottom one until the ERP
+    push balances it - about 1 cm deep here, where Bullet's coupled solve would hold it on top.
+    Pinned: the bottom drone stays on the plane, the top one stays above its lower half and comes
+    to rest."""
+    from oracle.ref_aviary import RefAviary
+    env = RefAviary(num_drones=2, task="none", integrator="bullet", drones_per_env=2)
+    raw = np.zeros((2, 20))
+    raw[0, 0:3] = [0, 0, -ZO + HH - 1e-5]              # bottom drone on the plane
+    raw[1, 0:3] = [0.01, 0, raw[0, 2] + 2 * HH + 0.001]
+    raw[:, 6] = 1.0
+    raw[1, 9] = -0.3
+    env.set_raw_state(raw)
+    out = env.integrate(np.zeros((240, 2, 4)))
+    gap = out[:, 1, 2] - out[:, 0, 2]
+    print(f"\n[stack] gap min {gap.min():.4f} m (touching: {2 * HH:.4f}), end {gap[-1]:.4f}")
+    assert gap.min() > HH                               # never past the bottom drone's mid-plane
+    assert abs(out[-1, 0, 2] - raw[0, 2]) < 2e-3          # the bottom drone stays on the plane
+    assert np.abs(out[-1, :, 10:13]).max() < 0.1          # both (nearly) at rest after 1 s
