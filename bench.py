@@ -455,6 +455,9 @@ def other_configs(device, precision, act):
         ("512 MultiHoverAviary x 8 drones, Physics.PYB_GND_DRAG_DW (Bullet step, staggered init)",
          dict(n_envs=512, drones_per_env=8, task="multihover", act=ActionType.RPM, physics=Physics.PYB_GND_DRAG_DW,
               initial_xyzs=stag), 4),
+        ("2048 MultiHoverAviary x 2 drones, Physics.PYB (MultiHoverAviary's default, examples/learn.py "
+         "--multiagent's env; drone<->drone and plane contact)",
+         dict(n_envs=2048, drones_per_env=2, task="multihover", act=ActionType.RPM, physics=Physics.PYB), 4),
     ]
     out = []
     for name, kw, A in cases:
@@ -779,11 +782,16 @@ def run(args):
     if rp is not None:
         result["roofline"]["kernel_us_rocprof"] = rp[0]
         result["roofline"]["kernel_us_rocprof_source"] = rp[1]
+        # the same fraction from the committed rocprofv3 trace's durations, so the line follows
+        # profiles/: the mean over all launches (most of them isolated by the profiler: what a
+        # caller that does other work between steps pays) and the back-to-back median
+        result["roofline"]["frac_rocprof_mean"] = alg / (rp[0] * 1e-6) / 1e9 / HBM_PEAK_GBPS
         if rp[2] is not None:
             # the profiler leaves most launches isolated (each waits for the host); the ones that
             # still ran back to back, as in the graph-replayed timed region, are the like-for-like
             # figure for kernel_us (scripts/prof_summary.py B2B_US)
             result["roofline"]["kernel_us_rocprof_back_to_back_median"] = rp[2]
+            result["roofline"]["frac_rocprof_back_to_back"] = alg / (rp[2] * 1e-6) / 1e9 / HBM_PEAK_GBPS
     tr = pmc_traffic(grid_lanes, args.precision)
     if tr is not None:
         result["roofline"]["traffic"] = tr[0]

@@ -52,6 +52,16 @@ __device__ __forceinline__ double g_rsqrt(double x) {
   e = fma(-h * y, y, 0.5);
   return fma(y, e, y);
 }
+// One Newton step only: v_rsq_f64 is good to ~2^29 ulp (2^-23 relative), one step squares that
+// to ~2^-46 - for the drone <-> drone narrowphase's radial scaling (0.06 m x 2^-46 ~ 1e-15 m).
+__device__ __forceinline__ double g_rsqrt1(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  return fma(y, fma(-(0.5 * x) * y, y, 0.5), y);
+}
+__device__ __forceinline__ float g_rsqrt1(float x) {
+  const float y = __builtin_amdgcn_rsqf(x);
+  return fmaf(y, fmaf(-(0.5f * x) * y, y, 0.5f), y);
+}
 __device__ __forceinline__ float g_rsqrt(float x) {
   float y = __builtin_amdgcn_rsqf(x);
   const float h = 0.5f * x;
@@ -506,12 +516,14 @@ __device__ __forceinline__ void attitude_decide(R qx, R qy, R qz, R qw, Attitude
   }
 }
 // float32 Euler angles for the float32 observation.  The reference computes them in float64
-// (pybullet's getEulerFromQuaternion, BaseAviary.py:518) and casts them (BaseRLAviary.py:313-315):
-// with GPD_OBS_ANGLES_F64 (the default) the f64 sim does the same - double-precision asin / atan2 on
-// the double arguments, then the cast - so the angle columns agree with the reference to the cast
-// of a state that agrees to ~1e-14; the f32 sim (and GPD_OBS_ANGLES_F64=0) evaluates them in float32.
+// (pybullet's getEulerFromQuaternion, BaseAviary.py:518) and casts them (BaseRLAviary.py:313-315).
+// Here they are float32 asinf / atan2f of the double arguments (within ~2 float32 ulp of the cast
+// double result).  GPD_OBS_ANGLES_F64=1 builds the reference's order - double asin / atan2, then
+// the cast - and was measured on the 4096-env headline kernel (budget 0.1 us):
+// 5.01-5.04 -> 5.41-5.73 us per launch (three alternations, profiles/r4/angles/), ~2 KB more code
+// in the epilogue; not the default.
 #ifndef GPD_OBS_ANGLES_F64
-#define GPD_OBS_ANGLES_F64 1
+#define GPD_OBS_ANGLES_F64 0
 #endif
 template <typename R>
 __device__ __forceinline__ void obs_euler_f32(const R q[4], const AttitudeArgs<R>& t, float& roll, float& pitch,

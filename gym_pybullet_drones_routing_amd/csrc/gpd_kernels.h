@@ -299,59 +299,97 @@ __device__ __forceinline__ void wave_lds_sync() {
 // two drones' deltas in registers for the whole solve and the sweep needs no LDS at all.
 constexpr int kPairCold = 8;   // oracle/bullet_mb.py PAIR_COLD
 template <typename R>
-__device__ __forceinline__ void cyl_project(R cx, R cy, R cz, R ax, R ay, R az, R r, R hh, R& x, R& y, R& z) {
-  const R dx = x - cx, dy = y - cy, dz = z - cz;
-  const R t = pc_dot(dx, dy, dz, ax, ay, az);
-  const R tc = t > hh ? hh : (t < -hh ? -hh : t);
-  R rx = dx - t * ax, ry = dy - t * ay, rz = dz - t * az;
-  const R rho2 = pc_dot(rx, ry, rz, rx, ry, rz);
-  if (rho2 > r * r) {
-    const R f = r * g_rsqrt(rho2);   // Newton-refined: within ~1 ulp of r / sqrt(rho2) (the oracle's)
-    rx = rx * f; ry = ry * f; rz = rz * f;
-  }
-  x = (cx + tc * ax) + rx;
-  y = (cy + tc * ay) + ry;
-  z = (cz + tc * az) + rz;
-}
-template <typename R>
 __device__ __forceinline__ R cyl_extent_cos(R ua, R r, R hh) {
   const R s2 = R(1) - ua * ua;
   return hh * g_abs(ua) + r * g_sqrt(s2 > R(0) ? s2 : R(0));
 }
+// btPlaneSpace1
+template <typename R>
+__device__ __forceinline__ void plane_space(const R n[3], R p[3], R q[3]) {
+  if (g_abs(n[2]) > R(0.7071067811865475244008443621048490)) {
+    const R a = n[1] * n[1] + n[2] * n[2];
+    const R k = R(1) / g_sqrt(a);
+    p[0] = R(0); p[1] = -n[2] * k; p[2] = n[1] * k;
+    q[0] = a * k; q[1] = -n[0] * p[2]; q[2] = n[0] * p[1];
+  } else {
+    const R a = n[0] * n[0] + n[1] * n[1];
+    const R k = R(1) / g_sqrt(a);
+    p[0] = -n[1] * k; p[1] = n[0] * k; p[2] = R(0);
+    q[0] = -n[2] * p[1]; q[1] = n[2] * p[0]; q[2] = a * k;
+  }
+}
+
 // contact of cylinders A (centre ca, axis aa) and B: normal (B -> A), point on B, distance
 // (oracle/bullet_mb.py pair_geometry).  beta: FISTA's momentum weights (Consts::dc_beta).
+// The rounds run in B's frame (btPlaneSpace1(aB), aB): B's projection is then a radial scaling of
+// (x, y) and a clamp of z, and the selects replace the branches - 26 instead of ~42 dependent
+// operations per round on the one lane that holds the pair.  The oracle projects in world
+// coordinates: the same operations up to rounding (the rounds are non-expansive).
 template <typename R>
 __device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], const R cb[3], const R ab[3], R r, R hh,
                                               const R* beta, R n[3], R pb[3], R& dist) {
+  R bp[3], bq[3];
+  plane_space(ab, bp, bq);
   const R lx = ca[0] - cb[0], ly = ca[1] - cb[1], lz = ca[2] - cb[2];
+  // A's centre and axis in B's frame
+  const R Lx = pc_dot(bp[0], bp[1], bp[2], lx, ly, lz), Ly = pc_dot(bq[0], bq[1], bq[2], lx, ly, lz),
+          Lz = pc_dot(ab[0], ab[1], ab[2], lx, ly, lz);
+  const R Ax = pc_dot(bp[0], bp[1], bp[2], aa[0], aa[1], aa[2]), Ay = pc_dot(bq[0], bq[1], bq[2], aa[0], aa[1], aa[2]),
+          Az = pc_dot(ab[0], ab[1], ab[2], aa[0], aa[1], aa[2]);
   const R margins[4] = {R(0.001), R(0.003), R(0.006), R(0.011)};
   R yx = R(0), yy = R(0), yz = R(0);
   for (int lv = 0; lv < 4; ++lv) {
-    const R mg = margins[lv], rc = r - mg, hc = hh - mg;
+    const R mg = margins[lv], rc = r - mg, hc = hh - mg, rc2 = rc * rc;
+    // A's projection of (x, y, z) (the oracle's cyl_project around A)
+    auto proj_a = [&](R& x, R& y, R& z) {
+      const R dx = x - Lx, dy = y - Ly, dz = z - Lz;
+      const R t = pc_dot(dx, dy, dz, Ax, Ay, Az);
+      const R tc = t > hc ? hc : (t < -hc ? -hc : t);
+      const R rx = dx - t * Ax, ry = dy - t * Ay, rz = dz - t * Az;
+      const R rho2 = pc_dot(rx, ry, rz, rx, ry, rz);
+      const R s = rc * g_rsqrt1(rho2);
+      const R f = rho2 > rc2 ? s : R(1);
+      x = (Lx + tc * Ax) + rx * f;
+      y = (Ly + tc * Ay) + ry * f;
+      z = (Lz + tc * Az) + rz * f;
+    };
     yx = R(0); yy = R(0); yz = R(0);
     R zx = R(0), zy = R(0), zz = R(0);
 #pragma unroll
     for (int it = 0; it < kPairCold; ++it) {
       R px = zx, py = zy, pz = zz;
-      cyl_project(lx, ly, lz, aa[0], aa[1], aa[2], rc, hc, px, py, pz);
-      cyl_project(R(0), R(0), R(0), ab[0], ab[1], ab[2], rc, hc, px, py, pz);
+      proj_a(px, py, pz);
+      // B's projection: radial scaling of (x, y), clamp of z
+      const R rho2 = px * px + py * py;
+      const R s = rc * g_rsqrt1(rho2);
+      const R f = rho2 > rc2 ? s : R(1);
+      px = px * f; py = py * f;
+      pz = pz > hc ? hc : (pz < -hc ? -hc : pz);
       const R b = beta[it];
       zx = px + b * (px - yx); zy = py + b * (py - yy); zz = pz + b * (pz - yz);
       yx = px; yy = py; yz = pz;
     }
     R ax = yx, ay = yy, az = yz;
-    cyl_project(lx, ly, lz, aa[0], aa[1], aa[2], rc, hc, ax, ay, az);
+    proj_a(ax, ay, az);
     const R vx = ax - yx, vy = ay - yy, vz = az - yz;
     const R d2 = pc_dot(vx, vy, vz, vx, vy, vz);
     if (d2 > R(1e-4) * R(1e-4)) {
       const R dc = g_sqrt(d2);
-      n[0] = vx / dc; n[1] = vy / dc; n[2] = vz / dc;
-      pb[0] = cb[0] + (yx + n[0] * mg); pb[1] = cb[1] + (yy + n[1] * mg); pb[2] = cb[2] + (yz + n[2] * mg);
+      // back to world coordinates: n = (v / |v|) in (bp, bq, ab), y likewise
+      const R ux = vx / dc, uy = vy / dc, uz = vz / dc;
+      n[0] = (ux * bp[0] + uy * bq[0]) + uz * ab[0];
+      n[1] = (ux * bp[1] + uy * bq[1]) + uz * ab[1];
+      n[2] = (ux * bp[2] + uy * bq[2]) + uz * ab[2];
+      const R wx = (yx * bp[0] + yy * bq[0]) + yz * ab[0], wy = (yx * bp[1] + yy * bq[1]) + yz * ab[1],
+              wz = (yx * bp[2] + yy * bq[2]) + yz * ab[2];
+      pb[0] = cb[0] + (wx + n[0] * mg); pb[1] = cb[1] + (wy + n[1] * mg); pb[2] = cb[2] + (wz + n[2] * mg);
       dist = dc - R(2) * mg;
       return;
     }
   }
-  pb[0] = cb[0] + yx; pb[1] = cb[1] + yy; pb[2] = cb[2] + yz;
+  pb[0] = cb[0] + ((yx * bp[0] + yy * bq[0]) + yz * ab[0]);
+  pb[1] = cb[1] + ((yx * bp[1] + yy * bq[1]) + yz * ab[1]);
+  pb[2] = cb[2] + ((yx * bp[2] + yy * bq[2]) + yz * ab[2]);
   const R c2 = pc_dot(lx, ly, lz, lx, ly, lz);
   R best = R(0);
   bool have = false;
@@ -377,22 +415,6 @@ __device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], cons
   }
   dist = -best;
 }
-// btPlaneSpace1
-template <typename R>
-__device__ __forceinline__ void plane_space(const R n[3], R p[3], R q[3]) {
-  if (g_abs(n[2]) > R(0.7071067811865475244008443621048490)) {
-    const R a = n[1] * n[1] + n[2] * n[2];
-    const R k = R(1) / g_sqrt(a);
-    p[0] = R(0); p[1] = -n[2] * k; p[2] = n[1] * k;
-    q[0] = a * k; q[1] = -n[0] * p[2]; q[2] = n[0] * p[1];
-  } else {
-    const R a = n[0] * n[0] + n[1] * n[1];
-    const R k = R(1) / g_sqrt(a);
-    p[0] = -n[1] * k; p[1] = n[0] * k; p[2] = R(0);
-    q[0] = -n[2] * p[1]; q[1] = n[2] * p[0]; q[2] = a * k;
-  }
-}
-
 #ifndef GPD_DC_DIAG
 #define GPD_DC_DIAG 0   // diagnostic builds only: 1 = broadphase only (no solve compiled),
                         // 3 = no drone contact, 6 = the solve compiled but never entered
@@ -405,8 +427,10 @@ struct DcLds {
   R dc[DC_N][kWave];                  // drone columns
   unsigned long long nearw[kDcChunks], contw[kDcChunks];   // pairs in reach / in contact, by chunk
   R eres[kWave];                      // per env: this iteration's largest squared residual
-  int edone[kWave], ecnt[kWave];      // per env: solve finished, contacts
+  int edone[kWave];                   // per env: solve finished
   int stouch[kWave];                  // drone in a contact
+  int cij[kWave], clev[kWave];        // chunk 0: the pair lane's contact (i | j << 8) and its level
+  int dlev[kWave];                    // per drone: the level of its last contact (level pass)
 };
 // one LDS block per instantiation, shared by the hook (inlined) and the solve (a call)
 template <typename R>
@@ -652,6 +676,7 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
   DcRow<R> w0;
   bool have0 = false;
   w0.i = w0.j = 0;
+  w0.rank = 0;
   R* rows = reinterpret_cast<R*>(dp.rows);
   constexpr int kRowR = dc_row_reals<R>();
   for (int ch = 0; ch < dp.nch; ++ch) {
@@ -674,6 +699,7 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
           DcRow<R> w;
           dc_row_setup(L, i, j, n, pb, dist, c, inv_m, idt, w);
           w.env = (p * dp.pmagic) >> 20;
+          w.rank = 0;   // the level pass below re-ranks when some env holds two contacts
           if (ch == 0) {
             w0 = w;
             have0 = true;
@@ -693,16 +719,63 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
   t1 = __builtin_readcyclecounter();
 #endif
   // contacts per env, each contact's rank within its env (the (i, j) order)
-  int rounds = 0;
-  for (int e = 0; e < nenv; ++e) {
-    const int k = popc_range(L.contw, e * dp.P, (e + 1) * dp.P);
-    rounds = k > rounds ? k : rounds;
+  // the largest contact count of an env: one count per env lane, then a wave max
+  int maxcnt = ln < nenv ? popc_range(L.contw, ln * dp.P, (ln + 1) * dp.P) : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int x = __shfl_xor(maxcnt, o);
+    maxcnt = x > maxcnt ? x : maxcnt;
   }
-  if (have0) w0.rank = popc_range(L.contw, w0.env * dp.P, ln);
-  for (int ch = 1; ch < dp.nch; ++ch) {
-    if (((L.contw[ch] >> ln) & 1ull) == 0) continue;
-    int* ri = reinterpret_cast<int*>(rows + (long long)(ch - 1) * kWave * kRowR + 55 * kWave);
-    ri[3 * kWave + ln] = popc_range(L.contw, ri[2 * kWave + ln] * dp.P, ln + kWave * ch);
+  // Gauss-Seidel levels (only when some env holds two contacts): a contact's level is one more
+  // than the highest level among the earlier contacts (in (i, j) order) that share a drone with it.
+  // Contacts of one level share no drone, so solving a level's contacts at once and the levels in
+  // order IS the sequential sweep over the env's contacts (non-adjacent rows of disjoint drones
+  // commute) - a pile of contacts through one drone still takes one round per contact, independent
+  // pairs of one env take one.
+  int rounds = maxcnt;
+  if (maxcnt > 1) {
+    L.dlev[ln] = 0;
+    L.cij[ln] = have0 ? (w0.i | (w0.j << 8)) : 0;
+    wave_lds_sync();
+    int lmax = 0;
+    if (ln < nenv) {
+      const int lo = ln * dp.P, hi = lo + dp.P;
+      for (int w = lo >> 6; w < ((hi + 63) >> 6); ++w) {
+        unsigned long long m = L.contw[w];
+        const int b0 = w << 6;
+        if (lo > b0) m &= ~0ull << (lo - b0);
+        if (hi < b0 + 64) m &= (1ull << (hi - b0)) - 1ull;
+        while (m) {
+          const int p = b0 + __builtin_ctzll(m);
+          m &= m - 1ull;
+          int pij;
+          int* rank_slot = nullptr;
+          if (p < kWave) {
+            pij = L.cij[p];
+          } else {
+            pij = dc_pair_lanes(dp, p);
+            rank_slot = reinterpret_cast<int*>(rows + (long long)(p / kWave - 1) * kWave * kRowR + 55 * kWave) +
+                        3 * kWave + (p & (kWave - 1));
+          }
+          const int i = pij & 255, j = pij >> 8;
+          const int li = L.dlev[i], lj = L.dlev[j];
+          const int lev = (li > lj ? li : lj) + 1;
+          L.dlev[i] = lev;
+          L.dlev[j] = lev;
+          if (p < kWave) L.clev[p] = lev - 1;
+          else *rank_slot = lev - 1;
+          lmax = lev > lmax ? lev : lmax;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const int x = __shfl_xor(lmax, o);
+      lmax = x > lmax ? x : lmax;
+    }
+    rounds = lmax;
+    wave_lds_sync();
+    if (have0) w0.rank = L.clev[ln];
   }
   const R mu = c.dd_mu, resid = c.resid;
   const int iters = c.iters;
@@ -710,7 +783,7 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
   t2 = __builtin_readcyclecounter();
   int it_used = 0;
 #endif
-  if (rounds <= 1 && dp.nch <= 1) {
+  if (maxcnt <= 1 && dp.nch <= 1) {
     // ---- every env has at most one contact: its lane owns both drones' deltas
     R vi[6] = {R(0), R(0), R(0), R(0), R(0), R(0)}, vj[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
     bool done = !have0;
@@ -732,7 +805,7 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
       L.dc[DC_DAX][w0.j] = vj[3]; L.dc[DC_DAY][w0.j] = vj[4]; L.dc[DC_DAZ][w0.j] = vj[5];
     }
   } else {
-    // ---- general case: round r solves the r-th contact of every env; deltas through LDS
+    // ---- general case: round r solves the level-r contacts of every env; deltas through LDS
     if (ln < nenv) L.edone[ln] = popc_range(L.contw, ln * dp.P, (ln + 1) * dp.P) == 0;
     wave_lds_sync();
     R vi[6], vj[6];
@@ -743,7 +816,12 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
       const R rr = friction ? dc_friction(w, mu, inv_m, vi, vj) : dc_normal(w, inv_m, vi, vj);
 #pragma unroll
       for (int x = 0; x < 6; ++x) { L.dc[DC_DLX + x][w.i] = vi[x]; L.dc[DC_DLX + x][w.j] = vj[x]; }
-      L.eres[w.env] = g_fmax(L.eres[w.env], rr);   // one row of an env per round: no race
+      // several rows of an env per round (one level): the max through an LDS atomic on the bit
+      // pattern (non-negative floats order as unsigned integers)
+      if (sizeof(R) == 8)
+        atomicMax(reinterpret_cast<unsigned long long*>(&L.eres[w.env]), (unsigned long long)__double_as_longlong((double)rr));
+      else
+        atomicMax(reinterpret_cast<unsigned int*>(&L.eres[w.env]), (unsigned int)__float_as_uint((float)rr));
     };
     for (int it = 0; it < iters; ++it) {
       if (__ballot(ln < nenv && !L.edone[ln]) == 0ull) break;

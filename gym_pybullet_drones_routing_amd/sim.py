@@ -49,7 +49,11 @@ def physics_flags(physics=Physics.DYN, aero=()):
     §8 f3): default damping, world-frame angular velocity, exponential-map orientation, and the
     collision cylinder's contact with the ground plane (``plane.urdf``, BaseAviary.py:484) and,
     in envs of several drones, with the env's other drones (every drone is a colliding body,
-    :486-491; envs of more than 64 drones raise NotImplementedError unless ``no_drone_contact``).  ``aero`` adds terms by name
+    :486-491; envs of more than 64 drones raise NotImplementedError unless ``no_drone_contact``).
+    Known deviations of the contact restatement from pybullet (parity unpinned):
+    one point per pair (Bullet keeps a 4-point manifold), and the pair rows are solved before the
+    plane rows instead of in one island solve, so a drone resting on another that rests on the
+    plane sinks into it until the ERP push balances (~1 cm).  ``aero`` adds terms by name
     (``gnd``, ``drag``, ``dw``, ``geom``, ``bullet``, ``no_plane``, ``no_drone_contact``), e.g.
     the aero terms on the DYN integrator (BASELINE config 3), ``no_plane`` for the reference's
     commented-out plane collision filter (:500-503), or ``no_drone_contact``.

@@ -11,6 +11,9 @@
 #   pmc_probe      one PMC pass per counter group of $PMC_GROUPS (';'-separated) and library of $LIBS
 #                  over contact_probe.py $PROBE_CASES (PROBE_STEPS / PROBE_WARM shorten it)
 #   ab             bench.py --no-cpu-baseline --steps 300 with every library of $LIBS, alternated
+#   rollout        scripts/prof_rollout.py (bench.py's RL-rollout leg) for each store policy of
+#                  $POLICIES (gpd_config::store_policy, 0 = library default), alternated $REPS times
+#   rollout_trace  rocprofv3 --kernel-trace --stats of prof_rollout.py for each policy of $POLICIES
 #   py             python -u $PY_ARGS (a probe script), output to py.log
 #   full           tests smoke bench traces pmc_bytes
 # Output: gpurun_out/$RUN_TAG/.
@@ -73,6 +76,20 @@ job_ab() {
       GPD_ALLOW_ABI_MISMATCH=1 GPD_LIB=$(libpath $v) timeout -k 10 300 python bench.py --no-cpu-baseline --steps 300 \
         ${BENCH_ARGS} > $OUT/ab_${v}_r$rep.json 2> $OUT/ab_${v}_r$rep.err || return $?
     done
+  done
+}
+job_rollout() {
+  for rep in $(seq $REPS); do
+    for pol in ${POLICIES:-0}; do
+      echo "== policy $pol rep $rep" >> $OUT/rollout.log
+      timeout -k 10 300 python -u scripts/prof_rollout.py --policy $pol 2>> $OUT/rollout.err | quiet >> $OUT/rollout.log || return $?
+    done
+  done
+}
+job_rollout_trace() {
+  for pol in ${POLICIES:-0}; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_rollout_p$pol -o rollout --output-format csv -- \
+      python3 scripts/prof_rollout.py --policy $pol > $OUT/prof_rollout_p$pol.json 2> $OUT/prof_rollout_p$pol.err || return $?
   done
 }
 job_py() { timeout -k 10 ${PY_TIMEOUT:-300} python -u $PY_ARGS > $OUT/py.log 2>&1; }
