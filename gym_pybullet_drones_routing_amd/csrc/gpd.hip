@@ -1043,12 +1043,12 @@ int gpd_debug_stamps(unsigned long long* out_host, int n_blocks) {
 #endif
 
 #ifdef GPD_CONTACT_STATS
-// diagnostic build only: read and clear the contact-solve histogram (128 counters)
+// diagnostic build only: read and clear the contact-solve histogram (kPcHist counters)
 int gpd_debug_contact_hist(unsigned long long* out_host) {
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_pc_hist), 128 * 8, 0, hipMemcpyDeviceToHost));
-  unsigned long long zero[128] = {};
-  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_pc_hist), zero, 128 * 8, 0, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_pc_hist), kPcHist * 8, 0, hipMemcpyDeviceToHost));
+  static unsigned long long zero[kPcHist] = {};
+  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_pc_hist), zero, kPcHist * 8, 0, hipMemcpyHostToDevice));
   return GPD_OK;
 }
 #endif

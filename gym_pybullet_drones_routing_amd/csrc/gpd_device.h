@@ -439,6 +439,30 @@ __device__ __forceinline__ bool upright(const AttitudeArgs<R>& t) {
   return !t.gimbal && (t.b > R(0) || (t.b == R(0) && t.a == R(0) && !signbit(t.b)));
 }
 
+// ---------------------------------------------------------------- cold paths out of line
+// GPD_COLD_CALLS=1: the rare branches' bodies (the library cos / sin of the _integrateQ weights for
+// |theta| >= 0.5, the exact attitude re-decision) become calls, so their code sits outside the
+// kernel's instruction stream instead of after its end (instruction fetch).
+// Measured: headline kernel 4.97 us vs 5.03-5.34 us inline (profiles/r4/cold/); 0 = inline.
+#ifndef GPD_COLD_CALLS
+#define GPD_COLD_CALLS 1
+#endif
+#if GPD_COLD_CALLS
+#define GPD_COLD __attribute__((noinline, cold))
+#else
+#define GPD_COLD __forceinline__
+#endif
+template <typename R>
+struct CoSh {
+  R co, sh;
+};
+// cos(|w| hdt) and sin(|w| hdt) / |w| from |w|^2 (the library functions: |theta| >= 0.5)
+template <typename R>
+__device__ GPD_COLD CoSh<R> cold_cos_sinc(R n2, R hdt) {
+  const R nrm = g_sqrt(n2), th = nrm * hdt;
+  return CoSh<R>{g_cos(th), g_sin(th) / nrm};
+}
+
 // ---------------------------------------------------------------- exact attitude decisions (f64)
 // tilted_beyond / upright see the fused readback's quaternion (~1 ulp from Bullet's) and compare
 // against rounded limits, so within a few ulp of a threshold they can disagree with the
@@ -485,6 +509,20 @@ __device__ __forceinline__ void attitude_literal(R x, R y, R z, R w, AttitudeArg
   t.gimbal = t.sarg <= R(-0.99999) || t.sarg >= R(0.99999);
 }
 
+// the exact decisions from the literal Bullet readback (attitude_decide's rare lanes)
+struct AttExact {
+  double sarg, a, b;
+  bool gimbal, tilt, up;
+};
+__device__ GPD_COLD AttExact attitude_exact(double qx, double qy, double qz, double qw) {
+  AttitudeArgs<double> t;
+  attitude_literal(qx, qy, qz, qw, t);
+  const bool zero_roll = t.a == 0.0 && t.b == 0.0 && !signbit(t.b);   // atan2(+-0, +0) = +-0
+  const bool roll_out = t.b > 0.0 ? dd_above(fabs(t.a), AttK::tan_hi, AttK::tan_lo, t.b) : !zero_roll;
+  const bool roll_in = t.b > 0.0 ? dd_above(t.b, AttK::cot_hi, AttK::cot_lo, fabs(t.a)) : zero_roll;
+  return AttExact{t.sarg, t.a, t.b, t.gimbal, t.gimbal || fabs(t.sarg) >= AttK::sin_lim || roll_out,
+                  !t.gimbal && roll_in};
+}
 // TILT: tilt = |roll| > 0.4 or |pitch| > 0.4; UP: up = |roll| < pi/2 and |pitch| < pi/2.
 // qs = the stored quaternion the readback starts from; t = attitude_args of the fused readback,
 // replaced by the literal arguments on the lanes that were re-decided (so that the observation's
@@ -501,16 +539,10 @@ __device__ __forceinline__ void attitude_decide(R qx, R qy, R qz, R qw, Attitude
     if (UP) near = near || fabs(t.b) < AttK::band;
     if (GPD_RARE(__ballot(near) != 0ull)) {
       if (near) {
-        attitude_literal(qx, qy, qz, qw, t);
-        const bool zero_roll = t.a == 0.0 && t.b == 0.0 && !signbit(t.b);   // atan2(+-0, +0) = +-0
-        if (TILT) {
-          const bool roll_out = t.b > 0.0 ? dd_above(fabs(t.a), AttK::tan_hi, AttK::tan_lo, t.b) : !zero_roll;
-          tilt = t.gimbal || fabs(t.sarg) >= AttK::sin_lim || roll_out;
-        }
-        if (UP) {
-          const bool roll_in = t.b > 0.0 ? dd_above(t.b, AttK::cot_hi, AttK::cot_lo, fabs(t.a)) : zero_roll;
-          up = !t.gimbal && roll_in;
-        }
+        const AttExact e = attitude_exact(qx, qy, qz, qw);
+        t.sarg = e.sarg; t.a = e.a; t.b = e.b; t.gimbal = e.gimbal;
+        if (TILT) tilt = e.tilt;
+        if (UP) up = e.up;
       }
     }
   }
@@ -650,8 +682,12 @@ __device__ __forceinline__ R pc_dot(R ax, R ay, R az, R bx, R by, R bz) { return
 constexpr int kWaveLanes = 64;
 
 #ifdef GPD_CONTACT_STATS
-// diagnostic build only: per solving wave, the iterations run [0..50] and the active lanes [51..115]
-__device__ unsigned long long g_pc_hist[128];
+// diagnostic build only: per solving wave, the iterations run [0..50] and the active lanes [51..115];
+// 116..127 drone-contact totals (DcHook / dc_solve); 128..191 log2 histogram of a drone-contact
+// solve's cycles; 192..242 its iteration histogram; 256 + b: block b's drone-contact cycles;
+// 256 + 4096 + b: block b's step-kernel cycles; 256 + 8192 + b: block b's plane-solve cycles
+constexpr int kPcHist = 256 + 3 * 4096;
+__device__ unsigned long long g_pc_hist[kPcHist];
 #endif
 // r_p x d for the rim point p (p = 0..3: (cr,0,zc), (0,cr,zc), (-cr,0,zc), (0,-cr,zc)), with the
 // zero components dropped (exact: 0*x - y == -y).
@@ -993,6 +1029,7 @@ __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], c
     atomicAdd(&g_pc_hist[120], t_loop - t_setup);   // setup cycles (s_memtime)
     atomicAdd(&g_pc_hist[121], t_end - t_loop);     // iteration-loop cycles (incl. the unpark)
     atomicAdd(&g_pc_hist[122], (unsigned long long)it_used);
+    if (blockIdx.x < 4096) atomicAdd(&g_pc_hist[256 + 8192 + blockIdx.x], t_end - t_setup);
   }
 #endif
   s.vx = any ? s.vx + DLx : s.vx;
@@ -1307,8 +1344,8 @@ __device__ __forceinline__ void dyn_substep(Drone<R>& s, R rpm[4], R W[4], R las
   asm volatile("" ::"v"(s.px), "v"(s.py), "v"(s.pz));
   if (GPD_RARE(__ballot(big) != 0ull)) {
     if (big) {
-      const R nrm = g_sqrt(n2), th = nrm * k.hdt;
-      update(g_cos(th), g_sin(th) / nrm);
+      const CoSh<R> cs = cold_cos_sinc(n2, k.hdt);
+      update(cs.co, cs.sh);
     }
   }
 }
@@ -1343,9 +1380,9 @@ __device__ __forceinline__ void rate_half(R& wx, R& wy, R& wz, const R W[4], con
   const bool big = t2 >= R(0.25);
   if (GPD_RARE(__ballot(big) != 0ull)) {
     if (big) {
-      const R nrm = g_sqrt(n2), th = nrm * k.hdt;
-      co = g_cos(th);
-      sh = g_sin(th) / nrm;
+      const CoSh<R> cs = cold_cos_sinc(n2, k.hdt);
+      co = cs.co;
+      sh = cs.sh;
     }
   }
   h[0] = co; h[1] = sh;

@@ -290,9 +290,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 // (i, j) index of bullet_mb.drone_contacts' order) and lane ln handles pairs ln, ln + 64, ... (chunk
 // ch = p / 64).  The hot part (DcHook, every substep): the drones' centre / axis columns into LDS,
 // the broadphase of every pair (the sphere test; the separating-axis tests only for pairs in
-// reach), one ballot per chunk.  A wave with a pair in reach calls dc_solve (rare): the narrowphase
-// of its near pairs in parallel over lanes, each contact's rows set up by the lane of its pair -
-// chunk 0 in that lane's registers, later chunks in a per-block global row store - then the
+// reach), one ballot per chunk.  A wave with a pair in reach calls dc_solve (rare): its near pairs
+// compacted over the lanes (in pair order, whatever chunk they come from), the narrowphase of up to
+// 64 of them per pass in parallel, each contact's rows set up by its lane - pass 0 in that lane's
+// registers, later passes (more than 64 near pairs) in a per-block global row store - then the
 // Gauss-Seidel sweeps: round r solves the r-th contact of every env at once (contacts of different
 // envs touch different drones), the drones' velocity deltas in LDS.  When no env of the wave has
 // more than one contact (every two-drone env, most waves of 8-drone envs) the owner lane keeps its
@@ -429,8 +430,10 @@ struct DcLds {
   R eres[kWave];                      // per env: this iteration's largest squared residual
   int edone[kWave];                   // per env: solve finished
   int stouch[kWave];                  // drone in a contact
-  int cij[kWave], clev[kWave];        // chunk 0: the pair lane's contact (i | j << 8) and its level
+  int cij[kWave], clev[kWave];        // pass 0: the lane's contact (i | j << 8) and its level
   int dlev[kWave];                    // per drone: the level of its last contact (level pass)
+  int nsp[kWave], nsij[kWave];        // this pass's near pairs: pair index, i | j << 8
+  int ecnt[kWave], ek0[kWave], ek1[kWave];   // per env: contacts, their near-index range [ek0, ek1)
 };
 // one LDS block per instantiation, shared by the hook (inlined) and the solve (a call)
 template <typename R>
@@ -602,7 +605,7 @@ __device__ __forceinline__ R dc_friction(DcRow<R>& w, R mu, R inv_m, R vi[6], R 
   R s2 = w.lam[2] + (w.rhs[2] - w.jdi[2] * dc_jv(w, 2, vi, vj));
   const R m2 = s1 * s1 + s2 * s2;
   if (m2 > lim * lim) {
-    const R f = lim * g_rsqrt(m2);
+    const R f = lim * g_rsqrt1(m2);   // one Newton step: ~1e-14 relative on the projected impulse
     s1 = s1 * f;
     s2 = s2 * f;
   }
@@ -613,18 +616,6 @@ __device__ __forceinline__ R dc_friction(DcRow<R>& w, R mu, R inv_m, R vi[6], R 
   dc_apply(w, 2, e2, inv_m, vi, vj);
   const R rr = e1 + e2;
   return rr * rr;
-}
-// bits set in words[] over [lo, hi)
-__device__ __forceinline__ int popc_range(const unsigned long long* words, int lo, int hi) {
-  int n = 0;
-  for (int w = lo >> 6; w < ((hi + 63) >> 6); ++w) {
-    unsigned long long m = words[w];
-    const int b0 = w << 6;
-    if (lo > b0) m &= ~0ull << (lo - b0);
-    if (hi < b0 + 64) m &= (1ull << (hi - b0)) - 1ull;
-    n += __popcll(m);
-  }
-  return n;
 }
 // the row store: per chunk, element x of lane ln at chunk[x * 64 + ln] (55 reals), then the four
 // ints (i, j, env, rank) at ints[k * 64 + ln] behind them
@@ -672,55 +663,76 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
   L.dc[DC_DLX][ln] = R(0); L.dc[DC_DLY][ln] = R(0); L.dc[DC_DLZ][ln] = R(0);
   L.dc[DC_DAX][ln] = R(0); L.dc[DC_DAY][ln] = R(0); L.dc[DC_DAZ][ln] = R(0);
   L.stouch[ln] = 0;
-  // ---- narrowphase of the pairs in reach (in parallel over lanes), rows by the pair's lane
+  // ---- the near pairs compacted (pair order kept): near pair k to lane k % 64 of pass k / 64, so
+  // that one pass of narrowphases covers up to 64 near pairs from any of the block's pair chunks;
+  // each contact's rows set up by its lane - pass 0 in the lane's registers, later passes in the
+  // block's global row store
+  int nnear = 0;
+  for (int ch = 0; ch < dp.nch; ++ch) nnear += __popcll(L.nearw[ch]);
+  if (ln < nenv) { L.ecnt[ln] = 0; L.ek0[ln] = 0x7fffffff; L.ek1[ln] = 0; }
+  const int npass = (nnear + kWave - 1) / kWave;
   DcRow<R> w0;
   bool have0 = false;
   w0.i = w0.j = 0;
   w0.rank = 0;
   R* rows = reinterpret_cast<R*>(dp.rows);
   constexpr int kRowR = dc_row_reals<R>();
-  for (int ch = 0; ch < dp.nch; ++ch) {
-    const unsigned long long nw = L.nearw[ch];
-    bool con = false;
-    if (nw != 0) {
-      const int p = ln + kWave * ch;
+  for (int ps = 0; ps < npass; ++ps) {
+    int base = -ps * kWave;
+    for (int ch = 0; ch < dp.nch; ++ch) {
+      const unsigned long long nw = L.nearw[ch];
       if ((nw >> ln) & 1ull) {
-#ifdef GPD_CONTACT_STATS
-        ++n_near;
-#endif
-        const int pij = dc_pair_of(dp, ch, p);
-        const int i = pij & 255, j = pij >> 8;
-        const R ca[3] = {L.dc[DC_CX][i], L.dc[DC_CY][i], L.dc[DC_CZ][i]}, aa[3] = {L.dc[DC_AX][i], L.dc[DC_AY][i], L.dc[DC_AZ][i]};
-        const R cb[3] = {L.dc[DC_CX][j], L.dc[DC_CY][j], L.dc[DC_CZ][j]}, ab[3] = {L.dc[DC_AX][j], L.dc[DC_AY][j], L.dc[DC_AZ][j]};
-        R n[3], pb[3], dist;
-        pair_geometry(ca, aa, cb, ab, c.cyl_r, c.cyl_hh, c.dc_beta, n, pb, dist);
-        con = dist < c.brk;
-        if (con) {
-          DcRow<R> w;
-          dc_row_setup(L, i, j, n, pb, dist, c, inv_m, idt, w);
-          w.env = (p * dp.pmagic) >> 20;
-          w.rank = 0;   // the level pass below re-ranks when some env holds two contacts
-          if (ch == 0) {
-            w0 = w;
-            have0 = true;
-          } else {
-            dc_row_store(rows + (long long)(ch - 1) * kWave * kRowR, ln, w);
-          }
-          L.stouch[i] = 1;
-          L.stouch[j] = 1;
+        const int k = base + __popcll(nw & ((1ull << ln) - 1ull));
+        if (k >= 0 && k < kWave) {
+          const int p = ln + kWave * ch;
+          L.nsp[k] = p;
+          L.nsij[k] = dc_pair_of(dp, ch, p);
         }
+      }
+      base += __popcll(nw);
+    }
+    wave_lds_sync();
+    const int k = ps * kWave + ln;
+    bool con = false;
+    if (k < nnear) {
+#ifdef GPD_CONTACT_STATS
+      ++n_near;
+#endif
+      const int p = L.nsp[ln], pij = L.nsij[ln];
+      const int i = pij & 255, j = pij >> 8;
+      const R ca[3] = {L.dc[DC_CX][i], L.dc[DC_CY][i], L.dc[DC_CZ][i]}, aa[3] = {L.dc[DC_AX][i], L.dc[DC_AY][i], L.dc[DC_AZ][i]};
+      const R cb[3] = {L.dc[DC_CX][j], L.dc[DC_CY][j], L.dc[DC_CZ][j]}, ab[3] = {L.dc[DC_AX][j], L.dc[DC_AY][j], L.dc[DC_AZ][j]};
+      R n[3], pb[3], dist;
+      pair_geometry(ca, aa, cb, ab, c.cyl_r, c.cyl_hh, c.dc_beta, n, pb, dist);
+      con = dist < c.brk;
+      if (con) {
+        DcRow<R> w;
+        dc_row_setup(L, i, j, n, pb, dist, c, inv_m, idt, w);
+        w.env = (p * dp.pmagic) >> 20;
+        w.rank = 0;   // the level pass below re-ranks when some env holds two contacts
+        if (ps == 0) {
+          w0 = w;
+          have0 = true;
+          L.cij[ln] = pij;
+        } else {
+          dc_row_store(rows + (long long)(ps - 1) * kWave * kRowR, ln, w);
+        }
+        L.stouch[i] = 1;
+        L.stouch[j] = 1;
+        atomicAdd(&L.ecnt[w.env], 1);
+        atomicMin(&L.ek0[w.env], k);
+        atomicMax(&L.ek1[w.env], k + 1);
       }
     }
     const unsigned long long cw = __ballot(con);
-    if (ln == 0) L.contw[ch] = cw;
+    if (ln == 0) L.contw[ps] = cw;
+    wave_lds_sync();   // this pass's near slots are rewritten by the next one
   }
-  wave_lds_sync();
 #ifdef GPD_CONTACT_STATS
   t1 = __builtin_readcyclecounter();
 #endif
-  // contacts per env, each contact's rank within its env (the (i, j) order)
-  // the largest contact count of an env: one count per env lane, then a wave max
-  int maxcnt = ln < nenv ? popc_range(L.contw, ln * dp.P, (ln + 1) * dp.P) : 0;
+  // the largest contact count of an env
+  int maxcnt = ln < nenv ? L.ecnt[ln] : 0;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const int x = __shfl_xor(maxcnt, o);
@@ -731,41 +743,32 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
   // Contacts of one level share no drone, so solving a level's contacts at once and the levels in
   // order IS the sequential sweep over the env's contacts (non-adjacent rows of disjoint drones
   // commute) - a pile of contacts through one drone still takes one round per contact, independent
-  // pairs of one env take one.
+  // pairs of one env take one.  An env's contacts are its near indices [ek0, ek1) with the contact bit.
   int rounds = maxcnt;
   if (maxcnt > 1) {
     L.dlev[ln] = 0;
-    L.cij[ln] = have0 ? (w0.i | (w0.j << 8)) : 0;
+    L.clev[ln] = 0;
     wave_lds_sync();
-    int lmax = 0;
-    if (ln < nenv) {
-      const int lo = ln * dp.P, hi = lo + dp.P;
-      for (int w = lo >> 6; w < ((hi + 63) >> 6); ++w) {
-        unsigned long long m = L.contw[w];
-        const int b0 = w << 6;
-        if (lo > b0) m &= ~0ull << (lo - b0);
-        if (hi < b0 + 64) m &= (1ull << (hi - b0)) - 1ull;
-        while (m) {
-          const int p = b0 + __builtin_ctzll(m);
-          m &= m - 1ull;
-          int pij;
-          int* rank_slot = nullptr;
-          if (p < kWave) {
-            pij = L.cij[p];
-          } else {
-            pij = dc_pair_lanes(dp, p);
-            rank_slot = reinterpret_cast<int*>(rows + (long long)(p / kWave - 1) * kWave * kRowR + 55 * kWave) +
-                        3 * kWave + (p & (kWave - 1));
-          }
-          const int i = pij & 255, j = pij >> 8;
-          const int li = L.dlev[i], lj = L.dlev[j];
-          const int lev = (li > lj ? li : lj) + 1;
-          L.dlev[i] = lev;
-          L.dlev[j] = lev;
-          if (p < kWave) L.clev[p] = lev - 1;
-          else *rank_slot = lev - 1;
-          lmax = lev > lmax ? lev : lmax;
+    int lmax = ln < nenv && L.ecnt[ln] > 0 ? 1 : 0;
+    if (ln < nenv && L.ecnt[ln] > 1) {
+      for (int k = L.ek0[ln]; k < L.ek1[ln]; ++k) {
+        if (((L.contw[k >> 6] >> (k & 63)) & 1ull) == 0) continue;
+        int pij;
+        int* ints = nullptr;
+        if (k < kWave) {
+          pij = L.cij[k];
+        } else {
+          ints = reinterpret_cast<int*>(rows + (long long)(k / kWave - 1) * kWave * kRowR + 55 * kWave) + (k & (kWave - 1));
+          pij = ints[0] | (ints[kWave] << 8);
         }
+        const int i = pij & 255, j = pij >> 8;
+        const int li = L.dlev[i], lj = L.dlev[j];
+        const int lev = (li > lj ? li : lj) + 1;
+        L.dlev[i] = lev;
+        L.dlev[j] = lev;
+        if (k < kWave) L.clev[k] = lev - 1;
+        else ints[3 * kWave] = lev - 1;
+        lmax = lev > lmax ? lev : lmax;
       }
     }
 #pragma unroll
@@ -783,7 +786,7 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
   t2 = __builtin_readcyclecounter();
   int it_used = 0;
 #endif
-  if (maxcnt <= 1 && dp.nch <= 1) {
+  if (maxcnt <= 1 && npass <= 1) {
     // ---- every env has at most one contact: its lane owns both drones' deltas
     R vi[6] = {R(0), R(0), R(0), R(0), R(0), R(0)}, vj[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
     bool done = !have0;
@@ -806,7 +809,7 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
     }
   } else {
     // ---- general case: round r solves the level-r contacts of every env; deltas through LDS
-    if (ln < nenv) L.edone[ln] = popc_range(L.contw, ln * dp.P, (ln + 1) * dp.P) == 0;
+    if (ln < nenv) L.edone[ln] = L.ecnt[ln] == 0;
     wave_lds_sync();
     R vi[6], vj[6];
     auto visit = [&](DcRow<R>& w, bool friction) {
@@ -833,7 +836,7 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
       for (int ph = 0; ph < 2; ++ph) {              // normal rows, then friction pairs
         for (int r = 0; r < rounds; ++r) {
           if (have0 && w0.rank == r) visit(w0, ph == 1);
-          for (int ch = 1; ch < dp.nch; ++ch) {
+          for (int ch = 1; ch < npass; ++ch) {
             if (((L.contw[ch] >> ln) & 1ull) == 0) continue;
             R* chunk = rows + (long long)(ch - 1) * kWave * kRowR;
             DcRow<R> w;
@@ -863,6 +866,10 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
       atomicAdd(&g_pc_hist[123], t1 - t0);
       atomicAdd(&g_pc_hist[126], (unsigned long long)nc);
       atomicAdd(&g_pc_hist[127], (unsigned long long)tot);
+      const unsigned long long cyc = t3 - t0;
+      atomicAdd(&g_pc_hist[128 + (63 - __clzll(cyc | 1ull))], 1ull);
+      atomicAdd(&g_pc_hist[192 + it_used], 1ull);
+      if (blockIdx.x < 4096) atomicAdd(&g_pc_hist[256 + blockIdx.x], cyc);
     }
   }
 #endif
@@ -1105,6 +1112,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
   __shared__ R spair[MULTI ? kPairMax : 1];
   GPD_RSTAMP(11);
   GPD_STAMP(0);
+#ifdef GPD_CONTACT_STATS
+  const unsigned long long tk0 = __builtin_readcyclecounter();
+#endif
   const Consts<R>& c = *cp;
   const int tid = threadIdx.x;
   const int D = MULTI ? v.D : 1;
@@ -1336,6 +1346,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
                                                              io.obs, io.terminal_obs, n0);
   GPD_STAMP(7);
   GPD_RSTAMP(12);
+#ifdef GPD_CONTACT_STATS
+  if (tid == 0 && blockIdx.x < 4096) atomicAdd(&g_pc_hist[256 + 4096 + blockIdx.x], __builtin_readcyclecounter() - tk0);
+#endif
   if (!active) return;
   store_drone_step<R, STREAM ? kAuxWtStream : kAuxWt>(v, n, s, last);
   mark_last_in_ring(v, n);

@@ -63,6 +63,9 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
     for t in range(warm):
         sim.step(acts[t])
     torch.cuda.synchronize()
+    NH = 256 + 3 * 4096
+    if hasattr(sim._lib, "gpd_debug_contact_hist"):     # the stats below cover the timed steps only
+        sim._lib.gpd_debug_contact_hist((ctypes.c_ulonglong * NH)())
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for t in range(warm, n):
@@ -75,7 +78,7 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
     print(f"{case:8s} {us:9.2f} us/step  low drones {lowf:.3f}", flush=True)
     lib = sim._lib
     if hasattr(lib, "gpd_debug_contact_hist"):       # -DGPD_CONTACT_STATS build
-        h = (ctypes.c_ulonglong * 128)()
+        h = (ctypes.c_ulonglong * NH)()
         lib.gpd_debug_contact_hist(h)
         it = np.array(h[:51])
         la = np.array(h[51:116])
@@ -86,6 +89,15 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
             if h[122]:
                 print(f"   shader cycles: setup {h[120] / it.sum():.0f} per solve, loop {h[121] / h[122]:.0f} per "
                       f"iteration ({h[121] / it.sum():.0f} per solve)", flush=True)
+        tot = np.array(h[256 + 4096:256 + 8192], dtype=np.float64) / steps
+        if tot.any():
+            pl = np.array(h[256 + 8192:256 + 12288], dtype=np.float64) / steps
+            dcb = np.array(h[256:256 + 4096], dtype=np.float64) / steps
+            order = np.argsort(tot)[::-1][:4]
+            print("   step-kernel cycles per step, slowest blocks: " + "; ".join(
+                f"b{b}: total {tot[b]:.0f} plane {pl[b]:.0f} pair {dcb[b]:.0f}" for b in order) +
+                f"; mean total {tot[tot > 0].mean():.0f} plane {pl[tot > 0].mean():.0f} pair {dcb[tot > 0].mean():.0f}",
+                flush=True)
         if h[124]:
             print(f"   drone contact: broadphase {h[124]} wave-substeps, {h[125] / h[124]:.0f} cycles each; "
                   f"solves {h[116]} ({h[116] / h[124]:.3f} of wave-substeps)", flush=True)
@@ -93,6 +105,15 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
             print(f"   drone contact per solve: setup {h[117] / h[116]:.0f} cycles (pass 1 {h[123] / h[116]:.0f}), "
                   f"iterations {h[119] / h[116]:.2f} x {h[118] / max(h[119], 1):.0f} cycles, "
                   f"near pairs {h[127] / h[116]:.2f}, contacts {h[126] / h[116]:.2f}", flush=True)
+            lg = np.array(h[128:192])
+            print(f"   drone contact solve cycles (log2 buckets): "
+                  f"{dict((f'2^{i}', int(v)) for i, v in enumerate(lg) if v)}", flush=True)
+            di = np.array(h[192:243])
+            print(f"   drone contact iterations hist {dict((i, int(v)) for i, v in enumerate(di) if v)}", flush=True)
+            blk = np.array(h[256:256 + 4096], dtype=np.float64) / steps
+            top = np.sort(blk)[::-1][:4]
+            print(f"   drone contact cycles per step, by block: max {top[0]:.0f} (next {top[1:].round().tolist()}), "
+                  f"mean over blocks {blk[blk > 0].mean() if (blk > 0).any() else 0:.0f}", flush=True)
     sim.close()
 
 
