@@ -62,6 +62,38 @@ __device__ __forceinline__ float g_rsqrt1(float x) {
   const float y = __builtin_amdgcn_rsqf(x);
   return fmaf(y, fmaf(-(0.5f * x) * y, y, 0.5f), y);
 }
+// k / sqrt(x) with g_rsqrt1's one Newton step, the scale folded into the step (one dependent
+// operation fewer than k * g_rsqrt1(x)).  x = 0 gives NaN (0 * inf in the step), not inf.
+__device__ __forceinline__ double g_krsqrt1(double x, double k) {
+  const double y = __builtin_amdgcn_rsq(x), ky = k * y;
+  return fma(ky, fma(-(0.5 * x) * y, y, 0.5), ky);
+}
+__device__ __forceinline__ float g_krsqrt1(float x, float k) {
+  const float y = __builtin_amdgcn_rsqf(x), ky = k * y;
+  return fmaf(ky, fmaf(-(0.5f * x) * y, y, 0.5f), ky);
+}
+// IEEE minNum / maxNum as ONE instruction each (a NaN operand yields the other operand): for
+// operands that are arithmetic results, where fmin / fmax would add canonicalising maxes
+__device__ __forceinline__ double g_min1(double a, double b) {
+  double o;
+  asm("v_min_f64 %0, %1, %2" : "=v"(o) : "v"(a), "v"(b));
+  return o;
+}
+__device__ __forceinline__ double g_max1(double a, double b) {
+  double o;
+  asm("v_max_f64 %0, %1, %2" : "=v"(o) : "v"(a), "v"(b));
+  return o;
+}
+__device__ __forceinline__ float g_min1(float a, float b) {
+  float o;
+  asm("v_min_f32 %0, %1, %2" : "=v"(o) : "v"(a), "v"(b));
+  return o;
+}
+__device__ __forceinline__ float g_max1(float a, float b) {
+  float o;
+  asm("v_max_f32 %0, %1, %2" : "=v"(o) : "v"(a), "v"(b));
+  return o;
+}
 __device__ __forceinline__ float g_rsqrt(float x) {
   float y = __builtin_amdgcn_rsqf(x);
   const float h = 0.5f * x;
@@ -685,8 +717,9 @@ constexpr int kWaveLanes = 64;
 // diagnostic build only: per solving wave, the iterations run [0..50] and the active lanes [51..115];
 // 116..127 drone-contact totals (DcHook / dc_solve); 128..191 log2 histogram of a drone-contact
 // solve's cycles; 192..242 its iteration histogram; 256 + b: block b's drone-contact cycles;
-// 256 + 4096 + b: block b's step-kernel cycles; 256 + 8192 + b: block b's plane-solve cycles
-constexpr int kPcHist = 256 + 3 * 4096;
+// 256 + 4096 + b: block b's step-kernel cycles; 256 + 8192 + b: block b's plane-solve cycles;
+// 256 + 12288 + b: block b's drone-contact rare-path cycles (the hook's solve branch, call included)
+constexpr int kPcHist = 256 + 4 * 4096;
 __device__ unsigned long long g_pc_hist[kPcHist];
 #endif
 // r_p x d for the rim point p (p = 0..3: (cr,0,zc), (0,cr,zc), (-cr,0,zc), (0,-cr,zc)), with the

@@ -309,12 +309,12 @@ template <typename R>
 __device__ __forceinline__ void plane_space(const R n[3], R p[3], R q[3]) {
   if (g_abs(n[2]) > R(0.7071067811865475244008443621048490)) {
     const R a = n[1] * n[1] + n[2] * n[2];
-    const R k = R(1) / g_sqrt(a);
+    const R k = g_rsqrt(a);   // ~2 ulp from 1 / sqrt(a), a third of the instructions
     p[0] = R(0); p[1] = -n[2] * k; p[2] = n[1] * k;
     q[0] = a * k; q[1] = -n[0] * p[2]; q[2] = n[0] * p[1];
   } else {
     const R a = n[0] * n[0] + n[1] * n[1];
-    const R k = R(1) / g_sqrt(a);
+    const R k = g_rsqrt(a);
     p[0] = -n[1] * k; p[1] = n[0] * k; p[2] = R(0);
     q[0] = -n[2] * p[1]; q[1] = n[2] * p[0]; q[2] = a * k;
   }
@@ -324,8 +324,10 @@ __device__ __forceinline__ void plane_space(const R n[3], R p[3], R q[3]) {
 // (oracle/bullet_mb.py pair_geometry).  beta: FISTA's momentum weights (Consts::dc_beta).
 // The rounds run in B's frame (btPlaneSpace1(aB), aB): B's projection is then a radial scaling of
 // (x, y) and a clamp of z, and the selects replace the branches - 26 instead of ~42 dependent
-// operations per round on the one lane that holds the pair.  The oracle projects in world
-// coordinates: the same operations up to rounding (the rounds are non-expansive).
+// operations per round on the one lane that holds the pair.  The clamps are a v_min / v_max pair
+// and the radial factor min(rc / |r|, 1) (one v_min: the factor is below 1 exactly when the point
+// is outside, up to its last bit; |r| = 0 gives NaN, which v_min turns into 1).  The oracle
+// projects in world coordinates: the same operations up to rounding (the rounds are non-expansive).
 template <typename R>
 __device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], const R cb[3], const R ab[3], R r, R hh,
                                               const R* beta, R n[3], R pb[3], R& dist) {
@@ -340,16 +342,15 @@ __device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], cons
   const R margins[4] = {R(0.001), R(0.003), R(0.006), R(0.011)};
   R yx = R(0), yy = R(0), yz = R(0);
   for (int lv = 0; lv < 4; ++lv) {
-    const R mg = margins[lv], rc = r - mg, hc = hh - mg, rc2 = rc * rc;
+    const R mg = margins[lv], rc = r - mg, hc = hh - mg;
     // A's projection of (x, y, z) (the oracle's cyl_project around A)
     auto proj_a = [&](R& x, R& y, R& z) {
       const R dx = x - Lx, dy = y - Ly, dz = z - Lz;
       const R t = pc_dot(dx, dy, dz, Ax, Ay, Az);
-      const R tc = t > hc ? hc : (t < -hc ? -hc : t);
+      const R tc = g_max1(g_min1(t, hc), -hc);
       const R rx = dx - t * Ax, ry = dy - t * Ay, rz = dz - t * Az;
       const R rho2 = pc_dot(rx, ry, rz, rx, ry, rz);
-      const R s = rc * g_rsqrt1(rho2);
-      const R f = rho2 > rc2 ? s : R(1);
+      const R f = g_min1(g_krsqrt1(rho2, rc), R(1));
       x = (Lx + tc * Ax) + rx * f;
       y = (Ly + tc * Ay) + ry * f;
       z = (Lz + tc * Az) + rz * f;
@@ -362,10 +363,9 @@ __device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], cons
       proj_a(px, py, pz);
       // B's projection: radial scaling of (x, y), clamp of z
       const R rho2 = px * px + py * py;
-      const R s = rc * g_rsqrt1(rho2);
-      const R f = rho2 > rc2 ? s : R(1);
+      const R f = g_min1(g_krsqrt1(rho2, rc), R(1));
       px = px * f; py = py * f;
-      pz = pz > hc ? hc : (pz < -hc ? -hc : pz);
+      pz = g_max1(g_min1(pz, hc), -hc);
       const R b = beta[it];
       zx = px + b * (px - yx); zy = py + b * (py - yy); zz = pz + b * (pz - yz);
       yx = px; yy = py; yz = pz;
@@ -375,9 +375,9 @@ __device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], cons
     const R vx = ax - yx, vy = ay - yy, vz = az - yz;
     const R d2 = pc_dot(vx, vy, vz, vx, vy, vz);
     if (d2 > R(1e-4) * R(1e-4)) {
-      const R dc = g_sqrt(d2);
+      const R idc = g_rsqrt(d2), dc = d2 * idc;   // |v| and 1 / |v| within ~2 ulp
       // back to world coordinates: n = (v / |v|) in (bp, bq, ab), y likewise
-      const R ux = vx / dc, uy = vy / dc, uz = vz / dc;
+      const R ux = vx * idc, uy = vy * idc, uz = vz * idc;
       n[0] = (ux * bp[0] + uy * bq[0]) + uz * ab[0];
       n[1] = (ux * bp[1] + uy * bq[1]) + uz * ab[1];
       n[2] = (ux * bp[2] + uy * bq[2]) + uz * ab[2];
@@ -417,8 +417,9 @@ __device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], cons
   dist = -best;
 }
 #ifndef GPD_DC_DIAG
-#define GPD_DC_DIAG 0   // diagnostic builds only (DESIGN.md §9): 1 = broadphase only (no solve compiled),
-                        // 3 = no drone contact, 6 = the solve compiled but never entered
+#define GPD_DC_DIAG 0   // diagnostic builds only (DESIGN.md §8.1): 1 = broadphase only (no solve compiled),
+                        // 3 = no drone contact, 6 = the solve compiled but never entered, 7 = the
+                        // solve called but returning at once, 8 = narrowphase and rows, no iterations
 #endif
 enum { DC_CX, DC_CY, DC_CZ, DC_AX, DC_AY, DC_AZ, DC_PX, DC_PY, DC_PZ, DC_VX, DC_VY, DC_VZ, DC_WX, DC_WY, DC_WZ,
        DC_I00, DC_I01, DC_I02, DC_I11, DC_I12, DC_I22, DC_DLX, DC_DLY, DC_DLZ, DC_DAX, DC_DAY, DC_DAZ, DC_N };
@@ -663,6 +664,10 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
   L.dc[DC_DLX][ln] = R(0); L.dc[DC_DLY][ln] = R(0); L.dc[DC_DLZ][ln] = R(0);
   L.dc[DC_DAX][ln] = R(0); L.dc[DC_DAY][ln] = R(0); L.dc[DC_DAZ][ln] = R(0);
   L.stouch[ln] = 0;
+#if GPD_DC_DIAG == 7
+  wave_lds_sync();
+  return;   // diagnostic build: the call entered, nothing solved
+#endif
   // ---- the near pairs compacted (pair order kept): near pair k to lane k % 64 of pass k / 64, so
   // that one pass of narrowphases covers up to 64 near pairs from any of the block's pair chunks;
   // each contact's rows set up by its lane - pass 0 in the lane's registers, later passes in the
@@ -786,6 +791,10 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
   t2 = __builtin_readcyclecounter();
   int it_used = 0;
 #endif
+#if GPD_DC_DIAG == 8
+  if (true) {   // diagnostic build: narrowphase and rows, no iterations
+  } else
+#endif
   if (maxcnt <= 1 && npass <= 1) {
     // ---- every env has at most one contact: its lane owns both drones' deltas
     R vi[6] = {R(0), R(0), R(0), R(0), R(0), R(0)}, vj[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
@@ -886,9 +895,6 @@ struct DcHook {
 #if GPD_DC_DIAG == 3
     return;   // diagnostic build: no drone contact at all (the hook compiled in, its body not)
 #endif
-#ifdef GPD_CONTACT_STATS
-    const unsigned long long tb = __builtin_readcyclecounter();
-#endif
     DcLds<R>& L = dc_lds<R>();
     const DcPairs& P = dp;
     const int ln = tid & (kWave - 1);
@@ -908,21 +914,15 @@ struct DcHook {
       if (ln == 0) L.nearw[ch] = w;
       any = any || w != 0ull;
     }
-#ifdef GPD_CONTACT_STATS
-    {
-      const unsigned long long te = __builtin_readcyclecounter();
-      if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) {
-        atomicAdd(&g_pc_hist[124], 1ull);
-        atomicAdd(&g_pc_hist[125], te - tb);
-      }
-    }
-#endif
 #if GPD_DC_DIAG == 1
     any = false;   // diagnostic build: broadphase only, no solve
 #elif GPD_DC_DIAG == 6
     any = any && (k.flags & (1 << 29)) != 0;   // diagnostic build: the solve compiled, never entered
 #endif
     if (GPD_RARE(any)) {
+#ifdef GPD_CONTACT_STATS
+      const unsigned long long tr0 = __builtin_readcyclecounter();
+#endif
       // this lane's columns for the solve: pose, velocities, world inverse inertia R diag(1/I) R^T
       const R q00 = k.ijx * Rm[0], q01 = k.ijy * Rm[1], q02 = k.ijz * Rm[2];
       const R q10 = k.ijx * Rm[3], q11 = k.ijy * Rm[4], q12 = k.ijz * Rm[5];
@@ -946,6 +946,9 @@ struct DcHook {
         s.vx = s.vx + L.dc[DC_DLX][ln]; s.vy = s.vy + L.dc[DC_DLY][ln]; s.vz = s.vz + L.dc[DC_DLZ][ln];
         s.wx = s.wx + L.dc[DC_DAX][ln]; s.wy = s.wy + L.dc[DC_DAY][ln]; s.wz = s.wz + L.dc[DC_DAZ][ln];
       }
+#ifdef GPD_CONTACT_STATS
+      if (ln == 0 && blockIdx.x < 4096) atomicAdd(&g_pc_hist[256 + 12288 + blockIdx.x], __builtin_readcyclecounter() - tr0);
+#endif
     }
     wave_lds_sync();   // the centre columns are rewritten by the next substep
   }

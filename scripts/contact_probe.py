@@ -63,7 +63,7 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
     for t in range(warm):
         sim.step(acts[t])
     torch.cuda.synchronize()
-    NH = 256 + 3 * 4096
+    NH = 256 + 4 * 4096
     if hasattr(sim._lib, "gpd_debug_contact_hist"):     # the stats below cover the timed steps only
         sim._lib.gpd_debug_contact_hist((ctypes.c_ulonglong * NH)())
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -98,9 +98,6 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
                 f"b{b}: total {tot[b]:.0f} plane {pl[b]:.0f} pair {dcb[b]:.0f}" for b in order) +
                 f"; mean total {tot[tot > 0].mean():.0f} plane {pl[tot > 0].mean():.0f} pair {dcb[tot > 0].mean():.0f}",
                 flush=True)
-        if h[124]:
-            print(f"   drone contact: broadphase {h[124]} wave-substeps, {h[125] / h[124]:.0f} cycles each; "
-                  f"solves {h[116]} ({h[116] / h[124]:.3f} of wave-substeps)", flush=True)
         if h[116]:
             print(f"   drone contact per solve: setup {h[117] / h[116]:.0f} cycles (pass 1 {h[123] / h[116]:.0f}), "
                   f"iterations {h[119] / h[116]:.2f} x {h[118] / max(h[119], 1):.0f} cycles, "
@@ -114,6 +111,23 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
             top = np.sort(blk)[::-1][:4]
             print(f"   drone contact cycles per step, by block: max {top[0]:.0f} (next {top[1:].round().tolist()}), "
                   f"mean over blocks {blk[blk > 0].mean() if (blk > 0).any() else 0:.0f}", flush=True)
+        # per launch: the slowest block (what the kernel's duration follows) and where its cycles went
+        nps = int(os.environ.get("PROBE_PERSTEP", "40"))
+        rows = []
+        g2 = torch.Generator(device="cuda:0").manual_seed(1)
+        for t in range(nps):
+            a = torch.rand((E, D, 4), generator=g2, device="cuda:0") * 2 - 1 if case in ("crash", "noplane", "multi", "multi2pyb") else acts[t % n]
+            sim.step(a)
+            lib.gpd_debug_contact_hist(h)
+            tb = np.array(h[256 + 4096:256 + 8192], dtype=np.float64)
+            b = int(np.argmax(tb))
+            rows.append((tb[b], h[256 + 8192 + b], h[256 + b], h[256 + 12288 + b],
+                         np.max(np.array(h[256:256 + 4096], dtype=np.float64)), tb.mean()))
+        r = np.array(rows, dtype=np.float64)
+        print(f"   per launch ({nps}): slowest block total {r[:, 0].mean():.0f} (plane {r[:, 1].mean():.0f}, pair solve "
+              f"{r[:, 2].mean():.0f}, pair rare path incl. the solve {r[:, 3].mean():.0f}); mean block total "
+              f"{r[:, 5].mean():.0f}; largest pair-solve cycles of any block {r[:, 4].mean():.0f} (max {r[:, 4].max():.0f})",
+              flush=True)
     sim.close()
 
 

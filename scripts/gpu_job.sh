@@ -8,6 +8,9 @@
 #   pmc_bytes      FETCH_SIZE / WRITE_SIZE passes (separate runs) over the 4096 .. 4M env steps
 #   probe          scripts/contact_probe.py $PROBE_CASES with every library of $LIBS, alternated
 #                  $REPS times (LIBS: names of libgpd_<name>.so, "main" = libgpd.so)
+#   probe_trace    rocprofv3 --kernel-trace --stats of contact_probe.py $PROBE_CASES for each library of $LIBS
+#   pmc_icache     SQC I-cache and FETCH_SIZE / WRITE_SIZE passes (separate runs) over the 4096-env
+#                  headline step for each library of $LIBS
 #   pmc_probe      one PMC pass per counter group of $PMC_GROUPS (';'-separated) and library of $LIBS
 #                  over contact_probe.py $PROBE_CASES (PROBE_STEPS / PROBE_WARM shorten it)
 #   ab             bench.py --no-cpu-baseline --steps 300 with every library of $LIBS, alternated
@@ -56,6 +59,22 @@ job_probe() {
       GPD_ALLOW_ABI_MISMATCH=1 GPD_LIB=$(libpath $v) timeout -k 10 300 python -u scripts/contact_probe.py $PROBE_CASES \
         > $OUT/probe_tmp.log 2>&1 || { cat $OUT/probe_tmp.log >> $OUT/probe.log; return 1; }
       quiet < $OUT/probe_tmp.log >> $OUT/probe.log
+    done
+  done
+}
+job_probe_trace() {
+  for v in $LIBS; do
+    GPD_ALLOW_ABI_MISMATCH=1 GPD_LIB=$(libpath $v) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_$v \
+      -o probe --output-format csv -- python3 scripts/contact_probe.py $PROBE_CASES > $OUT/trace_$v.log 2>&1 || return $?
+  done
+}
+job_pmc_icache() {
+  for v in $LIBS; do
+    local k=0
+    for grp in "SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE" FETCH_SIZE WRITE_SIZE; do
+      k=$((k + 1))
+      GPD_ALLOW_ABI_MISMATCH=1 GPD_LIB=$(libpath $v) timeout -s KILL 90 rocprofv3 --pmc $grp -d $OUT/icache_${v}_$k \
+        -o pmc --output-format csv -- python3 scripts/prof_step.py --envs 4096 --steps 40 > $OUT/icache_${v}_$k.log 2>&1 || return $?
     done
   done
 }
