@@ -939,15 +939,35 @@ struct DcHook {
       const R inv_m = k.inv_m, dt = k.dt;
       const DcPairs dpc = P;
       wave_lds_sync();
+#ifdef GPD_CONTACT_STATS
+      const unsigned long long tr1 = __builtin_readcyclecounter();
+#endif
       pk.park();
+#ifdef GPD_CONTACT_STATS
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const unsigned long long tr2 = __builtin_readcyclecounter();
+#endif
       dc_solve<R>(&c, inv_m, dt, ln, dpc);
+#ifdef GPD_CONTACT_STATS
+      const unsigned long long tr3 = __builtin_readcyclecounter();
+#endif
       pk.unpark();
       if (L.stouch[ln]) {
         s.vx = s.vx + L.dc[DC_DLX][ln]; s.vy = s.vy + L.dc[DC_DLY][ln]; s.vz = s.vz + L.dc[DC_DLZ][ln];
         s.wx = s.wx + L.dc[DC_DAX][ln]; s.wy = s.wy + L.dc[DC_DAY][ln]; s.wz = s.wz + L.dc[DC_DAZ][ln];
       }
 #ifdef GPD_CONTACT_STATS
-      if (ln == 0 && blockIdx.x < 4096) atomicAdd(&g_pc_hist[256 + 12288 + blockIdx.x], __builtin_readcyclecounter() - tr0);
+      {
+        const unsigned long long tr4 = __builtin_readcyclecounter();
+        if (ln == 0) {
+          if (blockIdx.x < 4096) atomicAdd(&g_pc_hist[256 + 12288 + blockIdx.x], tr4 - tr0);
+          atomicAdd(&g_pc_hist[244], tr1 - tr0);   // columns for the solve
+          atomicAdd(&g_pc_hist[245], tr2 - tr1);   // park
+          atomicAdd(&g_pc_hist[246], tr3 - tr2);   // the call (the solve included)
+          atomicAdd(&g_pc_hist[247], tr4 - tr3);   // unpark + deltas
+          atomicAdd(&g_pc_hist[248], 1ull);
+        }
+      }
 #endif
     }
     wave_lds_sync();   // the centre columns are rewritten by the next substep
@@ -1210,23 +1230,40 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
 #ifdef GPD_DMA_EARLY
   history_dma();   // diagnostic build: the DMA behind the state loads instead of the first substep
 #endif
-  if (dk.nsub > 1) {
-    substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, dcp);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
-    GPD_STAMP(1);
-#ifndef GPD_DMA_EARLY
-    history_dma();
+#ifndef GPD_PEEL_BULLET
+#define GPD_PEEL_BULLET 0   // A/B builds: 1 = the Bullet flag sets peel the first / last substep too
 #endif
-    for (int it = 1; it < dk.nsub - 1; ++it)
+  if (!GPD_PEEL_BULLET && PF != kPfRuntime && (PF & F_BULLET) != 0) {
+    // Bullet flag sets: ONE copy of the substep (its plane and pair solves are most of the kernel's
+    // code; peeled first / last copies would triple it past the instruction cache the SQC shares
+    // between two CUs).  The world ang_v is a three-register copy here, so every substep makes it.
+    for (int it = 0; it < dk.nsub; ++it) {
+      substep_block<R, MULTI, PF, true>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, dcp);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
+#ifndef GPD_DMA_EARLY
+      if (it == 0) history_dma();
+#endif
+    }
+  } else {
+    if (dk.nsub > 1) {
       substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, dcp);
-  }
-  substep_block<R, MULTI, PF, true>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, dcp);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) last[k] = rpm[k];
+      for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
+      GPD_STAMP(1);
 #ifndef GPD_DMA_EARLY
-  if (dk.nsub == 1) history_dma();
+      history_dma();
 #endif
+      for (int it = 1; it < dk.nsub - 1; ++it)
+        substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, dcp);
+    }
+    substep_block<R, MULTI, PF, true>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, dcp);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) last[k] = rpm[k];
+#ifndef GPD_DMA_EARLY
+    if (dk.nsub == 1) history_dma();
+#endif
+  }
   GPD_STAMP(2);
   // final readback (:374) -> obs / reward / done
   R qn[4], Rm[9];

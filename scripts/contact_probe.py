@@ -102,6 +102,10 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
             print(f"   drone contact per solve: setup {h[117] / h[116]:.0f} cycles (pass 1 {h[123] / h[116]:.0f}), "
                   f"iterations {h[119] / h[116]:.2f} x {h[118] / max(h[119], 1):.0f} cycles, "
                   f"near pairs {h[127] / h[116]:.2f}, contacts {h[126] / h[116]:.2f}", flush=True)
+            if h[248]:
+                print(f"   rare path per call: columns {h[244] / h[248]:.0f}, park {h[245] / h[248]:.0f}, call "
+                      f"{h[246] / h[248]:.0f} (solve {(h[117] + h[118]) / h[116]:.0f}), unpark + deltas "
+                      f"{h[247] / h[248]:.0f} cycles", flush=True)
             lg = np.array(h[128:192])
             print(f"   drone contact solve cycles (log2 buckets): "
                   f"{dict((f'2^{i}', int(v)) for i, v in enumerate(lg) if v)}", flush=True)
