@@ -385,6 +385,9 @@ __device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], cons
               wz = (yx * bp[2] + yy * bq[2]) + yz * ab[2];
       pb[0] = cb[0] + (wx + n[0] * mg); pb[1] = cb[1] + (wy + n[1] * mg); pb[2] = cb[2] + (wz + n[2] * mg);
       dist = dc - R(2) * mg;
+#ifdef GPD_CONTACT_STATS
+      atomicAdd(&g_pc_hist[249 + lv], 1ull);   // narrowphases ending at margin level lv
+#endif
       return;
     }
   }
@@ -415,6 +418,9 @@ __device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], cons
     }
   }
   dist = -best;
+#ifdef GPD_CONTACT_STATS
+  atomicAdd(&g_pc_hist[253], 1ull);   // narrowphases ending in the least-overlap fallback
+#endif
 }
 #ifndef GPD_DC_DIAG
 #define GPD_DC_DIAG 0   // diagnostic builds only: 1 = broadphase only (no solve compiled),
@@ -1230,6 +1236,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
 #ifdef GPD_DMA_EARLY
   history_dma();   // diagnostic build: the DMA behind the state loads instead of the first substep
 #endif
+#ifndef GPD_DC_DMA_LATE
+#define GPD_DC_DMA_LATE 1   // A/B builds: 1 = multi-drone Bullet kernels issue the history DMA after the
+                            // substeps (a drone-contact call waits for every memory operation in flight)
+#endif
 #ifndef GPD_PEEL_BULLET
 #define GPD_PEEL_BULLET 0   // A/B builds: 1 = the Bullet flag sets peel the first / last substep too
 #endif
@@ -1242,9 +1252,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
 #pragma unroll
       for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
 #ifndef GPD_DMA_EARLY
-      if (it == 0) history_dma();
+      if (it == 0 && !(MULTI && GPD_DC_DMA_LATE)) history_dma();
 #endif
     }
+#ifndef GPD_DMA_EARLY
+    if (MULTI && GPD_DC_DMA_LATE) history_dma();
+#endif
   } else {
     if (dk.nsub > 1) {
       substep_block<R, MULTI, PF, false>(s, rpm, W, last, c, dk, sx, sy, sz, tid, base, D, v.dw_pairs, spair, dcp);

@@ -106,6 +106,7 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
                 print(f"   rare path per call: columns {h[244] / h[248]:.0f}, park {h[245] / h[248]:.0f}, call "
                       f"{h[246] / h[248]:.0f} (solve {(h[117] + h[118]) / h[116]:.0f}), unpark + deltas "
                       f"{h[247] / h[248]:.0f} cycles", flush=True)
+            print(f"   narrowphase levels: {[int(x) for x in h[249:253]]}, least-overlap fallback {h[253]}", flush=True)
             lg = np.array(h[128:192])
             print(f"   drone contact solve cycles (log2 buckets): "
                   f"{dict((f'2^{i}', int(v)) for i, v in enumerate(lg) if v)}", flush=True)
