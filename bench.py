@@ -67,13 +67,17 @@ def pmc_traffic(grid, precision):
 
 def instruction_fetch_bytes(kernel, grid):
     """FETCH_SIZE bytes per launch that are instruction fetch (SQC I-cache misses x the FETCH_SIZE
-    per miss of scripts/ubench/ifetch_probe.hip), from profiles/r3/icache/calibration.json."""
-    f = os.path.join(ROOT, "profiles", "r3", "icache", "calibration.json")
-    try:
-        k = json.load(open(f))["step_kernels"][kernel]
-    except Exception:
-        return None
-    return k["instruction_fetch_size_bytes"] if k.get("grid") == grid else None
+    per miss of scripts/ubench/ifetch_probe.hip), from the newest profiles/r*/icache/calibration.json."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "icache", "calibration.json"))):
+        try:
+            k = json.load(open(f))["step_kernels"][kernel]
+        except Exception:
+            continue
+        if k.get("grid") == grid:
+            best = k["instruction_fetch_size_bytes"]
+    return best
 
 
 def rocprof_kernel_us(kernel, grid, precision):
