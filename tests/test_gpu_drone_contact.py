@@ -105,6 +105,20 @@ def _cube(rng):
     return raw
 
 
+def _ground_stack():
+    """Four drones at the plane: one resting on another that rests on the plane, and one falling onto
+    a grounded drone beside them (pair and plane contacts of one env, the sequential split)."""
+    from oracle.params import derived
+    hh = derived("cf2x")["collision_h"] / 2
+    raw = np.zeros((4, 20))
+    raw[0:4, 0:3] = [[0, 0, hh], [0.01, 0.005, 3 * hh - 0.0005], [0.1195, 0, hh], [0.1195, 0.01, 3 * hh + 0.01]]
+    raw[3, 7:10] = [0, 0, -0.5]
+    raw[1, 10:13] = [0.5, -0.3, 0.2]
+    raw[:, 6] = 1.0
+    raw[:, 16:20] = HOVER
+    return raw
+
+
 def _pyb():
     from gym_pybullet_drones_routing_amd.enums import Physics
     return Physics.PYB
@@ -157,26 +171,40 @@ def test_drone_contact_counts_beyond_d():
         assert len(cons) > D
 
 
-@pytest.mark.parametrize("D", [2, 3, 4])
-def test_drone_contact_step_kernel_resynced(D):
-    """The Physics.PYB flag-set step kernel (MultiHoverAviary's default physics; the parked call)."""
+@pytest.mark.parametrize("case", ["2", "3", "4", "4-ground", "8"])
+def test_drone_contact_step_kernel_resynced(case):
+    """The Physics.PYB flag-set step kernel (MultiHoverAviary's default physics; the parked call, one
+    copy of the substep, the history DMA after the substeps) for D = 2, 3, 4, for a stack on the plane
+    (pair and plane contacts together) and for two 2 x 2 x 2 stacks of 8 (near pairs compacted over
+    the lanes, several Gauss-Seidel levels).  Not with the downwash: the reference's
+    _downwash (BaseAviary.py:785-811) scales as (r_prop / 4 dz)^2 for ANY drone above another within
+    10 m, so drones in contact (|dz| < 2.5 cm) or at rounding-level height differences push each
+    other with tens to 1e30 N, and a control step amplifies rounding differences beyond any gate
+    (scripts/dbg_dc8.py: the same stacks without the pair contact fail the same way)."""
     from gym_pybullet_drones_routing_amd.enums import ActionType
-    raw0 = {2: _scenarios, 3: _triples, 4: _pile6}[D]()
+    D = int(case.split("-")[0])
+    physics, aero, lo, hi = _pyb(), (), -0.2, 0.2
+    if case == "4-ground":
+        raw0, lo, hi = _ground_stack(), -1.0, -0.9      # ~0.95 hover RPM: the stacks stay down
+    elif case == "8":
+        raw0 = np.concatenate([_cube(np.random.default_rng(3)) for _ in range(2)])
+    else:
+        raw0 = {2: _scenarios, 3: _triples, 4: _pile6}[D]()
     n = raw0.shape[0]
-    env = RefAviary(num_drones=n, task="none", integrator="bullet", act="rpm", drones_per_env=D)
+    env = RefAviary(num_drones=n, task="none", integrator="bullet", act="rpm", drones_per_env=D, aero=aero)
     env.set_raw_state(raw0)
-    sim = _sim(n_envs=n // D, drones_per_env=D, task="none", precision="f64", physics=_pyb(), act=ActionType.RPM)
+    sim = _sim(n_envs=n // D, drones_per_env=D, task="none", precision="f64", physics=physics, act=ActionType.RPM)
     sim.reset()
     rng = np.random.default_rng(5)
     errs = []
     for t in range(12):
-        a = rng.uniform(-0.2, 0.2, (n, 4)).astype(np.float32)
+        a = rng.uniform(lo, hi, (n, 4)).astype(np.float32)
         sim.set_raw_state(oracle_raw(env))
         sim.step(torch.from_numpy(a.reshape(n // D, D, 4)).cuda())
         env.step(a)
         errs.append(state_rel_err(sim.raw_state().cpu().numpy()[None, :, :16], oracle_raw(env)[None, :, :16])[0])
     err = np.array(errs)
-    print(f"\n[parity] drone contact, PYB step kernel D={D}: max {err.max():.3e}")
+    print(f"\n[parity] drone contact, Bullet step kernel {case}: max {err.max():.3e}")
     assert err.max() <= 1e-10
     sim.close()
 
