@@ -29,10 +29,11 @@ NODC = ("no_drone_contact",) if os.environ.get("GPD_PROBE_NODC") == "1" else ()
 
 def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.environ.get("PROBE_STEPS", 200))):
     aero = ("no_plane",) if case == "noplane" else ()
-    if case in ("multi", "multifly"):    # bench.py's PYB_GND_DRAG_DW row: 512 MultiHover envs x 8 drones, staggered
-        E, D = 512, 8
+    if case in ("multi", "multifly", "multi8pyb"):    # bench.py's PYB_GND_DRAG_DW row: 512 MultiHover envs x 8
+        E, D = 512, 8                                 # drones, staggered (multi8pyb: the same on Physics.PYB)
         sim = BatchedAviarySim(n_envs=E, drones_per_env=D, task="multihover", act=ActionType.RPM,
-                               physics=Physics.PYB_GND_DRAG_DW, initial_xyzs=STAG, device="cuda:0", aero=NODC)
+                               physics=Physics.PYB if case == "multi8pyb" else Physics.PYB_GND_DRAG_DW,
+                               initial_xyzs=STAG, device="cuda:0", aero=NODC)
     elif case == "multi2pyb":   # MultiHoverAviary's default: 2 drones, Physics.PYB (examples/learn.py --multiagent)
         E, D = 2048, 2
         sim = BatchedAviarySim(n_envs=E, drones_per_env=D, task="multihover", act=ActionType.RPM,
@@ -54,7 +55,7 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
         else:
             sim = BatchedAviarySim(n_envs=E, act=ActionType.RPM, physics=Physics.PYB, aero=aero, **kw)
     n = warm + steps
-    if case in ("crash", "noplane", "multi", "multi2pyb"):
+    if case in ("crash", "noplane", "multi", "multi2pyb", "multi8pyb"):
         acts = torch.rand((n, E, D, 4), generator=g, device="cuda:0", dtype=torch.float32) * 2 - 1
     elif case == "rest":
         acts = torch.full((n, E, D, 4), -1.0, device="cuda:0")      # 0.95 hover RPM: sinks and rests
@@ -121,7 +122,7 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
         rows = []
         g2 = torch.Generator(device="cuda:0").manual_seed(1)
         for t in range(nps):
-            a = torch.rand((E, D, 4), generator=g2, device="cuda:0") * 2 - 1 if case in ("crash", "noplane", "multi", "multi2pyb") else acts[t % n]
+            a = torch.rand((E, D, 4), generator=g2, device="cuda:0") * 2 - 1 if case in ("crash", "noplane", "multi", "multi2pyb", "multi8pyb") else acts[t % n]
             sim.step(a)
             lib.gpd_debug_contact_hist(h)
             tb = np.array(h[256 + 4096:256 + 8192], dtype=np.float64)
