@@ -660,7 +660,7 @@ template <typename R>
 __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln, DcPairs dp) {
 #ifdef GPD_CONTACT_STATS
   const unsigned long long t0 = __builtin_readcyclecounter();
-  unsigned long long t1 = t0, t2 = t0;
+  unsigned long long t1 = t0, t2 = t0, t_np = t0;
   int n_near = 0;
 #endif
   DcLds<R>& L = dc_lds<R>();
@@ -705,17 +705,22 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
     wave_lds_sync();
     const int k = ps * kWave + ln;
     bool con = false;
+    const int p = L.nsp[ln], pij = L.nsij[ln];
+    const int i = pij & 255, j = pij >> 8;
+    R n[3], pb[3], dist;
     if (k < nnear) {
 #ifdef GPD_CONTACT_STATS
       ++n_near;
 #endif
-      const int p = L.nsp[ln], pij = L.nsij[ln];
-      const int i = pij & 255, j = pij >> 8;
       const R ca[3] = {L.dc[DC_CX][i], L.dc[DC_CY][i], L.dc[DC_CZ][i]}, aa[3] = {L.dc[DC_AX][i], L.dc[DC_AY][i], L.dc[DC_AZ][i]};
       const R cb[3] = {L.dc[DC_CX][j], L.dc[DC_CY][j], L.dc[DC_CZ][j]}, ab[3] = {L.dc[DC_AX][j], L.dc[DC_AY][j], L.dc[DC_AZ][j]};
-      R n[3], pb[3], dist;
       pair_geometry(ca, aa, cb, ab, c.cyl_r, c.cyl_hh, c.dc_beta, n, pb, dist);
       con = dist < c.brk;
+    }
+#ifdef GPD_CONTACT_STATS
+    if (ps == 0) t_np = __builtin_readcyclecounter();   // narrowphases of pass 0 done
+#endif
+    {
       if (con) {
         DcRow<R> w;
         dc_row_setup(L, i, j, n, pb, dist, c, inv_m, idt, w);
@@ -879,6 +884,7 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
       atomicAdd(&g_pc_hist[118], t3 - t2);
       atomicAdd(&g_pc_hist[119], (unsigned long long)it_used);
       atomicAdd(&g_pc_hist[123], t1 - t0);
+      atomicAdd(&g_pc_hist[254], t_np - t0);   // to the end of pass 0's narrowphases
       atomicAdd(&g_pc_hist[126], (unsigned long long)nc);
       atomicAdd(&g_pc_hist[127], (unsigned long long)tot);
       const unsigned long long cyc = t3 - t0;

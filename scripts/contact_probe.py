@@ -107,6 +107,7 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
                 print(f"   rare path per call: columns {h[244] / h[248]:.0f}, park {h[245] / h[248]:.0f}, call "
                       f"{h[246] / h[248]:.0f} (solve {(h[117] + h[118]) / h[116]:.0f}), unpark + deltas "
                       f"{h[247] / h[248]:.0f} cycles", flush=True)
+            print(f"   pass 0 narrowphases end at {h[254] / h[116]:.0f} cycles per solve", flush=True)
             print(f"   narrowphase levels: {[int(x) for x in h[249:253]]}, least-overlap fallback {h[253]}", flush=True)
             lg = np.array(h[128:192])
             print(f"   drone contact solve cycles (log2 buckets): "
