@@ -183,17 +183,19 @@ def test_drone_contact_step_kernel_resynced(case):
     (scripts/dbg_dc8.py: the same stacks without the pair contact fail the same way)."""
     from gym_pybullet_drones_routing_amd.enums import ActionType
     D = int(case.split("-")[0])
-    physics, aero, lo, hi = _pyb(), (), -0.2, 0.2
+    physics, aero, lo, hi, tuning = _pyb(), (), -0.2, 0.2, None
     if case == "4-ground":
         raw0, lo, hi = _ground_stack(), -1.0, -0.9      # ~0.95 hover RPM: the stacks stay down
-    elif case == "8":
-        raw0 = np.concatenate([_cube(np.random.default_rng(3)) for _ in range(2)])
+    elif case == "8":     # eight stacks in one 64-drone block: 224 pairs, several 64-pair passes
+        raw0 = np.concatenate([_cube(np.random.default_rng(3 + k)) for k in range(8)])
+        tuning = {"drones_per_block": 64}
     else:
         raw0 = {2: _scenarios, 3: _triples, 4: _pile6}[D]()
     n = raw0.shape[0]
     env = RefAviary(num_drones=n, task="none", integrator="bullet", act="rpm", drones_per_env=D, aero=aero)
     env.set_raw_state(raw0)
-    sim = _sim(n_envs=n // D, drones_per_env=D, task="none", precision="f64", physics=physics, act=ActionType.RPM)
+    sim = _sim(n_envs=n // D, drones_per_env=D, task="none", precision="f64", physics=physics, act=ActionType.RPM,
+               tuning=tuning)
     sim.reset()
     rng = np.random.default_rng(5)
     errs = []
