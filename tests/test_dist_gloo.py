@@ -244,6 +244,7 @@ def _learner_worker(rank, world, port, q, ack):
         if rank == 0:
             q.put((out, pars, f0))
             ack.wait(60)          # keep the queue's feeder alive until the parent has read it
+        dist.barrier()            # neither rank tears the group down while the other still uses it
     finally:
         dist.destroy_process_group()
 
