@@ -139,16 +139,78 @@ def make_env(multiagent, n_envs, act, physics, device, seed=0, distributed=False
                         distributed=distributed)
 
 
+class GraphedMinibatch:
+    """One PPO minibatch step (forward, clipped surrogate + value loss, backward, grad-norm clip,
+    Adam) captured in a hipGraph: the ~100 small kernels of the eager step replay without a host
+    launch each (world == 1; the per-rank learners' all-reduce stays eager).  The minibatch is
+    gathered into static buffers outside the graph.  Capture needs the optimizer's state and the
+    allocator's warm-up: a few eager steps on a side stream, after which the policy's parameters
+    and the optimizer's state are restored to their values from before them (in place: the graph
+    holds those tensors), so the training is the same as the eager loop's."""
+
+    def __init__(self, policy, opt, mb, n_obs, n_act, clip, vf_coef, max_grad_norm, device):
+        self.policy, self.opt = policy, opt
+        self.obs = torch.zeros((mb, n_obs), device=device)
+        self.act = torch.zeros((mb, n_act), device=device)
+        self.logp = torch.zeros(mb, device=device)
+        self.adv = torch.zeros(mb, device=device)
+        self.ret = torch.zeros(mb, device=device)
+        self.clip, self.vf_coef, self.max_grad_norm = clip, vf_coef, max_grad_norm
+        params0 = [p.detach().clone() for p in policy.parameters()]
+        s = torch.cuda.Stream(device=device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                opt.zero_grad(set_to_none=True)
+                self._body()
+        torch.cuda.current_stream(device).wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(self.graph):
+            self._body()
+        with torch.no_grad():                        # undo the warm-up steps, in place
+            for p, p0 in zip(policy.parameters(), params0):
+                p.copy_(p0)
+            for st in opt.state.values():
+                for k, t in st.items():
+                    if torch.is_tensor(t):
+                        t.zero_()                    # Adam's moments and step count start at zero
+
+    def _body(self):
+        # Normal(mu, exp(log_std)).log_prob, written out as torch.distributions computes it (its
+        # argument validation would read a device flag on the host: not capturable)
+        mu = self.policy.pi(self.obs)
+        scale = self.policy.log_std.exp()
+        logp = (-((self.act - mu) ** 2) / (2 * scale ** 2) - scale.log() - math.log(math.sqrt(2 * math.pi))).sum(-1)
+        ratio = (logp - self.logp).exp()
+        ma = (self.adv - self.adv.mean()) / (self.adv.std() + 1e-8)
+        pg = -torch.min(ratio * ma, ratio.clamp(1 - self.clip, 1 + self.clip) * ma).mean()
+        vl = ((self.policy.value(self.obs) - self.ret) ** 2).mean()
+        loss = pg + self.vf_coef * vl
+        loss.backward()
+        nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
+        self.opt.step()
+
+    def step(self, obs, act, logp, adv, ret):
+        self.obs.copy_(obs)
+        self.act.copy_(act)
+        self.logp.copy_(logp)
+        self.adv.copy_(adv)
+        self.ret.copy_(ret)
+        self.graph.replay()
+
+
 def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), lr=3e-4, epochs=10,
           minibatch=16384, gamma=0.99, gae_lambda=0.95, clip=0.2, vf_coef=0.5, max_grad_norm=0.5,
           eval_every=2, seed=0, device="cuda:0", act=DEFAULT_ACT, target_reward=None, max_seconds=None,
-          log=print, physics=Physics.PYB, env=None, world=1, rank=0):
+          log=print, physics=Physics.PYB, env=None, world=1, rank=0, graph=True):
     """PPO on the batched env.  ``env``: an already built torch-output VecEnv (e.g. the
     multi-GPU ``ShardedAviaryVecEnv``); by default one ``AviaryVecEnv`` on ``device``.
     world > 1: per-rank learners under torch.distributed — this rank trains on its own
     ``n_envs`` envs with ``minibatch / world`` samples per minibatch, gradients are averaged over
     the ranks (sync_grads), rank 0 evaluates and decides when every rank stops; ``timesteps``
-    and the history count all ranks' samples."""
+    and the history count all ranks' samples.  ``graph``: the minibatch steps as one captured
+    hipGraph (``GraphedMinibatch``; world == 1 and full minibatches only)."""
     import torch.distributed as dist
     torch.manual_seed(seed)
     physics = Physics(physics)
@@ -168,7 +230,9 @@ def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), l
         broadcast_params(policy)
         torch.manual_seed(seed + 1000003 * rank)   # each rank samples its own actions / minibatches
         minibatch = max(1, minibatch // world)
-    opt = torch.optim.Adam(policy.parameters(), lr=lr, eps=1e-5)
+    graph = graph and world == 1 and torch.device(device).type == "cuda"
+    opt = torch.optim.Adam(policy.parameters(), lr=lr, eps=1e-5, capturable=graph)
+    gstep = GraphedMinibatch(policy, opt, minibatch, n_obs, n_act, clip, vf_coef, max_grad_norm, device) if graph else None
     E = n_envs
     buf_obs = torch.zeros((n_steps, E, n_obs), device=device)
     buf_act = torch.zeros((n_steps, E, n_act), device=device)
@@ -215,6 +279,9 @@ def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), l
             perm = torch.randperm(N, device=device)
             for s in range(0, N, minibatch):
                 idx = perm[s:s + minibatch]
+                if gstep is not None and idx.numel() == minibatch:
+                    gstep.step(b_obs[idx], b_act[idx], b_logp[idx], b_adv[idx], b_ret[idx])
+                    continue
                 d = policy.dist(b_obs[idx])
                 logp = d.log_prob(b_act[idx]).sum(-1)
                 ratio = (logp - b_logp[idx]).exp()
@@ -271,6 +338,8 @@ def parse_args(argv=None):
                         "(without WORLD_SIZE in the env, learn.py starts the ranks itself)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL over xGMI); gloo only to rehearse several ranks on one GPU")
+    p.add_argument("--no-graph", action="store_true",
+                   help="run the PPO minibatch steps eagerly instead of as one captured hipGraph")
     p.add_argument("--learner", default="rank0", choices=["rank0", "per-rank"],
                    help="rank0: one learner on the gathered batch (ShardedAviaryVecEnv); per-rank: a learner "
                         "per GPU on its own env shard, gradients all-reduced")
@@ -318,7 +387,8 @@ def run(a):
             dist.destroy_process_group()
             return
     policy, hist, best, target = train(multiagent=multi, n_envs=a.n_envs, total_timesteps=int(a.total_timesteps),
-                                       max_seconds=a.max_seconds, physics=Physics(a.physics), device=device, env=env)
+                                       max_seconds=a.max_seconds, physics=Physics(a.physics), device=device, env=env,
+                                       graph=not a.no_graph)
     out = {"multiagent": multi, "physics": a.physics, "n_envs": a.n_envs, "gpus": world, "target_reward": target,
            "best_eval_return": best, "reached": best >= target, "history": hist}
     print(json.dumps({k: v for k, v in out.items() if k != "history"}), flush=True)

@@ -122,3 +122,43 @@ def test_ppo_per_rank_learners_two_ranks():
     assert [h["timesteps"] for h in hist] == [2 * 64 * 8, 2 * 2 * 64 * 8]
     assert all(math.isfinite(h["mean_step_reward"]) and h["eval_len"] >= 1 for h in hist)
     assert math.isfinite(best)
+
+
+def test_graphed_minibatch_matches_eager():
+    """learn.GraphedMinibatch (the PPO minibatch step replayed as one hipGraph) starts from the
+    policy's own weights after its capture warm-up, and five replays track five eager steps (the
+    train() loop's eager form, torch.distributions and a non-capturable Adam) to f32 rounding."""
+    import copy
+
+    import learn
+    import torch
+    torch.manual_seed(0)
+    dev = torch.device("cuda:0")
+    n_obs, n_act, mb, clip, vf_coef, mgn = 12, 4, 256, 0.2, 0.5, 0.5
+    pol_a = learn.ActorCritic(n_obs, n_act).to(dev)
+    pol_b = copy.deepcopy(pol_a)
+    opt_a = torch.optim.Adam(pol_a.parameters(), lr=3e-4, eps=1e-5)
+    opt_b = torch.optim.Adam(pol_b.parameters(), lr=3e-4, eps=1e-5, capturable=True)
+    gstep = learn.GraphedMinibatch(pol_b, opt_b, mb, n_obs, n_act, clip, vf_coef, mgn, dev)
+    for pa, pb in zip(pol_a.parameters(), pol_b.parameters()):
+        assert torch.equal(pa, pb)
+    g = torch.Generator(device=dev).manual_seed(3)
+    for _ in range(5):
+        obs = torch.randn(mb, n_obs, device=dev, generator=g)
+        act = torch.randn(mb, n_act, device=dev, generator=g)
+        logp_old = torch.randn(mb, device=dev, generator=g) - 4.0
+        adv = torch.randn(mb, device=dev, generator=g)
+        ret = torch.randn(mb, device=dev, generator=g)
+        d = pol_a.dist(obs)
+        ratio = (d.log_prob(act).sum(-1) - logp_old).exp()
+        ma = (adv - adv.mean()) / (adv.std() + 1e-8)
+        pg = -torch.min(ratio * ma, ratio.clamp(1 - clip, 1 + clip) * ma).mean()
+        loss = pg + vf_coef * ((pol_a.value(obs) - ret) ** 2).mean()
+        opt_a.zero_grad(set_to_none=True)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(pol_a.parameters(), mgn)
+        opt_a.step()
+        gstep.step(obs, act, logp_old, adv, ret)
+    torch.cuda.synchronize()
+    for pa, pb in zip(pol_a.parameters(), pol_b.parameters()):
+        torch.testing.assert_close(pb, pa, rtol=1e-5, atol=1e-6)
