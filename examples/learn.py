@@ -203,7 +203,7 @@ class GraphedMinibatch:
 def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), lr=3e-4, epochs=10,
           minibatch=16384, gamma=0.99, gae_lambda=0.95, clip=0.2, vf_coef=0.5, max_grad_norm=0.5,
           eval_every=2, seed=0, device="cuda:0", act=DEFAULT_ACT, target_reward=None, max_seconds=None,
-          log=print, physics=Physics.PYB, env=None, world=1, rank=0, graph=True):
+          log=print, physics=Physics.PYB, env=None, world=1, rank=0, graph=False):
     """PPO on the batched env.  ``env``: an already built torch-output VecEnv (e.g. the
     multi-GPU ``ShardedAviaryVecEnv``); by default one ``AviaryVecEnv`` on ``device``.
     world > 1: per-rank learners under torch.distributed — this rank trains on its own
@@ -338,8 +338,10 @@ def parse_args(argv=None):
                         "(without WORLD_SIZE in the env, learn.py starts the ranks itself)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL over xGMI); gloo only to rehearse several ranks on one GPU")
-    p.add_argument("--no-graph", action="store_true",
-                   help="run the PPO minibatch steps eagerly instead of as one captured hipGraph")
+    p.add_argument("--graph", action="store_true",
+                   help="replay each PPO minibatch step as one captured hipGraph (faster update; same "
+                        "arithmetic up to rounding, so a different training trajectory than the default "
+                        "eager loop, which reproduces the recorded runs step for step)")
     p.add_argument("--learner", default="rank0", choices=["rank0", "per-rank"],
                    help="rank0: one learner on the gathered batch (ShardedAviaryVecEnv); per-rank: a learner "
                         "per GPU on its own env shard, gradients all-reduced")
@@ -388,7 +390,7 @@ def run(a):
             return
     policy, hist, best, target = train(multiagent=multi, n_envs=a.n_envs, total_timesteps=int(a.total_timesteps),
                                        max_seconds=a.max_seconds, physics=Physics(a.physics), device=device, env=env,
-                                       graph=not a.no_graph)
+                                       graph=a.graph)
     out = {"multiagent": multi, "physics": a.physics, "n_envs": a.n_envs, "gpus": world, "target_reward": target,
            "best_eval_return": best, "reached": best >= target, "history": hist}
     print(json.dumps({k: v for k, v in out.items() if k != "history"}), flush=True)
