@@ -459,6 +459,10 @@ def other_configs(device, precision, act):
         ("512 MultiHoverAviary x 8 drones, Physics.PYB_GND_DRAG_DW (Bullet step, staggered init)",
          dict(n_envs=512, drones_per_env=8, task="multihover", act=ActionType.RPM, physics=Physics.PYB_GND_DRAG_DW,
               initial_xyzs=stag), 4),
+        ("512 MultiHoverAviary x 8 drones, Physics.PYB (the same staggered batch without the downwash, "
+         "whose (r/4dz)^2 force drives the row above into piles)",
+         dict(n_envs=512, drones_per_env=8, task="multihover", act=ActionType.RPM, physics=Physics.PYB,
+              initial_xyzs=stag), 4),
         ("2048 MultiHoverAviary x 2 drones, Physics.PYB (MultiHoverAviary's default, examples/learn.py "
          "--multiagent's env; drone<->drone and plane contact)",
          dict(n_envs=2048, drones_per_env=2, task="multihover", act=ActionType.RPM, physics=Physics.PYB), 4),
