@@ -338,6 +338,7 @@ def parse_args(argv=None):
                         "(without WORLD_SIZE in the env, learn.py starts the ranks itself)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL over xGMI); gloo only to rehearse several ranks on one GPU")
+    p.add_argument("--seed", type=int, default=0, help="torch seed of the policy, the sampling and the envs")
     p.add_argument("--graph", action="store_true",
                    help="replay each PPO minibatch step as one captured hipGraph (faster update; same "
                         "arithmetic up to rounding, so a different training trajectory than the default "
@@ -390,7 +391,7 @@ def run(a):
             return
     policy, hist, best, target = train(multiagent=multi, n_envs=a.n_envs, total_timesteps=int(a.total_timesteps),
                                        max_seconds=a.max_seconds, physics=Physics(a.physics), device=device, env=env,
-                                       graph=a.graph)
+                                       graph=a.graph, seed=a.seed)
     out = {"multiagent": multi, "physics": a.physics, "n_envs": a.n_envs, "gpus": world, "target_reward": target,
            "best_eval_return": best, "reached": best >= target, "history": hist}
     print(json.dumps({k: v for k, v in out.items() if k != "history"}), flush=True)
