@@ -180,7 +180,7 @@ def test_drone_contact_step_kernel_resynced(case):
     _downwash (BaseAviary.py:785-811) scales as (r_prop / 4 dz)^2 for ANY drone above another within
     10 m, so drones in contact (|dz| < 2.5 cm) or at rounding-level height differences push each
     other with tens to 1e30 N, and a control step amplifies rounding differences beyond any gate
-    (scripts/dbg_dc8.py: the same stacks without the pair contact fail the same way)."""
+    (tests/tools/dbg_dc8.py: the same stacks without the pair contact fail the same way)."""
     from gym_pybullet_drones_routing_amd.enums import ActionType
     D = int(case.split("-")[0])
     physics, aero, lo, hi, tuning = _pyb(), (), -0.2, 0.2, None

@@ -156,7 +156,7 @@ def test_narrowphase_is_fixed_round_accelerated_projection():
     n1, pb1, d1 = pair_geometry(ca + 1e-12, aa, cb, ab, R_, HH)
     assert abs(d1 - d0) < 1e-10 and np.abs(pb1 - pb0).max() < 1e-10
     # accuracy against many plain rounds over random tilted pairs 1 mm+ apart: micrometre-level
-    # (on the contacts recorded from crashing 2- and 8-drone envs - scripts/dc_narrowphase_stats.py -
+    # (on the contacts recorded from crashing 2- and 8-drone envs - tests/tools/dc_narrowphase_stats.py -
     # the 8 accelerated rounds match round 3's 16 plain ones: p90 1.4e-4 vs 1.2e-4 m)
     rng = np.random.default_rng(5)
     mg = CORE_MARGINS[0]

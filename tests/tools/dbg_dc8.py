@@ -6,7 +6,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from gym_pybullet_drones_routing_amd.enums import ActionType, Physics  # noqa: E402
 from oracle.ref_aviary import RefAviary  # noqa: E402
 from tests.oracle_runs import oracle_raw, state_rel_err  # noqa: E402

@@ -2,14 +2,14 @@
 Physics.PYB, U[-1,1] RPM actions, auto-reset), counted in the numpy oracle: near pairs per
 env-substep, margin levels tried and alternating-projection rounds per level, and how long a pair
 stays in contact (persistent contacts are what hold the slowest GPU wave: 8 solves per step).
-Usage: python scripts/dc_narrowphase_stats.py [envs] [steps] [drones]"""
+Usage: python tests/tools/dc_narrowphase_stats.py [envs] [steps] [drones]"""
 import collections
 import os
 import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import oracle.bullet_mb as mb  # noqa: E402
 from tests.oracle_runs import run_vec  # noqa: E402
 
