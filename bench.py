@@ -489,14 +489,16 @@ def _policy_mlp(n_in, n_out):
     return nn.Sequential(nn.Linear(n_in, 64), nn.Tanh(), nn.Linear(64, 64), nn.Tanh(), nn.Linear(64, n_out))
 
 
-def rollout_leg(device, precision, act, E, K=64, reps=8, store_policy=0):
+def rollout_leg(device, precision, act, E, K=64, reps=8, store_policy=2):
     """What an RL caller pays per env.step (the caller: examples/learn.py's PPO rollout, the
     reference's learn.py:52-94 through SB3): ONE hipGraph of K x (actor and critic MLP forward on
     the observation, Normal sample, clamp, gpd_step, the rollout-buffer copies) at E envs, against
     the same graph without gpd_step.  Per step: the whole sequence, the policy part, and their
     difference = the step's cost inside a rollout (its kernel plus the boundary, with the policy's
     kernels between consecutive steps instead of another step), by HIP events over graph replays.
-    ``store_policy``: gpd_config::store_policy (0 = the library's choice)."""
+    ``store_policy``: gpd_config::store_policy (0 = the library's choice); 2 (write-through rows),
+    what examples/learn.py sets: between the policy's kernels it measured 6.12 vs 6.40 us per step
+    against the back-to-back default 3 (five alternations, profiles/r4/rollout_policy/)."""
     from gym_pybullet_drones_routing_amd.enums import ActionType
     from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
     tuning = {"store_policy": store_policy} if store_policy else None

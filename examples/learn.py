@@ -135,8 +135,10 @@ def make_env(multiagent, n_envs, act, physics, device, seed=0, distributed=False
     kw = dict(obs=DEFAULT_OBS, act=act, physics=Physics(physics))
     if multiagent:
         kw["num_drones"] = DEFAULT_AGENTS
+    # store policy 2 (write-through rows): between the policy's kernels the step measured 6.12 vs
+    # 6.40 us (bench.py rollout leg, profiles/r4/rollout_policy/); the back-to-back default is 3
     return make_vec_env(env_cls, env_kwargs=kw, n_envs=n_envs, seed=seed, output="torch", device=device,
-                        distributed=distributed)
+                        distributed=distributed, tuning={"store_policy": 2})
 
 
 class GraphedMinibatch:

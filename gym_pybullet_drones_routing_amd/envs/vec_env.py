@@ -26,7 +26,7 @@ class AviaryVecEnv(_VecEnvBase):
     def __init__(self, num_envs, task="hover", num_drones=1, drone_model=DroneModel.CF2X, initial_xyzs=None,
                  initial_rpys=None, physics=Physics.DYN, aero=(), pyb_freq=240, ctrl_freq=30,
                  obs=ObservationType.KIN, act=ActionType.RPM, precision="f64", device=None, output="numpy",
-                 episode_len_sec=8, urdf_path=None):
+                 episode_len_sec=8, urdf_path=None, tuning=None):
         if ObservationType(obs) != ObservationType.KIN:
             raise NotImplementedError("ObservationType.RGB is out of scope")
         if output not in ("numpy", "torch"):
@@ -37,7 +37,7 @@ class AviaryVecEnv(_VecEnvBase):
                                     urdf_path=urdf_path, pyb_freq=pyb_freq, ctrl_freq=ctrl_freq, act=act,
                                     task=task, physics=physics, aero=aero, precision=precision, autoreset=True,
                                     episode_len_sec=episode_len_sec, initial_xyzs=initial_xyzs,
-                                    initial_rpys=initial_rpys, device=device)
+                                    initial_rpys=initial_rpys, device=device, tuning=tuning)
         self.num_envs = int(num_envs)
         self.num_drones = int(num_drones)
         self.output = output
