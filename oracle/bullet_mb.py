@@ -44,8 +44,8 @@ Bullet's multibody contact constraints solved by projected Gauss-Seidel inside
 ``btMultiBodyConstraintSolver`` between the velocity update and ``integrateTransforms``.  The
 contact set is this restatement's own (see ``plane_contact``).  Drone <-> drone collisions
 (cylinder vs cylinder, MultiHoverAviary's drones, ``:486-491``) are restated as ``drone_contact``:
-one contact per pair (every pair in contact, no cap) from the margin-shrunk cores' closest points
-(FISTA-accelerated alternating projection from B's centre), solved with the same rows between two moving bodies before the plane solve.  Bit-level rounding of Bullet's own
+one contact per pair (every pair in contact, no cap) from the margin-shrunk cores' converged closest
+points, solved with the same rows between two moving bodies before the plane solve.  Bit-level rounding of Bullet's own
 operation order (the world <-> base round trips of the link forces, the 6x6 inverse of the
 articulated inertia) is not reproduced either; the restatement is exact in exact arithmetic.
 
@@ -301,34 +301,26 @@ def plane_contact(pos, rot_bw, vel_w, omega_w, m, inertia, dt, radius, half_heig
 
 # ---------------------------------------------------------------------------- drone <-> drone contact
 # MultiHoverAviary's drones are colliding Bullet bodies (BaseAviary.py:486-491, stepped together
-# by :369-370).  Bullet finds a cylinder pair's contact with GJK / EPA and keeps it in a persistent
-# manifold; this restatement's own deterministic contact set (parity unpinned, like the plane's):
-# one point per pair per step from the closest points of the two cylinders' margin-shrunk cores,
-# found by a fixed number of FISTA-accelerated alternating-projection rounds from B's centre.
+# by :369-370).  Bullet finds a cylinder pair's contact with GJK / EPA (to a distance tolerance) and
+# keeps it in a persistent manifold; this restatement's own deterministic contact set (parity
+# unpinned, like the plane's): one point per pair per step, the CONVERGED closest points of the two
+# cylinders' margin-shrunk cores (``core_pair``: every feature pair the closest points can lie on,
+# each minimised to rounding - DESIGN.md §2.3).
 # (Continuing a pair from its previous substep's point, as Bullet's persistent manifold does with
-# its points, was measured and rejected: on flat faces every point of the overlap is a fixed point
-# of the projections, so the single contact point drifts with the bodies and tips a drone resting
-# on another one over - DESIGN.md §2.3.)
+# its points, was measured and rejected in round 3: on flat faces every point of the overlap is a
+# closest point, so the single contact point drifted with the bodies and tipped a drone resting on
+# another one over - DESIGN.md §2.3.)
 FRICTION_DD = 0.5 * 0.5     # drone x drone combined friction (btCollisionObject default 0.5 each)
-PAIR_COLD = 8               # accelerated alternating-projection rounds from B's centre
 CORE_MARGINS = (0.001, 0.003, 0.006, 0.011)   # core shrink per level (the first = the URDF margin)
 CORE_SEP = 1e-4             # core distance below which a level has no well-conditioned normal
 SAT_SLACK = 1e-9            # the broadphase's separating-axis reject keeps this much against rounding
 SIMDSQRT12 = 0.7071067811865475244008443621048490
-
-
-def fista_momentum(k):
-    """FISTA's momentum weights beta_0..beta_{k-1}: t_0 = 1, t_{i+1} = (1 + sqrt(1 + 4 t_i^2)) / 2,
-    beta_i = (t_i - 1) / t_{i+1} (beta_0 = 0)."""
-    out, t = [], 1.0
-    for _ in range(k):
-        tn = (1.0 + math.sqrt(1.0 + 4.0 * t * t)) / 2.0
-        out.append((t - 1.0) / tn)
-        t = tn
-    return tuple(out)
-
-
-PAIR_BETA = fista_momentum(PAIR_COLD)
+RIM_SAMPLES = 8             # start azimuths per rim circle (k * 45 deg in btPlaneSpace1 of the axis)
+RIM_ITERS = 10              # trust-region Newton steps per rim circle
+RIM_ACCEPT = 1e-10          # a step must lower the squared distance by this fraction (rounding-proof)
+PAIR_TIE = 1e-10            # a later candidate wins only when it is closer by more than this (m)
+RIM_COS = tuple(math.cos(2.0 * math.pi * k / RIM_SAMPLES) for k in range(RIM_SAMPLES))
+RIM_SIN = tuple(math.sin(2.0 * math.pi * k / RIM_SAMPLES) for k in range(RIM_SAMPLES))
 
 
 def plane_space(n):
@@ -396,39 +388,155 @@ def cyl_extent_cos(ua, radius, half_height):
     return half_height * abs(ua) + radius * math.sqrt(max(0.0, 1.0 - ua * ua))
 
 
-def pair_geometry(ca, aa, cb, ab, radius, half_height):
+def axial_project(x, r, h):
+    """Closest point of the solid cylinder (centre 0, axis z, radius r, half-height h) to x."""
+    rho2 = x[0] * x[0] + x[1] * x[1]
+    f = r / math.sqrt(rho2) if rho2 > r * r else 1.0
+    return np.array([x[0] * f, x[1] * f, min(max(x[2], -h), h)])
+
+
+def _rim_eval(C, e1, e2, c, s, r, h):
+    """Rim point P = C + r (c e1 + s e2) (c^2 + s^2 = 1) against the axial cylinder: the squared
+    distance f, and with phi the rim angle, f'/2 = e.P' and f''/2 = ((I - J) P').P' + e.P'' (e = P -
+    proj(P), J = the projection's Jacobian: the radial scaling (r/rho)(I - rr^T) in xy outside the
+    radius, 0 in z beyond the caps)."""
+    u = c * e1 + s * e2
+    d1 = r * (c * e2 - s * e1)                       # P'
+    P = C + r * u
+    rho2 = P[0] * P[0] + P[1] * P[1]
+    Q = axial_project(P, r, h)
+    e = P - Q
+    f = float(e @ e)
+    g = float(e @ d1)
+    m0 = m1 = m2 = 0.0
+    if rho2 > r * r:
+        rho = math.sqrt(rho2)
+        k = r / rho
+        rt = (P[0] * d1[0] + P[1] * d1[1]) / rho2
+        m0 = d1[0] - k * (d1[0] - rt * P[0])
+        m1 = d1[1] - k * (d1[1] - rt * P[1])
+    if abs(P[2]) > h:
+        m2 = d1[2]
+    hh = (m0 * d1[0] + m1 * d1[1] + m2 * d1[2]) - r * float(e @ u)    # P'' = -r u
+    return f, g, hh, P, Q
+
+
+def rim_closest(C, e1, e2, r, h):
+    """The point of the rim circle (centre C, orthonormal in-plane basis e1, e2, radius r) closest to
+    the axial cylinder (centre 0, axis z, radius r, half-height h), and that cylinder's point.
+    The rim's distance is not convex in the angle (two local minima on nearly parallel stacked
+    faces), so: RIM_SAMPLES azimuths, the best as the start (ties keep the earlier), then RIM_ITERS
+    trust-region Newton steps on the angle (tangent step c' = c - d s, s' = s + d c, renormalised; a
+    step is kept only when it lowers the squared distance by the fraction RIM_ACCEPT - rounding noise
+    never moves the point - and the radius doubles, up to 1 rad, else it shrinks to |d| / 4)."""
+    best_f, bc, bs = math.inf, 1.0, 0.0
+    for k in range(RIM_SAMPLES):
+        P = C + r * (RIM_COS[k] * e1 + RIM_SIN[k] * e2)
+        e = P - axial_project(P, r, h)
+        f = float(e @ e)
+        if f < best_f * (1.0 - RIM_ACCEPT):
+            best_f, bc, bs = f, RIM_COS[k], RIM_SIN[k]
+    c, s = bc, bs
+    f, g, hh, P, Q = _rim_eval(C, e1, e2, c, s, r, h)
+    rad = math.pi / RIM_SAMPLES
+    for _ in range(RIM_ITERS):
+        d = -g / hh if hh > 0.0 else -math.copysign(rad, g)
+        d = min(max(d, -rad), rad)
+        c2, s2 = c - d * s, s + d * c
+        k = 1.0 / math.sqrt(c2 * c2 + s2 * s2)
+        c2, s2 = c2 * k, s2 * k
+        f2, g2, hh2, P2, Q2 = _rim_eval(C, e1, e2, c2, s2, r, h)
+        if f2 < f * (1.0 - RIM_ACCEPT):
+            c, s, f, g, hh, P, Q = c2, s2, f2, g2, hh2, P2, Q2
+            rad = min(2.0 * rad, 1.0)
+        else:
+            rad = abs(d) * 0.25
+    return P, Q
+
+
+def segment_closest(L, A, h):
+    """Closest points of the axis segments L + s A and t z, s, t in [-h, h] (A, z unit)."""
+    b = float(A[2])
+    dd = float(A @ L)
+    e = float(L[2])
+    den = 1.0 - b * b
+    s = (b * e - dd) / den if den > 1e-12 else 0.0
+    s = min(max(s, -h), h)
+    t = min(max(b * s + e, -h), h)
+    s = min(max(b * t - dd, -h), h)
+    return L + s * A, np.array([0.0, 0.0, t])
+
+
+def core_pair(L, A, r, h):
+    """Closest points (x on A, y on B) of two solid cylinders of radius r and half-height h in B's
+    frame: B centred at 0 with axis z, A centred at L with unit axis A.  The closest points of two
+    separated cylinders lie on a rim of one of them (against any feature of the other), or on both
+    lateral surfaces (the axes' closest points interior); every other feature pair (face-face,
+    face-lateral) shares its distance with a rim point.  So the distance is the smallest of:
+      0/1. the near caps' centres against the other cylinder (level stacks: the centred point);
+      2.   the lateral surfaces along the axes' closest points (closed form; level side-by-side
+           pairs: the point at mid-height);
+      3-6. the four rim circles against the other cylinder (rim_closest, the caps facing the other
+           cylinder first; B's rims in A's frame, btPlaneSpace1 of A);
+    each candidate a feasible pair (an upper bound), taken in that order, a later one only when it
+    is closer by more than PAIR_TIE.  Accuracy against the certified exact distance
+    (tests/tools/np_exact.py): <= 1e-5 m on random, side-by-side, rim-to-rim and stacked pairs
+    (tests/test_oracle_drone_contact.py).  Overlapping cores give a distance <= CORE_SEP (a rim or
+    a cap centre inside the other core)."""
+    ap, aq = plane_space(A)
+    Ma = np.stack([ap, aq, A])                        # B's frame -> A's frame
+    Lb = Ma @ (-L)                                    # B's centre and axis in A's frame
+    Bz = Ma[:, 2].copy()
+    bp, bq = plane_space(Bz)
+    sa = -1.0 if float(L @ A) > 0.0 else 1.0          # A's cap facing B
+    sb = 1.0 if L[2] >= 0.0 else -1.0                 # B's cap facing A
+    cands = []
+    xa = L + sa * h * A
+    cands.append((xa, axial_project(xa, r, h)))
+    yb = Lb + sb * h * Bz                             # in A's frame
+    cands.append((Ma.T @ axial_project(yb, r, h) + L, Ma.T @ yb + L))
+    pa, pb = segment_closest(L, A, h)
+    w = pa - pb
+    wn = math.sqrt(float(w @ w))
+    if wn > 1e-12:
+        u = w / wn
+        cands.append((cyl_project(L, A, r, h, pa - r * u), axial_project(pb + r * u, r, h)))
+    for sg, sgb in ((sa, sb), (-sa, -sb)):
+        cands.append(rim_closest(L + sg * h * A, ap, aq, r, h))
+        yb, xa_ = rim_closest(Lb + sgb * h * Bz, bp, bq, r, h)
+        cands.append((Ma.T @ xa_ + L, Ma.T @ yb + L))
+    bx, by = cands[0]
+    bd = math.sqrt(float((bx - by) @ (bx - by)))
+    for x, y in cands[1:]:
+        d = math.sqrt(float((x - y) @ (x - y)))
+        if d < bd - PAIR_TIE:
+            bx, by, bd = x, y, d
+    return bx, by, bd
+
+
+def pair_geometry(ca, aa, cb, ab, radius, half_height, with_margin=False):
     """One contact of cylinders A and B: (normal on B pointing to A, point on B, distance;
-    negative = penetration).  Bullet's margin scheme:
-    the closest points of the CORE cylinders (radius and half-height shrunk by a margin m) give
-    the normal and the distance core_distance - 2 m; the point on B's surface is B's core point +
-    m n.  Core points by PAIR_COLD rounds of alternating projection in B-centred coordinates from
-    B's centre with FISTA momentum (y' = P_B(P_A(z)), z = y' + beta (y' - y)) - a fixed count, no
-    convergence test, so the result is a continuous function of the poses (16 plain rounds, round
-    3's choice, left up to 2 mm of distance error on tilted face-to-face pairs where the plain
-    rounds creep at cos^2 of the faces' angle; 8 accelerated ones reach the same accuracy, 16 ten
-    times better) - then the point of A's core closest to B's.  A level whose cores come within CORE_SEP of each
-    other (overlapping or nearly so: no well-conditioned normal) passes to the next, thicker
-    margin (CORE_MARGINS: penetrations up to ~2 cm).  Deeper overlaps: the axis of least overlap
-    among the centre line and the two cylinder axes, at the point the last level reached (Bullet
-    runs EPA here)."""
+    negative = penetration).  Bullet's margin scheme: the closest points of the CORE cylinders
+    (radius and half-height shrunk by a margin m) give the normal and the distance core_distance -
+    2 m; the point on B's surface is B's core point + m n.  Core points by ``core_pair`` in B's frame
+    (btPlaneSpace1(aB), aB), converged to rounding.  A level whose cores come within CORE_SEP of each
+    other (overlapping or nearly so: no well-conditioned normal) passes to the next, thicker margin
+    (CORE_MARGINS: penetrations up to ~2 cm).  Deeper overlaps: the axis of least overlap among the
+    centre line and the two cylinder axes, at the point the last level reached (Bullet runs EPA
+    here).  ``with_margin``: also return the margin of the level that gave the contact (None for the
+    least-overlap fallback)."""
+    bp, bq = plane_space(ab)
+    Mb = np.stack([bp, bq, ab])                       # world -> B's frame
     cl = ca - cb
-    zero = np.zeros(3)
-    y = zero
+    L = Mb @ cl
+    A = Mb @ aa
+    y = np.zeros(3)
     for mg in CORE_MARGINS:
-        r, h = radius - mg, half_height - mg
-        y = zero.copy()
-        z = zero.copy()
-        for beta in PAIR_BETA:
-            yn = cyl_project(zero, ab, r, h, cyl_project(cl, aa, r, h, z))
-            z = yn + beta * (yn - y)
-            y = yn
-        pa = cyl_project(cl, aa, r, h, y)
-        dv = pa - y
-        d2 = float(dv @ dv)
-        if d2 > CORE_SEP * CORE_SEP:
-            dc = math.sqrt(d2)
-            n = dv / dc
-            return n, cb + (y + n * mg), dc - 2.0 * mg
+        x, y, dc = core_pair(L, A, radius - mg, half_height - mg)
+        if dc > CORE_SEP:
+            n = Mb.T @ ((x - y) / dc)
+            out = (n, cb + (Mb.T @ y + n * mg), dc - 2.0 * mg)
+            return out + (mg,) if with_margin else out
     cands = []
     c2 = float(cl @ cl)
     if c2 > 1e-24:
@@ -440,13 +548,59 @@ def pair_geometry(ca, aa, cb, ab, radius, half_height):
         ov = cyl_extent(u, aa, radius, half_height) + cyl_extent(u, ab, radius, half_height) - float(u @ cl)
         if best is None or ov < best_ov:
             best, best_ov = u, ov
-    return best, cb + y, -best_ov
+    out = (best, cb + Mb.T @ y, -best_ov)
+    return out + (None,) if with_margin else out
+
+
+FACE_COS = SIMDSQRT12       # both near caps' normals within 45 deg of the contact normal: a face contact
+
+
+def face_points(ca, aa, cb, ab, n, radius, half_height, mg):
+    """The face manifold of a cap-to-cap contact: four points spanning the overlap of the two near
+    caps, as (point on B, distance) - a deterministic stand-in for the up-to-4-point persistent
+    manifold Bullet builds over frames (btPersistentManifold, MANIFOLD_CACHE_SIZE 4) for two
+    resting faces, as ``contact_points`` is for the plane.  With one point per pair (the exact
+    closest point, at a rim as soon as the faces tilt) a drone resting on another rocks from rim
+    to rim and sinks ~6 mm into it (tests/test_oracle_drone_contact.py).
+    A face contact: the cores' caps facing each other (A's cap nearer B, outward normal nu_A =
+    +-a_A, and B's, nu_B) with n.nu_B >= FACE_COS and -n.nu_A >= FACE_COS.  In the plane normal to
+    n the two cap discs (radius r of the core at margin mg) overlap in a lens; its four extreme
+    points: the two tips on the line of the cap centres (from B's centre cB: (s - r) u and r u, u
+    the unit centre offset, s its length; u = btPlaneSpace1(n)'s first direction for coaxial caps)
+    and the two corners (s/2) u +- sqrt(r^2 - s^2/4) (n x u).  Each point p is carried along n to
+    B's cap plane (y) and to A's (x); its distance is (x - y).n - 2 mg and its point on B y + mg n.
+    No points when the caps do not overlap (s >= 2 r)."""
+    r, h = radius - mg, half_height - mg
+    sa = 1.0 if float((cb - ca) @ aa) >= 0.0 else -1.0
+    sb = 1.0 if float((ca - cb) @ ab) >= 0.0 else -1.0
+    cA, nuA = ca + sa * h * aa, sa * aa
+    cB, nuB = cb + sb * h * ab, sb * ab
+    nb, na = float(n @ nuB), -float(n @ nuA)
+    if not (nb >= FACE_COS and na >= FACE_COS):
+        return []
+    c_ab = cA - cB
+    dl = c_ab - float(c_ab @ n) * n                    # the centre offset in the plane normal to n
+    s2 = float(dl @ dl)
+    if not s2 < 4.0 * r * r:
+        return []
+    s = math.sqrt(s2)
+    u = dl / s if s > 1e-9 else plane_space(n)[0]
+    v = np.cross(n, u)
+    w = math.sqrt(max(r * r - 0.25 * s2, 0.0))
+    out = []
+    for p in ((s - r) * u, r * u, (0.5 * s) * u + w * v, (0.5 * s) * u - w * v):
+        tb = -float(p @ nuB) / nb                      # along n from cB + p to B's cap plane
+        ta = float((c_ab - p) @ nuA) / -na             # ... to A's cap plane ((cA - cB - p).nuA / n.nuA)
+        out.append((cB + p + (tb + mg) * n, (ta - tb) - 2.0 * mg))
+    return out
 
 
 def drone_contacts(pos, rot_bw, radius, half_height, z_offset):
     """The env's contacts in solve order: pairs (i, j), i < j, lexicographic, that pass the
     broadphase (``pair_near``) and whose distance is below the breaking threshold - every such
-    pair, however many (up to D (D - 1) / 2; round 3 kept at most D)."""
+    pair, however many (up to D (D - 1) / 2; round 3 kept at most D).  Per pair: the closest
+    points (``pair_geometry``), then for a cap-to-cap contact its face manifold (``face_points``)
+    points below the breaking threshold, as further contacts of the same pair (i, j, n, pb, dist)."""
     D = pos.shape[0]
     brk = breaking_threshold(radius, half_height)
     axes = [rot_bw[i][:, 2].copy() for i in range(D)]
@@ -456,39 +610,84 @@ def drone_contacts(pos, rot_bw, radius, half_height, z_offset):
         for j in range(i + 1, D):
             if not pair_near(cent[i], axes[i], cent[j], axes[j], radius, half_height, brk):
                 continue
-            n, pb, dist = pair_geometry(cent[i], axes[i], cent[j], axes[j], radius, half_height)
+            n, pb, dist, mg = pair_geometry(cent[i], axes[i], cent[j], axes[j], radius, half_height, with_margin=True)
             if dist < brk:
                 out.append((i, j, n, pb, dist))
+                if mg is not None:
+                    for pb2, d2 in face_points(cent[i], axes[i], cent[j], axes[j], n, radius, half_height, mg):
+                        if d2 < brk:
+                            out.append((i, j, n, pb2, d2))
     return out
 
 
-def drone_contact(pos, rot_bw, vel_w, omega_w, m, inertia, dt, radius, half_height, z_offset):
-    """Drone <-> drone contact of one env for one ``stepSimulation``: the rows of
-    ``plane_contact`` between two moving bodies, solved before it (between the unconstrained
-    velocity update and the ground-plane solve).  Known deviation: Bullet solves the pair and
-    plane rows of an island in one Gauss-Seidel loop; here the pair solve runs first and each
-    drone's plane solve after it, so a drone resting on another that rests on the plane settles
-    over substeps rather than within one solve (tests/test_oracle_drone_contact.py pins the
-    stacked-on-the-plane case).
+def _plane_rows_world(pos, rot_bw, vel, omg, im, iw, dt, radius, half_height, z_offset):
+    """``plane_contact``'s rows of one drone in world coordinates (directions +z, (0,-1,0), (1,0,0);
+    arms R r; angular Jacobians r x d; I_w^-1 = R diag(1/I) R^T): the same rows as its base-frame
+    form up to rounding, for an island solve that also holds pair rows."""
+    brk = breaking_threshold(radius, half_height)
+    dirs = (np.array([0.0, 0.0, 1.0]), np.array([0.0, -1.0, 0.0]), np.array([1.0, 0.0, 0.0]))
+    rows = []
+    for r in contact_points(radius, half_height, z_offset, rot_bw):
+        rw = rot_bw @ r
+        dist = pos[2] + rw[2]
+        if not (dist < brk and abs(pos[0] + rw[0]) <= PLANE_HALF and abs(pos[1] + rw[1]) <= PLANE_HALF):
+            continue
+        row = dict(a=[], g=[], jdi=[], rhs=[], lam=[0.0, 0.0, 0.0])
+        for k, d in enumerate(dirs):
+            a = np.cross(rw, d)
+            g = iw @ a
+            jd = im + float(a @ g)
+            rel = float(d @ vel) + float(a @ omg)
+            if k == 0:
+                pen = dist + LINEAR_SLOP
+                rhs = (-rel - pen / dt) / jd if pen > 0 else (-pen * CONTACT_ERP / dt - rel) / jd
+                row["jdn"] = jd
+            else:
+                rhs = -rel / jd
+            row["a"].append(a); row["g"].append(g); row["jdi"].append(1.0 / jd); row["rhs"].append(rhs)
+        rows.append(row)
+    return rows
+
+
+def drone_contact(pos, rot_bw, vel_w, omega_w, m, inertia, dt, radius, half_height, z_offset, plane=False):
+    """Drone <-> drone contact of one env for one ``stepSimulation`` (between the unconstrained
+    velocity update and the position update).
 
     ``pos`` [D, 3] start-of-step positions, ``rot_bw`` [D, 3, 3] body -> world, ``vel_w`` /
     ``omega_w`` [D, 3] after the unconstrained update.  Per contact (A = i, B = j, normal n from B
     to A, point on B ``pb``, point on A ``pb + n dist``): rows along n and btPlaneSpace1(n) with
     arms from each COM, effective mass 2/m + a_A.I_A^-1 a_A + a_B.I_B^-1 a_B (world inverse
     inertia R diag(1/I) R^T), the plane's rhs rules (speculative / ERP, slop) and friction cone
-    (FRICTION_DD); Gauss-Seidel over the env's normal rows, then its friction pairs, in contact
-    order, until the largest squared residual <= RESIDUAL_THRESHOLD or SOLVER_ITERS.  Returns
-    the new (vel, omega) [D, 3]."""
+    (FRICTION_DD).
+
+    ``plane=True`` (the ground plane is on): the island solve.  Bullet solves the rows of all
+    bodies an island's contacts connect in one Gauss-Seidel loop; here every drone that is in a
+    pair contact AND touches the plane (``plane_contact``'s points) brings its plane rows into the
+    env's loop, and its own plane solve is skipped (the caller uses the returned set).  Per
+    iteration: the plane normal rows of those drones (drone order, point order), the pair normal
+    rows (contact order), the plane friction pairs, the pair friction pairs; the env stops at its
+    largest squared residual <= RESIDUAL_THRESHOLD or after SOLVER_ITERS (the env's islands share
+    the stopping rule).  Round 4; before it the pair solve ran first and each drone's plane solve
+    after it, so a drone resting on another that rests on the plane sank ~1 cm into it.
+    ``plane=False``: pair rows only.  Returns (vel, omega) [D, 3], and with ``plane=True`` also the
+    set of drones whose plane rows were solved here."""
     pos = np.asarray(pos, dtype=np.float64)
     vel = np.array(vel_w, dtype=np.float64)
     omg = np.array(omega_w, dtype=np.float64)
     cons = drone_contacts(pos, rot_bw, radius, half_height, z_offset)
     if not cons:
-        return vel, omg
+        return (vel, omg, set()) if plane else (vel, omg)
     D = pos.shape[0]
     im = 1.0 / m
     inv_i = 1.0 / np.asarray(inertia, dtype=np.float64)
     iw = [rot_bw[i] @ np.diag(inv_i) @ rot_bw[i].T for i in range(D)]
+    touched = sorted({c[0] for c in cons} | {c[1] for c in cons})
+    prows = {}
+    if plane:
+        for i in touched:
+            r = _plane_rows_world(pos[i], rot_bw[i], vel[i], omg[i], im, iw[i], dt, radius, half_height, z_offset)
+            if r:
+                prows[i] = r
     rows = []
     for (i, j, n, pb, dist) in cons:
         pa = pb + n * dist
@@ -511,6 +710,7 @@ def drone_contact(pos, rot_bw, vel_w, omega_w, m, inertia, dt, radius, half_heig
         rows.append(row)
     dl = np.zeros((D, 3))
     da = np.zeros((D, 3))
+    pdirs = (np.array([0.0, 0.0, 1.0]), np.array([0.0, -1.0, 0.0]), np.array([1.0, 0.0, 0.0]))
 
     def jv(c, k):
         i, j = c["i"], c["j"]
@@ -523,29 +723,63 @@ def drone_contact(pos, rot_bw, vel_w, omega_w, m, inertia, dt, radius, half_heig
         dl[j] -= c["d"][k] * (im * delta)
         da[j] -= c["gb"][k] * delta
 
+    def pjv(i, c, k):
+        return float(pdirs[k] @ dl[i]) + float(c["a"][k] @ da[i])
+
+    def papply(i, c, k, delta):
+        dl[i] += pdirs[k] * (im * delta)
+        da[i] += c["g"][k] * delta
+
+    def cone(s1, s2, lim):
+        m2 = s1 * s1 + s2 * s2
+        if m2 > lim * lim:
+            f = lim / math.sqrt(m2)
+            return s1 * f, s2 * f
+        return s1, s2
+
     for _ in range(SOLVER_ITERS):
         res = 0.0
-        for c in rows:                                        # normal rows
+        for i, pr in prows.items():                           # plane normal rows
+            for c in pr:
+                delta = c["rhs"][0] - c["jdi"][0] * pjv(i, c, 0)
+                s_ = c["lam"][0] + delta
+                if s_ < 0.0:
+                    delta = -c["lam"][0]
+                    s_ = 0.0
+                c["lam"][0] = s_
+                papply(i, c, 0, delta)
+                res = max(res, (delta * c["jdn"]) ** 2)
+        for c in rows:                                        # pair normal rows
             delta = c["rhs"][0] - c["jdi"][0] * jv(c, 0)
-            s = c["lam"][0] + delta
-            if s < 0.0:
+            s_ = c["lam"][0] + delta
+            if s_ < 0.0:
                 delta = -c["lam"][0]
-                s = 0.0
-            c["lam"][0] = s
+                s_ = 0.0
+            c["lam"][0] = s_
             apply(c, 0, delta)
             res = max(res, (delta * c["jdn"]) ** 2)
-        for c in rows:                                        # friction pairs (implicit cone)
+        for i, pr in prows.items():                           # plane friction pairs
+            for c in pr:
+                ln = c["lam"][0]
+                if not ln > 0.0:
+                    continue
+                s1 = c["lam"][1] + (c["rhs"][1] - c["jdi"][1] * pjv(i, c, 1))
+                s2 = c["lam"][2] + (c["rhs"][2] - c["jdi"][2] * pjv(i, c, 2))
+                s1, s2 = cone(s1, s2, FRICTION * ln)
+                d1 = s1 - c["lam"][1]
+                d2 = s2 - c["lam"][2]
+                c["lam"][1] = s1
+                c["lam"][2] = s2
+                papply(i, c, 1, d1)
+                papply(i, c, 2, d2)
+                res = max(res, (d1 + d2) ** 2)
+        for c in rows:                                        # pair friction pairs (implicit cone)
             ln = c["lam"][0]
             if not ln > 0.0:
                 continue
-            lim = FRICTION_DD * ln
             s1 = c["lam"][1] + (c["rhs"][1] - c["jdi"][1] * jv(c, 1))
             s2 = c["lam"][2] + (c["rhs"][2] - c["jdi"][2] * jv(c, 2))
-            m2 = s1 * s1 + s2 * s2
-            if m2 > lim * lim:
-                f = lim / math.sqrt(m2)
-                s1 = s1 * f
-                s2 = s2 * f
+            s1, s2 = cone(s1, s2, FRICTION_DD * ln)
             d1 = s1 - c["lam"][1]
             d2 = s2 - c["lam"][2]
             c["lam"][1] = s1
@@ -555,8 +789,7 @@ def drone_contact(pos, rot_bw, vel_w, omega_w, m, inertia, dt, radius, half_heig
             res = max(res, (d1 + d2) ** 2)
         if res <= RESIDUAL_THRESHOLD:
             break
-    touched = sorted({c["i"] for c in rows} | {c["j"] for c in rows})
     for i in touched:
         vel[i] = vel[i] + dl[i]
         omg[i] = omg[i] + da[i]
-    return vel, omg
+    return (vel, omg, set(prows)) if plane else (vel, omg)

@@ -251,23 +251,29 @@ class RefAviary:
     def _bullet_step_all(self, rpms):
         """One p.stepSimulation() of every drone (PYB* modes): the unconstrained velocity update
         of each drone (_bullet_physics), the drone <-> drone contact over the env (envs of D > 1
-        drones, bullet_mb.drone_contact), then each drone's ground-plane contact and position
-        update (bullet_mb.multibody_finish)."""
+        drones, bullet_mb.drone_contact: the island solve, which also takes the plane rows of the
+        drones in a pair contact that touch the plane), then each other drone's ground-plane contact
+        and every drone's position update (bullet_mb.multibody_finish)."""
         p = self.P
         cyl = (p["collision_r"], p["collision_h"] / 2, p["collision_z_offset"])
         inertia = np.array([p["ixx"], p["iyy"], p["izz"]])
         mids = [self._bullet_physics(rpms[i, :], i) for i in range(self.NUM_DRONES)]
         G = self.DRONES_PER_ENV
+        plane = "no_plane" not in self.AERO
+        island = set()                   # drones whose plane rows the island solve took
         if G > 1 and "no_drone_contact" not in self.AERO:
             for e0 in range(0, self.NUM_DRONES, G):
                 env = mids[e0:e0 + G]
-                vel, omg = drone_contact(self._b_pos[e0:e0 + G], np.array([m[1].T for m in env]),
-                                         np.array([m[2] for m in env]), np.array([m[3] for m in env]),
-                                         self.M, inertia, self.PYB_TIMESTEP, *cyl)
+                out = drone_contact(self._b_pos[e0:e0 + G], np.array([m[1].T for m in env]),
+                                    np.array([m[2] for m in env]), np.array([m[3] for m in env]),
+                                    self.M, inertia, self.PYB_TIMESTEP, *cyl, plane=plane)
+                vel, omg = out[0], out[1]
+                if plane:
+                    island |= {e0 + i for i in out[2]}
                 mids[e0:e0 + G] = [(m[0], m[1], vel[i], omg[i]) for i, m in enumerate(env)]
         for i, (q_wb, rot, vel, omega) in enumerate(mids):
             pos, q_s, vel, omega = multibody_finish(self._b_pos[i], q_wb, rot, vel, omega, self.M, inertia,
-                                                    self.PYB_TIMESTEP, None if "no_plane" in self.AERO else cyl)
+                                                    self.PYB_TIMESTEP, cyl if plane and i not in island else None)
             self._b_pos[i], self._b_quat[i], self._b_vel[i], self._b_angv[i] = pos, q_s, vel, omega
             self.rpy_rates[i, :] = omega
 
