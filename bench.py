@@ -10,7 +10,8 @@ substep (drone*dt).  value = drone*dt of all ranks / max-over-ranks wall time of
 
 Multi-GPU: one process per GPU (torchrun); each rank owns E envs (weak scaling), there is no
 collective inside the timed loop.  The RCCL all-gather of the observation batch to a learner
-on rank 0 (config 5) is timed separately and reported under "gather".
+on rank 0 (config 5) is timed separately and reported under "handoff" (on one GPU: a one-rank RCCL
+group with the collectives forced).
 
 Extra JSON fields: "roofline" (step kernel, HIP events on the launch stream), "cpu_baseline"
 (the oracle, rank 0 at N=1), "parity" (the metric's state-L2 leg: GPU vs the C oracle over 5 s,
@@ -489,6 +490,43 @@ def _policy_mlp(n_in, n_out):
     return nn.Sequential(nn.Linear(n_in, 64), nn.Tanh(), nn.Linear(64, 64), nn.Tanh(), nn.Linear(64, n_out))
 
 
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def handoff_leg(sim, global_envs, hmode, cap, gpool, G, rank, device, force=False):
+    """One LearnerHandoff configuration timed over G steps (after 3 warm ones): ms per step, the
+    bytes that land per step, how many steps needed the second (overflow) exchange and the
+    finished-env rate of the batch (mean / max envs per step, from the gathered done flags)."""
+    import torch.distributed as dist
+
+    from gym_pybullet_drones_routing_amd.shard import LearnerHandoff, max_over_ranks
+    h = LearnerHandoff(sim, global_envs, mode=hmode, force_collectives=force, terminal_capacity=cap)
+    for k in range(3):
+        h.step(gpool[k % 8] if rank == 0 else None)
+    torch.cuda.synchronize(device)
+    dist.barrier()
+    torch.cuda.synchronize(device)
+    h.terminal_bytes, h.steps, h.second_exchanges = 0, 0, 0
+    fin = torch.zeros((G,), dtype=torch.int64, device=device)
+    t0 = time.perf_counter()
+    for k in range(G):
+        r = h.step(gpool[k % 8] if rank == 0 else None)
+        if r is not None:
+            fin[k] = (r[2] | r[3]).sum()
+    torch.cuda.synchronize(device)
+    gw = max_over_ranks(time.perf_counter() - t0, device)
+    out = dict(h.stats(), ms_per_step=1000 * gw / G)
+    if rank == 0:
+        f = fin.double()
+        out["finished_envs_per_step"] = {"mean": float(f.mean()), "max": int(fin.max()),
+                                         "frac_mean": float(f.mean()) / global_envs}
+    return out
+
+
 def rollout_leg(device, precision, act, E, K=64, reps=8, store_policy=2):
     """What an RL caller pays per env.step (the caller: examples/learn.py's PPO rollout, the
     reference's learn.py:52-94 through SB3): ONE hipGraph of K x (actor and critic MLP forward on
@@ -653,6 +691,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-latency-model", action="store_true",
                     help="skip the latency-model leg (its 1- and 16-substep launches share the bench kernel's "
                          "name and grid, so a rocprofv3 trace of the bench kernel leaves it out)")
+    ap.add_argument("--no-handoff", action="store_true",
+                    help="skip the one-GPU learner hand-off leg (a one-rank RCCL group)")
     ap.add_argument("--no-rollout", action="store_true",
                     help="skip the RL-rollout leg (its step launches share the bench kernel's name and grid)")
     ap.add_argument("--mode", default="graph", choices=["native", "graph", "eager"],
@@ -827,35 +867,36 @@ def run(args):
                             "kernel_us": ks, "steps": ns}
         ss.close()
         del sp
-    if world > 1:
+    if world > 1 or (rank == 0 and not args.no_handoff):
         # config 5: the learner hand-off (shard.LearnerHandoff): rank 0 scatters the global action
         # batch, every rank steps its shard, the output-pack prefixes (obs, reward, terminated,
-        # truncated) go to the learner ("gather") or to every rank ("all_gather"), and the finished
-        # envs' terminal rows follow, densely packed
-        gpool = None
-        if rank == 0:
-            gpool = make_pool(E * world, A, device, seed=11, pool=8)
-        G = max(10, args.steps // 3)
-        coll = "RCCL" if args.dist_backend == "nccl" else "gloo (rehearsal, through host memory)"
-        legs = {}
-        for hmode in ("gather", "all_gather"):
-            handoff = LearnerHandoff(sim, E * world, mode=hmode)
-            for k in range(3):
-                handoff.step(gpool[k % 8] if rank == 0 else None)
-            torch.cuda.synchronize(device)
-            torch.distributed.barrier()
-            torch.cuda.synchronize(device)
-            handoff.terminal_bytes, handoff.steps = 0, 0
-            t0 = time.perf_counter()
-            for k in range(G):
-                handoff.step(gpool[k % 8] if rank == 0 else None)
-            torch.cuda.synchronize(device)
-            gw = max_over_ranks(time.perf_counter() - t0, device)
-            legs[hmode] = dict(handoff.stats(), ms_per_step=1000 * gw / G, value=world * E * nsub * G / gw)
-        result["gather"] = {"mode": f"learner hand-off per step ({coll}): scatter of actions from rank 0, eager "
-                                    "shard step, gather / all_gather_into_tensor of the output-pack prefixes, "
-                                    "terminal rows of finished envs only",
-                            "legs": legs}
+        # truncated) go to the learner ("gather") or to every rank ("all_gather"), then the finished
+        # envs' terminal rows (their 12 state columns).  One GPU: a one-rank RCCL group with the
+        # collectives forced, so the same calls run as on a node
+        one_rank = world == 1
+        if one_rank and args.dist_backend == "nccl" and not torch.distributed.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ["MASTER_PORT"] = str(_free_port())
+            torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=device)
+        if torch.distributed.is_initialized():
+            gpool = make_pool(E * world, A, device, seed=11, pool=8) if rank == 0 else None
+            G = max(30, args.steps // 3)
+            coll = "RCCL" if args.dist_backend == "nccl" else "gloo (rehearsal, through host memory)"
+            legs = {}
+            for hmode in ("gather", "all_gather"):
+                for cap in (None, max(1, E // 8)):
+                    legs[f"{hmode}_cap{'shard' if cap is None else cap}"] = handoff_leg(
+                        sim, E * world, hmode, cap, gpool, G, rank, device, force=one_rank)
+            result["handoff"] = {
+                "mode": f"learner hand-off per step ({coll}{', one rank, collectives forced' if one_rank else ''}): "
+                        "scatter of actions from rank 0, eager shard step, gather / all_gather_into_tensor of the "
+                        "output-pack prefixes, then the finished envs' terminal rows (12 state columns per drone; the "
+                        "history columns are the auto-reset obs's): a block of terminal_capacity rows per rank, and "
+                        "with a capacity below the shard an all-reduce of the largest finished count (one host sync) "
+                        "and, when it overflows, a second exchange of exactly the missing rows",
+                "step_only_ms": 1000.0 * eager_wall / args.steps, "legs": legs}
+            if one_rank:
+                torch.distributed.destroy_process_group()
 
     if rank == 0 and world == 1 and not args.no_latency_model:
         result["roofline"]["latency_model"] = latency_model(device, args.precision, args.act, E, kern_us, nsub)

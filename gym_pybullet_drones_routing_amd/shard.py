@@ -93,18 +93,21 @@ class LearnerHandoff:
        ``mode="gather"`` (one learner: ``dist.gather`` to rank 0, G x prefix bytes land there
        only) or ``mode="all_gather"`` (data-parallel learners: ``all_gather_into_tensor``, the
        batch lands on every rank);
-    4. terminal rows (``terminal_obs=True``): every rank compacts the rows of its envs that
-       finished this step on the device (a prefix sum over its done flags, ``index_copy_``) into
-       a fixed block of ``terminal_capacity`` rows (default: the shard's env count, so it never
-       overflows), and that block goes the prefix's way (``gather`` / ``all_gather_into_tensor``);
-       the receiving ranks place row j of rank r at rank r's j-th finished env, again from the
-       gathered flags on the device.  Every size is fixed, so a step issues its collectives without
-       waiting for the device: no ``.item()`` / ``.tolist()`` / boolean indexing anywhere (round
-       3 sized the terminal exchange from the done counts, two host syncs per step, each longer
-       than the ~5 us step itself).  A smaller ``terminal_capacity`` moves fewer bytes; a step
-       whose finished envs exceed it on some rank drops their rows and raises the
-       ``overflowed()`` flag (a device tensor the caller reads when it synchronises anyway).
-
+    4. terminal rows (``terminal_obs=True``): only their 12 state columns travel.  The reference
+       never clears the action buffer on reset (``BaseRLAviary`` has no ``reset`` override, SURVEY
+       a13), so a finished env's terminal observation and its auto-reset observation share the 15
+       history columns; the receiving ranks rebuild the terminal row from the gathered obs (48 B per
+       drone instead of 288 B with RPM actions).  Every rank compacts the state columns of its envs
+       that finished this step on the device (a prefix sum over its done flags, ``index_copy_``)
+       into a fixed block of ``terminal_capacity`` rows, and that block goes the prefix's way
+       (``gather`` / ``all_gather_into_tensor``); the receivers place row j of rank r at rank r's
+       j-th finished env, from the gathered flags on the device.  With the default capacity (the
+       shard's env count) every size is fixed and nothing waits for the device: no ``.item()`` /
+       boolean indexing (round 3 sized the exchange from the done counts, two host syncs per step,
+       each longer than the ~5 us step).  A smaller ``terminal_capacity`` sends fewer rows first and
+       never drops one: an all-reduce of the largest finished count follows (read on the host - one
+       synchronisation per step, the price of the smaller block), and when some rank finished more
+       envs than the capacity a second exchange of exactly the missing rows runs in the same step.
     ``step`` returns (obs [E, D, W], reward [E], terminated [E], truncated [E], terminal_obs or
     None) - freshly allocated tensors, so a caller may keep them across steps - on the learner
     rank ("gather") or every rank ("all_gather"), None elsewhere.  Rows of ``terminal_obs`` whose
@@ -113,6 +116,7 @@ class LearnerHandoff:
     With gloo (CPU tests, one-GPU rehearsals) the same exchange runs through host memory."""
 
     MODES = ("all_gather", "gather")
+    STATE_COLS = 12    # KIN observation: pos, rpy, vel, ang_v (BaseRLAviary.py:313-316) before the history
 
     def __init__(self, sim, global_envs, learner_rank=0, terminal_obs=True, mode="all_gather",
                  force_collectives=False, terminal_capacity=None):
@@ -144,12 +148,16 @@ class LearnerHandoff:
             raise ValueError(f"terminal_capacity must be in [1, {self.count}]")
         self.capacity = C
         W = sim.obs_width
-        # the compacted block (+ one scratch row that the envs still running write to) and the
-        # gathered blocks of every rank
-        self._tblock = torch.zeros((C + 1, D * W), dtype=torch.float32, device=dev)
-        self._trows = torch.zeros((self.world * C, D * W), dtype=torch.float32, device=dev)
-        self._overflow = torch.zeros((), dtype=torch.bool, device=dev)
+        if W < self.STATE_COLS:
+            raise ValueError(f"observation rows of width {W} have no {self.STATE_COLS} state columns")
+        S = self.STATE_COLS
+        # the compacted block of state columns (+ one scratch row that the envs still running write
+        # to) and the gathered blocks of every rank
+        self._tblock = torch.zeros((self.count + 1, D * S), dtype=torch.float32, device=dev)
+        self._trows = torch.zeros((self.world * C, D * S), dtype=torch.float32, device=dev)
         self.terminal_bytes = 0     # terminal-row bytes received by the learner so far (all steps)
+        self.second_exchanges = 0   # steps that needed the overflow exchange (capacity < shard)
+        self.finished = 0           # finished envs seen (receiving ranks; counted only with a capacity < shard)
         self.steps = 0
 
     @property
@@ -166,17 +174,13 @@ class LearnerHandoff:
         return (self.global_envs * self.sim.drones_per_env * self.sim.act_width * 4,
                 self.world * self.nbytes)
 
-    def overflowed(self):
-        """True when some step's finished envs exceeded ``terminal_capacity`` on some rank (their
-        terminal rows were not delivered).  Reads a device flag: a host synchronisation."""
-        return bool(self._overflow)
-
     def stats(self):
         """Bytes per step of each part of the hand-off (learner side), averaged over the steps."""
         act_b, pre_b = self.bytes_per_step()
         return {"mode": self.mode, "action_bytes": act_b, "prefix_bytes": pre_b,
                 "terminal_bytes_avg": self.terminal_bytes / max(1, self.steps),
-                "terminal_row_bytes": self.row_bytes,
+                "terminal_row_bytes": self.sim.drones_per_env * self.STATE_COLS * 4,
+                "terminal_capacity": self.capacity, "second_exchanges": self.second_exchanges,
                 "lands_on": "every rank" if self.mode == "all_gather" else "learner"}
 
     # ------------------------------------------------------------------ collectives
@@ -197,27 +201,7 @@ class LearnerHandoff:
             dist.scatter(self.local_actions, [p.contiguous() for p in parts] if parts else None, src=self.learner)
 
     def _gather_prefix(self):
-        local = self.sim.out_pack[:self.nbytes]
-        if not self._coll:
-            self.pack_all.copy_(local)
-            return
-        parts = list(self.pack_all.view(self.world, self.nbytes).unbind(0))
-        if self.mode == "all_gather":
-            if self._gloo:
-                host = [torch.empty((self.nbytes,), dtype=torch.uint8) for _ in range(self.world)]
-                dist.all_gather(host, local.cpu())
-                self.pack_all.copy_(torch.cat(host))
-            else:
-                dist.all_gather_into_tensor(self.pack_all, local)
-        else:
-            if self._gloo:
-                host = [torch.empty((self.nbytes,), dtype=torch.uint8) for _ in range(self.world)] \
-                    if self.is_learner else None
-                dist.gather(local.cpu(), host, dst=self.learner)
-                if self.is_learner:
-                    self.pack_all.copy_(torch.cat(host))
-            else:
-                dist.gather(local, parts if self.is_learner else None, dst=self.learner)
+        self._exchange(self.sim.out_pack[:self.nbytes], self.pack_all)
 
     def _field(self, name, dtype, shape):
         """Field `name` of every rank's gathered pack, as ONE fresh tensor [G*E, ...]."""
@@ -231,54 +215,74 @@ class LearnerHandoff:
         off, n = self.layout[name]
         return self.sim.out_pack[off:off + n].view(dtype).reshape(shape)
 
-    def _exchange_rows(self):
-        """The compacted terminal blocks [C, D*W] of every rank -> self._trows (receiving ranks)."""
-        local = self._tblock[:self.capacity]
+    def _exchange(self, local, out):
+        """Every rank's block ``local`` [n, ...] -> ``out`` [G * n, ...] on the receiving ranks."""
         if not self._coll:
-            self._trows.copy_(local)
+            out.copy_(local)
             return
         if self.mode == "all_gather":
             if self._gloo:
-                host = [torch.empty(tuple(local.shape), dtype=torch.float32) for _ in range(self.world)]
+                host = [torch.empty(tuple(local.shape), dtype=local.dtype) for _ in range(self.world)]
                 dist.all_gather(host, local.cpu())
-                self._trows.copy_(torch.cat(host))
+                out.copy_(torch.cat(host))
             else:
-                dist.all_gather_into_tensor(self._trows, local)
+                dist.all_gather_into_tensor(out, local.contiguous())
         else:
             if self._gloo:
-                host = [torch.empty(tuple(local.shape), dtype=torch.float32) for _ in range(self.world)] \
+                host = [torch.empty(tuple(local.shape), dtype=local.dtype) for _ in range(self.world)] \
                     if self.is_learner else None
                 dist.gather(local.cpu(), host, dst=self.learner)
                 if self.is_learner:
-                    self._trows.copy_(torch.cat(host))
+                    out.copy_(torch.cat(host))
             else:
-                parts = list(self._trows.view(self.world, self.capacity, -1).unbind(0)) if self.is_learner else None
-                dist.gather(local, parts, dst=self.learner)
+                parts = list(out.view((self.world,) + tuple(local.shape)).unbind(0)) if self.is_learner else None
+                dist.gather(local.contiguous(), parts, dst=self.learner)
 
-    def _terminal_rows(self, te, tr):
+    def _max_finished(self, ldone):
+        """The largest finished-env count of any rank (an all-reduce, read on the host)."""
+        n = ldone.sum().to(torch.int64).reshape(1)
+        if self._coll:
+            if self._gloo:
+                n = n.cpu()
+            dist.all_reduce(n, op=dist.ReduceOp.MAX)
+        return int(n.item())
+
+    def _terminal_rows(self, obs, te, tr):
         """Terminal rows of the envs that finished this step ([G*E, D, W], zero elsewhere) on the
-        ranks that receive; None elsewhere.  te / tr: gathered flags (receiving ranks).  Fixed
-        sizes and device-side indices only: nothing here waits for the device."""
+        ranks that receive; None elsewhere.  obs / te / tr: the gathered batch (receiving ranks).
+        With the default capacity, fixed sizes and device-side indices only: nothing here waits for
+        the device."""
         G, E, D, W = self.world, self.count, self.sim.drones_per_env, self.sim.obs_width
-        C = self.capacity
+        C, S = self.capacity, self.STATE_COLS
         ldone = (self._local("terminated", torch.uint8, (E,)) | self._local("truncated", torch.uint8, (E,))).bool()
-        lrows = self._local("terminal_obs", torch.float32, (E, D * W))
-        # compaction: the j-th finished env's row -> block row j; the others -> the scratch row C
+        lrows = self._local("terminal_obs", torch.float32, (E, D, W))[:, :, :S].reshape(E, D * S)
+        # compaction: the j-th finished env's state columns -> block row j; the others -> the scratch row E
         j = torch.cumsum(ldone.to(torch.int64), 0) - 1
-        dst = torch.where(ldone & (j < C), j, torch.full_like(j, C))
-        self._tblock.index_copy_(0, dst, lrows)
-        self._exchange_rows()
-        self.terminal_bytes += G * C * D * W * 4
+        self._tblock.index_copy_(0, torch.where(ldone, j, torch.full_like(j, E)), lrows)
+        self._exchange(self._tblock[:C], self._trows)
+        self.terminal_bytes += G * C * D * S * 4
+        need = C
+        if C < E:
+            # a smaller first block: rows past it follow in a second exchange of exactly their count
+            need = self._max_finished(ldone)
+            if need > C:
+                extra = torch.empty((G * (need - C), D * S), dtype=torch.float32, device=self.device)
+                self._exchange(self._tblock[C:need], extra)
+                self.terminal_bytes += G * (need - C) * D * S * 4
+                self.second_exchanges += 1
         if not self.receives:
             return None
         done_all = (te | tr).bool().reshape(G, E)
         within = torch.cumsum(done_all.to(torch.int64), 1) - 1
-        src = torch.arange(G, device=self.device)[:, None] * C + within.clamp(0, C - 1)
-        keep = done_all & (within < C)
-        self._overflow |= (done_all & (within >= C)).any()
-        rows = self._trows.index_select(0, src.reshape(-1))
-        out = torch.where(keep.reshape(-1, 1), rows, torch.zeros((), dtype=rows.dtype, device=self.device))
-        return out.view(G * E, D, W)
+        if need > C:
+            rows_all = torch.cat([self._trows.view(G, C, D * S), extra.view(G, need - C, D * S)], 1).reshape(G * need, -1)
+        else:
+            rows_all, need = self._trows, C
+        src = torch.arange(G, device=self.device)[:, None] * need + within.clamp(0, need - 1)
+        rows = rows_all.index_select(0, src.reshape(-1)).view(G * E, D, S)
+        full = torch.cat([rows, obs[:, :, S:]], 2)      # the history columns: the reset obs's (shared)
+        out = torch.where(done_all.reshape(-1, 1, 1), full, torch.zeros((), dtype=full.dtype, device=self.device))
+        return out
 
     def _views(self):
         """The learner's global batch, reassembled from the gathered packs (rank order)."""
@@ -305,8 +309,8 @@ class LearnerHandoff:
         if self.receives:
             obs, rew, te, tr = self._views()
         else:
-            te = tr = None
-        tobs = self._terminal_rows(te, tr) if self.terminal_obs else None
+            obs = te = tr = None
+        tobs = self._terminal_rows(obs, te, tr) if self.terminal_obs else None
         if not self.receives:
             return None
         return obs, rew, te, tr, tobs
