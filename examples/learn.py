@@ -20,7 +20,10 @@ Physics defaults to the env classes' default, Physics.PYB (the reference's learn
 pass one), i.e. the restated Bullet multibody step.
 
 Evaluation follows the reference's EvalCallback(deterministic=True): the mean action of the
-policy on a fresh single env, the return of one full episode.
+policy on a fresh single env, the return of one full episode (the env and the policy are
+deterministic, so EvalCallback's 5 episodes are 5 copies of it), after every PPO update - the
+reference's eval_freq=1000 with n_envs=1 evaluates about twice per 2048-step update
+(``examples/learn.py:84-91`` there); round 4 evaluated after every second update.
 """
 import argparse
 import json
@@ -204,7 +207,7 @@ class GraphedMinibatch:
 
 def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), lr=3e-4, epochs=10,
           minibatch=16384, gamma=0.99, gae_lambda=0.95, clip=0.2, vf_coef=0.5, max_grad_norm=0.5,
-          eval_every=2, seed=0, device="cuda:0", act=DEFAULT_ACT, target_reward=None, max_seconds=None,
+          eval_every=1, seed=0, device="cuda:0", act=DEFAULT_ACT, target_reward=None, max_seconds=None,
           log=print, physics=Physics.PYB, env=None, world=1, rank=0, graph=False):
     """PPO on the batched env.  ``env``: an already built torch-output VecEnv (e.g. the
     multi-GPU ``ShardedAviaryVecEnv``); by default one ``AviaryVecEnv`` on ``device``.

@@ -196,13 +196,6 @@ Consts<R> make_consts(const gpd_sim* s) {
     const double reach = 2.0 * bs + (double)c.brk;
     c.dd_reach2 = (R)(reach * reach);
     c.dd_mu = (R)(0.5 * 0.5);   // drone x drone default friction
-    // FISTA momentum of the narrowphase's rounds (oracle/bullet_mb.py fista_momentum)
-    double t = 1.0;
-    for (int k = 0; k < kPairCold; ++k) {
-      const double tn = (1.0 + std::sqrt(1.0 + 4.0 * t * t)) / 2.0;
-      c.dc_beta[k] = (R)((t - 1.0) / tn);
-      t = tn;
-    }
   }
   c.iters = 50;              // m_numIterations (pybullet numSolverIterations)
 #ifdef GPD_DIAG_RESID
@@ -754,13 +747,14 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   }
   if ((C.physics_flags & GPD_F_BULLET) && s->D > 1 && !(C.physics_flags & GPD_F_NO_DRONE_CONTACT)) {
     // drone <-> drone contact (gpd_kernels.h DcHook / dc_solve): the pair table of an env and the
-    // row store for a block's pairs past its first 64
+    // row store for a block's contacts past its first 64 (up to kDcPts per pair: the closest point
+    // and the face manifold)
     const int D = s->D, P = D * (D - 1) / 2;
     const int npairs = (s->tpb / D) * P;
     s->dcP = P;
-    s->dc_pmagic = ((1 << 20) + P - 1) / P;
+    s->dc_pmagic = ((1 << 24) + P - 1) / P;   // exact for p < npairs <= 32 (D - 1) <= 2016 (p P < 2^24)
     for (int p = 0; p < npairs; ++p)
-      if (((p * s->dc_pmagic) >> 20) != p / P) {
+      if (((p * s->dc_pmagic) >> 24) != p / P) {
         free_sim(s);
         return fail(GPD_EUNSUPPORTED, "gpd_create: drone contact pair layout not supported");
       }
@@ -774,9 +768,9 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
       (void)hipGetLastError();
       return fail(GPD_ENOMEM, "gpd_create: drone contact pair table");
     }
-    if (npairs > kWave) {
+    if (npairs * kDcPts > kDcRegRows * kWave) {
       const int row_reals = s->prec == GPD_F64 ? dc_row_reals<double>() : dc_row_reals<float>();
-      const int chunks = (npairs + kWave - 1) / kWave - 1;
+      const int chunks = (npairs * kDcPts + kWave - 1) / kWave - kDcRegRows;
       s->dc_row_stride = (long long)chunks * kWave * row_reals;
       const long long blocks = ((long long)s->N + s->tpb - 1) / s->tpb;
       if (hipMalloc(&s->d_dc_rows, (size_t)(blocks * s->dc_row_stride) * rs) != hipSuccess) {

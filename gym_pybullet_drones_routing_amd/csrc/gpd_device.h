@@ -170,7 +170,6 @@ struct Consts {
   R brk;                       // contact breaking threshold (0.02 x the cylinder's motion disc)
   R slop, erp, mu, plane_half, resid;   // m_linearSlop, m_erp2, combined friction, plane box, residual
   R dd_reach2, dd_mu;          // drone <-> drone contact: broadphase (2 x bounding sphere + brk)^2, friction
-  R dc_beta[8];                // drone <-> drone narrowphase: FISTA momentum weights (bullet_mb.PAIR_BETA)
   int iters;                   // m_numIterations
   R init0[10];             // reset template of drone 0 (pos, stored quat, rpy): single-drone envs
   R target0[3];            // task target of drone 0 (single-drone envs: no dependent global load)
@@ -719,7 +718,8 @@ constexpr int kWaveLanes = 64;
 // solve's cycles; 192..242 its iteration histogram; 256 + b: block b's drone-contact cycles;
 // 256 + 4096 + b: block b's step-kernel cycles; 256 + 8192 + b: block b's plane-solve cycles;
 // 256 + 12288 + b: block b's drone-contact rare-path cycles (the hook's solve branch, call included)
-constexpr int kPcHist = 256 + 4 * 4096;
+constexpr int kPcHist = 256 + 4 * 4096 + 16;   // + 16: narrowphase phase cycles (dc_narrow_pass)
+constexpr int kPcNp = 256 + 4 * 4096;
 __device__ unsigned long long g_pc_hist[kPcHist];
 #endif
 // r_p x d for the rim point p (p = 0..3: (cr,0,zc), (0,cr,zc), (-cr,0,zc), (0,-cr,zc)), with the
@@ -732,8 +732,10 @@ __device__ __forceinline__ void pc_arm(R cr, R zc, R dx, R dy, R dz, R& ax, R& a
   if (P == 3) { ax = -(cr * dz) - zc * dy; ay = zc * dx; az = cr * dx; }
 }
 
+// skip: this lane's drone takes no part (its plane rows were solved in the drone <-> drone island)
 template <typename R>
-__device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const Consts<R>& c, const DynK<R>& k) {
+__device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const Consts<R>& c, const DynK<R>& k,
+                                              bool skip = false) {
   // The rows' constants (rhs, 1/jacDiag, jacDiag) and impulses live in LDS, one column per lane
   // of the block's single wave (the run-time-flag kernels, which also serve non-contact configs,
   // and the multi-wave envs; the PYB flag-set kernels use plane_contact_regs below).  Kept in
@@ -762,7 +764,7 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
       const R dist = s.pz + pc_dot(nx, ny, nz, rx, ry, zc);
       const R wxp = s.px + pc_dot(Rm[0], Rm[1], Rm[2], rx, ry, zc);
       const R wyp = s.py + pc_dot(Rm[3], Rm[4], Rm[5], rx, ry, zc);
-      const bool act = dist < c.brk && g_abs(wxp) <= c.plane_half && g_abs(wyp) <= c.plane_half;
+      const bool act = !skip && dist < c.brk && g_abs(wxp) <= c.plane_half && g_abs(wyp) <= c.plane_half;
       any = any || act;
       const R dx[3] = {nx, ux, ex}, dy[3] = {ny, uy, ey}, dz[3] = {nz, uz, ez};
 #pragma unroll
@@ -930,7 +932,7 @@ __device__ __forceinline__ float max_abs(float r, float x) {
 }
 template <typename R, class PK = NoPark>
 __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], const Consts<R>& c, const DynK<R>& k,
-                                                   const PK& pk = PK()) {
+                                                   const PK& pk = PK(), bool skip = false) {
 #ifdef GPD_CONTACT_STATS
   const unsigned long long t_setup = __builtin_readcyclecounter();
 #endif
@@ -959,7 +961,7 @@ __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], c
     rwy[p] = pc_dot(Rm[3], Rm[4], Rm[5], rx, ry, zc);
     rwz[p] = pc_dot(Rm[6], Rm[7], Rm[8], rx, ry, zc);
     const R dist = s.pz + rwz[p];
-    act[p] = dist < c.brk && g_abs(s.px + rwx[p]) <= c.plane_half && g_abs(s.py + rwy[p]) <= c.plane_half;
+    act[p] = !skip && dist < c.brk && g_abs(s.px + rwx[p]) <= c.plane_half && g_abs(s.py + rwy[p]) <= c.plane_half;
     any = any || act[p];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
@@ -1106,7 +1108,7 @@ __device__ __forceinline__ R contact_low(const Drone<R>& s, const R Rm[9], const
 // unconstrained velocities before the ground-plane solve; NoDc elsewhere.
 struct NoDc {
   template <typename R, class PK>
-  __device__ void operator()(Drone<R>&, R*, const Consts<R>&, const DynK<R>&, const PK&) const {}
+  __device__ bool operator()(Drone<R>&, R*, const Consts<R>&, const DynK<R>&, const PK&, bool) const { return false; }
 };
 template <typename R, int PF, bool ANGV, int CW = 1, class HK = NoDc>
 __device__ __forceinline__ void bullet_substep(Drone<R>& s, R rpm[4], R W[4], R last[4], R dwsum,
@@ -1198,28 +1200,31 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, R rpm[4], R W[4], R 
 #pragma unroll
     for (int j = 0; j < 9; ++j) Rm[j] = pk[kPark + j][o];
   };
+  // island: this drone's plane rows were solved with its pair contacts (the hook's island solve)
+  bool island = false;
   if (!pf_on<PF>(k.flags, F_NO_DC)) {
     // the run-time-flag kernels (a long observation tile may leave no LDS for the parked columns)
     // call the solve without parking
-    if (PF != kPfRuntime) hk(s, Rm, c, k, ParkFns<decltype(park_dc), decltype(unpark_dc)>{park_dc, unpark_dc});
-    else hk(s, Rm, c, k, NoPark());
+    const bool plane = !pf_on<PF>(k.flags, F_NO_PLANE);
+    if (PF != kPfRuntime) island = hk(s, Rm, c, k, ParkFns<decltype(park_dc), decltype(unpark_dc)>{park_dc, unpark_dc}, plane);
+    else island = hk(s, Rm, c, k, NoPark(), plane);
   }
   // ground-plane contact (solveConstraints, before integrateTransforms); the margin keeps the
   // gate conservative against the candidates' own rounding
   if (!pf_on<PF>(k.flags, F_NO_PLANE)) {
-    const bool low = contact_low(s, Rm, c) < c.brk + R(1e-6);
+    const bool low = contact_low(s, Rm, c) < c.brk + R(1e-6) && !island;
     if (CW == 1) {
       // compiled-in PYB flag sets: the register-resident solve; run-time flags (every other
       // combination, whose kernels also serve non-contact configs) keep the LDS rows
       if (GPD_RARE(__ballot(low) != 0ull)) {
         if (PF != kPfRuntime) {
 #if GPD_CONTACT_PARK
-          plane_contact_regs<R>(s, Rm, c, k, ParkFns<decltype(park), decltype(unpark)>{park, unpark});
+          plane_contact_regs<R>(s, Rm, c, k, ParkFns<decltype(park), decltype(unpark)>{park, unpark}, island);
 #else
-          plane_contact_regs<R>(s, Rm, c, k);
+          plane_contact_regs<R>(s, Rm, c, k, NoPark(), island);
 #endif
         } else {
-          plane_contact<R>(s, Rm, c, k);
+          plane_contact<R>(s, Rm, c, k, island);
         }
       }
     } else {

@@ -275,30 +275,33 @@ __device__ __forceinline__ void wave_lds_sync() {
 //   * broadphase (pair_near): pairs (i, j > i) of an env whose bounding spheres come within the
 //     breaking threshold and that no separating axis (the two cylinder axes, the centre line)
 //     keeps farther apart than it;
-//   * one contact per pair: Bullet's margin scheme, the closest points of the margin-shrunk core
-//     cylinders by kPairCold rounds of FISTA-accelerated alternating projection from B's centre
-//     (a fixed count: the result is a continuous function of the poses) give the normal (B -> A)
-//     and distance core - 2 x margin, with thicker margins for deeper overlaps (up to ~2 cm),
-//     beyond that the least overlap over the centre line and the two axes;
-//   * EVERY pair whose distance is below the breaking threshold is a contact (up to D(D-1)/2 per
-//     env), solved in (i, j) order;
+//   * narrowphase: Bullet's margin scheme, the CONVERGED closest points of the margin-shrunk core
+//     cylinders (core_pair: cap centres, lateral surfaces, the four rims by trust-region Newton)
+//     give the normal (B -> A) and distance core - 2 x margin, with thicker margins for deeper
+//     overlaps (up to ~2 cm), beyond that the least overlap over the centre line and the two axes;
+//   * a cap-to-cap contact adds its face manifold (face_points: four points spanning the caps'
+//     overlap), each point below the breaking threshold a contact of the pair;
+//   * EVERY pair whose distance is below the breaking threshold is in contact (up to kDcPts
+//     contacts per pair), solved in (i, j) order;
 //   * rows (normal, btPlaneSpace1 friction pair) between two bodies: effective mass
 //     2/m + a_A.I_A^-1 a_A + a_B.I_B^-1 a_B; the plane's rhs rules and cone (mu 0.25); projected
 //     Gauss-Seidel over the env's normal rows, then friction pairs, in contact order; the env stops
-//     at its largest squared residual <= resid or after `iters` iterations.
+//     at its largest squared residual <= resid or after `iters` iterations;
+//   * island: a drone in a pair contact that touches the ground plane brings its plane rows into
+//     the env's loop (plane normal rows, pair normal rows, plane friction, pair friction per
+//     iteration, as Bullet solves an island), and skips its own plane solve.
 // GPU layout.  The pairs of a block's whole envs are numbered p = env * P + q (P = D(D-1)/2, q the
 // (i, j) index of bullet_mb.drone_contacts' order) and lane ln handles pairs ln, ln + 64, ... (chunk
 // ch = p / 64).  The hot part (DcHook, every substep): the drones' centre / axis columns into LDS,
 // the broadphase of every pair (the sphere test; the separating-axis tests only for pairs in
 // reach), one ballot per chunk.  A wave with a pair in reach calls dc_solve (rare): its near pairs
 // compacted over the lanes (in pair order, whatever chunk they come from), the narrowphase of up to
-// 64 of them per pass in parallel, each contact's rows set up by its lane - pass 0 in that lane's
-// registers, later passes (more than 64 near pairs) in a per-block global row store - then the
-// Gauss-Seidel sweeps: round r solves the r-th contact of every env at once (contacts of different
-// envs touch different drones), the drones' velocity deltas in LDS.  When no env of the wave has
-// more than one contact (every two-drone env, most waves of 8-drone envs) the owner lane keeps its
-// two drones' deltas in registers for the whole solve and the sweep needs no LDS at all.
-constexpr int kPairCold = 8;   // oracle/bullet_mb.py PAIR_COLD
+// 64 of them per pass in parallel, their contacts (closest point + face points) numbered in order
+// and each set up by lane c % 64 - the first 64 in registers, later ones in a per-block global row
+// store - then the Gauss-Seidel sweeps: round r solves the level-r contacts of every env at once
+// (contacts of one level touch different drones), the drones' velocity deltas in LDS.  When no env
+// of the wave has more than one contact (no face manifold, no island) the owner lane keeps its two
+// drones' deltas in registers for the whole solve and the sweep needs no LDS at all.
 template <typename R>
 __device__ __forceinline__ R cyl_extent_cos(R ua, R r, R hh) {
   const R s2 = R(1) - ua * ua;
@@ -320,80 +323,192 @@ __device__ __forceinline__ void plane_space(const R n[3], R p[3], R q[3]) {
   }
 }
 
-// contact of cylinders A (centre ca, axis aa) and B: normal (B -> A), point on B, distance
-// (oracle/bullet_mb.py pair_geometry).  beta: FISTA's momentum weights (Consts::dc_beta).
-// The rounds run in B's frame (btPlaneSpace1(aB), aB): B's projection is then a radial scaling of
-// (x, y) and a clamp of z, and the selects replace the branches - 26 instead of ~42 dependent
-// operations per round on the one lane that holds the pair.  The clamps are a v_min / v_max pair
-// and the radial factor min(rc / |r|, 1) (one v_min: the factor is below 1 exactly when the point
-// is outside, up to its last bit; |r| = 0 gives NaN, which v_min turns into 1).  The oracle
-// projects in world coordinates: the same operations up to rounding (the rounds are non-expansive).
+// ---- narrowphase (oracle/bullet_mb.py core_pair / rim_newton / rim_closest / pair_geometry / face_points)
+// The closest points of the margin-shrunk cores, converged: the near caps' centres, the lateral
+// surfaces along the axes' closest points (closed forms), and the four rim circles against the other
+// cylinder - trust-region Newton on the rim angle from each of 8 start azimuths, the smallest
+// squared distance per rim; the first candidate within the tie of the closest wins.  Everything in
+// B's frame (btPlaneSpace1(aB), aB); B's rims in A's frame (btPlaneSpace1 of A).  A pass's near
+// pairs split into 32 tasks each (4 rims x 8 starts) over the wave's lanes (dc_narrow_pass): a
+// sparse wave (one or two near pairs, the common case) runs ONE Newton chain per lane.
+template <typename R> struct NpTol;
+template <> struct NpTol<double> { static constexpr double accept = 1e-10, same = 1e-9, tie = 1e-10; };   // RIM_ACCEPT, RIM_SAME, PAIR_TIE
+template <> struct NpTol<float> { static constexpr float accept = 1e-5f, same = 1e-4f, tie = 1e-7f; };
+constexpr int kRimSamples = 8, kRimIters = 8;   // RIM_SAMPLES, RIM_ITERS
 template <typename R>
-__device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], const R cb[3], const R ab[3], R r, R hh,
-                                              const R* beta, R n[3], R pb[3], R& dist) {
-  R bp[3], bq[3];
-  plane_space(ab, bp, bq);
-  const R lx = ca[0] - cb[0], ly = ca[1] - cb[1], lz = ca[2] - cb[2];
-  // A's centre and axis in B's frame
-  const R Lx = pc_dot(bp[0], bp[1], bp[2], lx, ly, lz), Ly = pc_dot(bq[0], bq[1], bq[2], lx, ly, lz),
-          Lz = pc_dot(ab[0], ab[1], ab[2], lx, ly, lz);
-  const R Ax = pc_dot(bp[0], bp[1], bp[2], aa[0], aa[1], aa[2]), Ay = pc_dot(bq[0], bq[1], bq[2], aa[0], aa[1], aa[2]),
-          Az = pc_dot(ab[0], ab[1], ab[2], aa[0], aa[1], aa[2]);
-  const R margins[4] = {R(0.001), R(0.003), R(0.006), R(0.011)};
-  R yx = R(0), yy = R(0), yz = R(0);
-  for (int lv = 0; lv < 4; ++lv) {
-    const R mg = margins[lv], rc = r - mg, hc = hh - mg;
-    // A's projection of (x, y, z) (the oracle's cyl_project around A)
-    auto proj_a = [&](R& x, R& y, R& z) {
-      const R dx = x - Lx, dy = y - Ly, dz = z - Lz;
-      const R t = pc_dot(dx, dy, dz, Ax, Ay, Az);
-      const R tc = g_max1(g_min1(t, hc), -hc);
-      const R rx = dx - t * Ax, ry = dy - t * Ay, rz = dz - t * Az;
-      const R rho2 = pc_dot(rx, ry, rz, rx, ry, rz);
-      const R f = g_min1(g_krsqrt1(rho2, rc), R(1));
-      x = (Lx + tc * Ax) + rx * f;
-      y = (Ly + tc * Ay) + ry * f;
-      z = (Lz + tc * Az) + rz * f;
-    };
-    yx = R(0); yy = R(0); yz = R(0);
-    R zx = R(0), zy = R(0), zz = R(0);
-#pragma unroll
-    for (int it = 0; it < kPairCold; ++it) {
-      R px = zx, py = zy, pz = zz;
-      proj_a(px, py, pz);
-      // B's projection: radial scaling of (x, y), clamp of z
-      const R rho2 = px * px + py * py;
-      const R f = g_min1(g_krsqrt1(rho2, rc), R(1));
-      px = px * f; py = py * f;
-      pz = g_max1(g_min1(pz, hc), -hc);
-      const R b = beta[it];
-      zx = px + b * (px - yx); zy = py + b * (py - yy); zz = pz + b * (pz - yz);
-      yx = px; yy = py; yz = pz;
-    }
-    R ax = yx, ay = yy, az = yz;
-    proj_a(ax, ay, az);
-    const R vx = ax - yx, vy = ay - yy, vz = az - yz;
-    const R d2 = pc_dot(vx, vy, vz, vx, vy, vz);
-    if (d2 > R(1e-4) * R(1e-4)) {
-      const R idc = g_rsqrt(d2), dc = d2 * idc;   // |v| and 1 / |v| within ~2 ulp
-      // back to world coordinates: n = (v / |v|) in (bp, bq, ab), y likewise
-      const R ux = vx * idc, uy = vy * idc, uz = vz * idc;
-      n[0] = (ux * bp[0] + uy * bq[0]) + uz * ab[0];
-      n[1] = (ux * bp[1] + uy * bq[1]) + uz * ab[1];
-      n[2] = (ux * bp[2] + uy * bq[2]) + uz * ab[2];
-      const R wx = (yx * bp[0] + yy * bq[0]) + yz * ab[0], wy = (yx * bp[1] + yy * bq[1]) + yz * ab[1],
-              wz = (yx * bp[2] + yy * bq[2]) + yz * ab[2];
-      pb[0] = cb[0] + (wx + n[0] * mg); pb[1] = cb[1] + (wy + n[1] * mg); pb[2] = cb[2] + (wz + n[2] * mg);
-      dist = dc - R(2) * mg;
-#ifdef GPD_CONTACT_STATS
-      atomicAdd(&g_pc_hist[249 + lv], 1ull);   // narrowphases ending at margin level lv
-#endif
-      return;
-    }
+__device__ __forceinline__ void axial_project(R x, R y, R z, R r, R h, R& qx, R& qy, R& qz) {
+  const R rho2 = x * x + y * y;
+  const R f = rho2 > r * r ? r / g_sqrt(rho2) : R(1);
+  qx = x * f; qy = y * f; qz = g_max1(g_min1(z, h), -h);
+}
+template <typename R>
+__device__ __forceinline__ R axial_extent(R az, R r, R h) {
+  const R s2 = R(1) - az * az;
+  return h * g_abs(az) + r * g_sqrt(s2 > R(0) ? s2 : R(0));
+}
+// the rim point C + r (c e1 + s e2) against the axial cylinder: squared distance f, f'/2 = g and
+// f''/2 = hh in the rim angle (bullet_mb._rim_eval), the point P and its projection Q
+template <typename R>
+struct RimEval {
+  R f, g, hh, P[3], Q[3];
+};
+template <typename R>
+__device__ __forceinline__ void rim_eval(const R C[3], const R e1[3], const R e2[3], R c, R s, R r, R h, RimEval<R>& o) {
+  const R u0 = c * e1[0] + s * e2[0], u1 = c * e1[1] + s * e2[1], u2 = c * e1[2] + s * e2[2];
+  const R d0 = r * (c * e2[0] - s * e1[0]), d1 = r * (c * e2[1] - s * e1[1]), d2 = r * (c * e2[2] - s * e1[2]);
+  o.P[0] = C[0] + r * u0; o.P[1] = C[1] + r * u1; o.P[2] = C[2] + r * u2;
+  const R rho2 = o.P[0] * o.P[0] + o.P[1] * o.P[1];
+  const bool out_r = rho2 > r * r;
+  const R ir = g_rsqrt(out_r ? rho2 : R(1));
+  const R k = out_r ? r * ir : R(1);
+  o.Q[0] = o.P[0] * k; o.Q[1] = o.P[1] * k; o.Q[2] = g_max1(g_min1(o.P[2], h), -h);
+  const R e0 = o.P[0] - o.Q[0], e1_ = o.P[1] - o.Q[1], e2_ = o.P[2] - o.Q[2];
+  o.f = pc_dot(e0, e1_, e2_, e0, e1_, e2_);
+  o.g = pc_dot(e0, e1_, e2_, d0, d1, d2);
+  const R rt = (o.P[0] * d0 + o.P[1] * d1) * (ir * ir);
+  const R m0 = out_r ? d0 - k * (d0 - rt * o.P[0]) : R(0);
+  const R m1 = out_r ? d1 - k * (d1 - rt * o.P[1]) : R(0);
+  const R m2 = g_abs(o.P[2]) > h ? d2 : R(0);
+  o.hh = pc_dot(m0, m1, m2, d0, d1, d2) - r * pc_dot(e0, e1_, e2_, u0, u1, u2);
+}
+// bullet_mb.rim_newton: kRimIters trust-region Newton steps on the rim angle from (c, s)
+template <typename R>
+__device__ __forceinline__ void rim_newton(const R C[3], const R e1[3], const R e2[3], R r, R h, R c, R s, RimEval<R>& cur) {
+  constexpr R kAcc = NpTol<R>::accept;
+  rim_eval(C, e1, e2, c, s, r, h, cur);
+  R rad = R(0.39269908169872414);   // pi / RIM_SAMPLES
+#pragma unroll 1
+  for (int it = 0; it < kRimIters; ++it) {
+    // -g / hh and 1 / sqrt as Newton-refined reciprocals (~1 ulp; the oracle divides)
+    R d = cur.hh > R(0) ? -cur.g * g_rcp(cur.hh > R(0) ? cur.hh : R(1)) : -copysign(rad, cur.g);
+    d = g_max1(g_min1(d, rad), -rad);
+    R c2 = c - d * s, s2 = s + d * c;
+    const R kn = g_rsqrt(c2 * c2 + s2 * s2);
+    c2 = c2 * kn; s2 = s2 * kn;
+    RimEval<R> nx;
+    rim_eval(C, e1, e2, c2, s2, r, h, nx);
+    const bool acc = nx.f < cur.f * (R(1) - kAcc);
+    if (acc) { c = c2; s = s2; cur = nx; }
+    rad = acc ? g_min1(R(2) * rad, R(1)) : g_abs(d) * R(0.25);
   }
-  pb[0] = cb[0] + ((yx * bp[0] + yy * bq[0]) + yz * ab[0]);
-  pb[1] = cb[1] + ((yx * bp[1] + yy * bq[1]) + yz * ab[1]);
-  pb[2] = cb[2] + ((yx * bp[2] + yy * bq[2]) + yz * ab[2]);
+}
+// closest point of the cylinder (centre c, unit axis a) to x (bullet_mb.cyl_project)
+template <typename R>
+__device__ __forceinline__ void cyl_project(const R c[3], const R a[3], R r, R h, const R x[3], R o[3]) {
+  const R dx = x[0] - c[0], dy = x[1] - c[1], dz = x[2] - c[2];
+  const R t = pc_dot(dx, dy, dz, a[0], a[1], a[2]);
+  const R tc = g_max1(g_min1(t, h), -h);
+  R rx = dx - t * a[0], ry = dy - t * a[1], rz = dz - t * a[2];
+  const R rho2 = pc_dot(rx, ry, rz, rx, ry, rz);
+  const R f = rho2 > r * r ? r / g_sqrt(rho2) : R(1);
+  o[0] = (c[0] + tc * a[0]) + rx * f; o[1] = (c[1] + tc * a[1]) + ry * f; o[2] = (c[2] + tc * a[2]) + rz * f;
+}
+// a pair in B's frame: A's centre L and axis A, B's world basis (bp, bq, ab); A's frame (ap, aq, A)
+// with B's centre Lb and axis Bz in it and B's rim basis (bp2, bq2) there; the facing caps and
+// which far rims (and the lateral pair) are needed (bullet_mb.core_pair)
+template <typename R>
+struct NpPair {
+  R L[3], A[3], bp[3], bq[3], ap[3], aq[3], Lb[3], Bz[3], bp2[3], bq2[3];
+  R la, sa, sb;
+};
+template <typename R>
+__device__ __forceinline__ void np_pair(const R ca[3], const R aa[3], const R cb[3], const R ab[3], NpPair<R>& q) {
+  plane_space(ab, q.bp, q.bq);
+  const R lx = ca[0] - cb[0], ly = ca[1] - cb[1], lz = ca[2] - cb[2];
+  q.L[0] = pc_dot(q.bp[0], q.bp[1], q.bp[2], lx, ly, lz); q.L[1] = pc_dot(q.bq[0], q.bq[1], q.bq[2], lx, ly, lz);
+  q.L[2] = pc_dot(ab[0], ab[1], ab[2], lx, ly, lz);
+  q.A[0] = pc_dot(q.bp[0], q.bp[1], q.bp[2], aa[0], aa[1], aa[2]); q.A[1] = pc_dot(q.bq[0], q.bq[1], q.bq[2], aa[0], aa[1], aa[2]);
+  q.A[2] = pc_dot(ab[0], ab[1], ab[2], aa[0], aa[1], aa[2]);
+  plane_space(q.A, q.ap, q.aq);
+  q.Lb[0] = -pc_dot(q.ap[0], q.ap[1], q.ap[2], q.L[0], q.L[1], q.L[2]);
+  q.Lb[1] = -pc_dot(q.aq[0], q.aq[1], q.aq[2], q.L[0], q.L[1], q.L[2]);
+  q.Lb[2] = -pc_dot(q.A[0], q.A[1], q.A[2], q.L[0], q.L[1], q.L[2]);
+  q.Bz[0] = q.ap[2]; q.Bz[1] = q.aq[2]; q.Bz[2] = q.A[2];
+  plane_space(q.Bz, q.bp2, q.bq2);
+  q.la = -q.Lb[2];
+  q.sa = q.la > R(0) ? R(-1) : R(1);
+  q.sb = q.L[2] >= R(0) ? R(1) : R(-1);
+}
+template <typename R>
+__device__ __forceinline__ void np_far(const NpPair<R>& q, R r, R h, bool& far_a, bool& far_b) {
+  far_a = -q.sa * q.la - h < axial_extent(q.sa * q.A[2], r, h);
+  far_b = q.sb * q.L[2] - h < axial_extent(q.A[2], r, h);
+}
+template <typename R>
+__device__ __forceinline__ void np_to_b(const NpPair<R>& q, const R v[3], R o[3]) {   // A's frame -> B's: Ma^T v + L
+  o[0] = ((q.ap[0] * v[0] + q.aq[0] * v[1]) + q.A[0] * v[2]) + q.L[0];
+  o[1] = ((q.ap[1] * v[0] + q.aq[1] * v[1]) + q.A[1] * v[2]) + q.L[1];
+  o[2] = ((q.ap[2] * v[0] + q.aq[2] * v[1]) + q.A[2] * v[2]) + q.L[2];
+}
+// one rim task: rim 0/2 = A's near / far rim against B, 1/3 = B's near / far rim against A, from
+// start azimuth k; (x on A, y on B) in B's frame and the squared distance
+template <typename R>
+__device__ __forceinline__ void np_rim_task(const NpPair<R>& q, int rim, int k, R r, R h, R& f, R x[3], R y[3]) {
+  const R S = R(0.7071067811865475244008443621048490);   // bullet_mb.RIM_COS / RIM_SIN
+  const R c0 = k == 0 ? R(1) : (k == 1 || k == 7 ? S : (k == 3 || k == 5 ? -S : (k == 4 ? R(-1) : R(0))));
+  const R s0 = k == 2 ? R(1) : (k == 1 || k == 3 ? S : (k == 5 || k == 7 ? -S : (k == 6 ? R(-1) : R(0))));
+  const bool on_a = (rim & 1) == 0;
+  const R sg = on_a ? (rim < 2 ? q.sa : -q.sa) : (rim < 2 ? q.sb : -q.sb);
+  const R* base = on_a ? q.L : q.Lb;
+  const R* ax = on_a ? q.A : q.Bz;
+  const R* e1 = on_a ? q.ap : q.bp2;
+  const R* e2 = on_a ? q.aq : q.bq2;
+  const R C[3] = {base[0] + sg * h * ax[0], base[1] + sg * h * ax[1], base[2] + sg * h * ax[2]};
+  RimEval<R> o;
+  rim_newton(C, e1, e2, r, h, c0, s0, o);
+  f = o.f;
+  if (on_a) {
+    x[0] = o.P[0]; x[1] = o.P[1]; x[2] = o.P[2];
+    y[0] = o.Q[0]; y[1] = o.Q[1]; y[2] = o.Q[2];
+  } else {   // B's rim point P and A's point Q, both in A's frame
+    np_to_b(q, o.Q, x);
+    np_to_b(q, o.P, y);
+  }
+}
+// the closed-form candidates 0..2 of bullet_mb.core_pair: the near caps' centres and the lateral pair
+// (d = +inf where the lateral pair is not a candidate)
+template <typename R>
+__device__ __forceinline__ void np_closed(const NpPair<R>& q, R r, R h, bool far_a, bool far_b, R x[3][3], R y[3][3],
+                                          R d[3]) {
+  const R inf = R(INFINITY);
+  x[0][0] = q.L[0] + q.sa * h * q.A[0]; x[0][1] = q.L[1] + q.sa * h * q.A[1]; x[0][2] = q.L[2] + q.sa * h * q.A[2];
+  axial_project(x[0][0], x[0][1], x[0][2], r, h, y[0][0], y[0][1], y[0][2]);
+  {
+    const R yb[3] = {q.Lb[0] + q.sb * h * q.Bz[0], q.Lb[1] + q.sb * h * q.Bz[1], q.Lb[2] + q.sb * h * q.Bz[2]};
+    R xa[3];
+    axial_project(yb[0], yb[1], yb[2], r, h, xa[0], xa[1], xa[2]);
+    np_to_b(q, xa, x[1]);
+    np_to_b(q, yb, y[1]);
+  }
+  {
+    const R b = q.A[2], dd = q.la, e = q.L[2];
+    const R den = R(1) - b * b;
+    R s = den > R(1e-12) ? (b * e - dd) / den : R(0);
+    s = g_max1(g_min1(s, h), -h);
+    const R t = g_max1(g_min1(b * s + e, h), -h);
+    s = g_max1(g_min1(b * t - dd, h), -h);
+    const R pa[3] = {q.L[0] + s * q.A[0], q.L[1] + s * q.A[1], q.L[2] + s * q.A[2]};
+    const R wx = pa[0], wy = pa[1], wz = pa[2] - t;
+    const R wn = g_sqrt(pc_dot(wx, wy, wz, wx, wy, wz));
+    const bool ok = far_a && far_b && wn > R(1e-12);
+    const R wd = ok ? wn : R(1);
+    const R ux = wx / wd, uy = wy / wd, uz = wz / wd;
+    const R xq[3] = {pa[0] - r * ux, pa[1] - r * uy, pa[2] - r * uz};
+    cyl_project(q.L, q.A, r, h, xq, x[2]);
+    axial_project(r * ux, r * uy, t + r * uz, r, h, y[2][0], y[2][1], y[2][2]);
+    d[2] = ok ? R(0) : inf;
+  }
+  for (int c = 0; c < 3; ++c) {
+    if (c == 2 && !(d[2] == R(0))) continue;
+    const R dx = x[c][0] - y[c][0], dy = x[c][1] - y[c][1], dz = x[c][2] - y[c][2];
+    d[c] = g_sqrt(pc_dot(dx, dy, dz, dx, dy, dz));
+  }
+}
+// the least-overlap fallback of bullet_mb.pair_geometry (cores overlapping at every margin level)
+template <typename R>
+__device__ __forceinline__ void np_fallback(const R ca[3], const R aa[3], const R cb[3], const R ab[3], R r, R hh,
+                                            R n[3], R& dist) {
+  const R lx = ca[0] - cb[0], ly = ca[1] - cb[1], lz = ca[2] - cb[2];
   const R c2 = pc_dot(lx, ly, lz, lx, ly, lz);
   R best = R(0);
   bool have = false;
@@ -418,9 +533,49 @@ __device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], cons
     }
   }
   dist = -best;
-#ifdef GPD_CONTACT_STATS
-  atomicAdd(&g_pc_hist[253], 1ull);   // narrowphases ending in the least-overlap fallback
-#endif
+}
+// bullet_mb.face_points: the face manifold of a cap-to-cap contact - four points spanning the
+// overlap of the two near caps (the lens's tips on the line of the cap centres and its corners),
+// each carried along n to B's and A's cap planes: point on B fp[k] and distance fd[k]; returns
+// false (no points) unless the caps face each other and overlap.
+template <typename R>
+__device__ __forceinline__ bool face_points(const R ca[3], const R aa[3], const R cb[3], const R ab[3], const R n[3],
+                                            R radius, R half_height, R mg, R fp[4][3], R fd[4]) {
+  const R r = radius - mg, h = half_height - mg;
+  const R sa = pc_dot(cb[0] - ca[0], cb[1] - ca[1], cb[2] - ca[2], aa[0], aa[1], aa[2]) >= R(0) ? R(1) : R(-1);
+  const R sb = pc_dot(ca[0] - cb[0], ca[1] - cb[1], ca[2] - cb[2], ab[0], ab[1], ab[2]) >= R(0) ? R(1) : R(-1);
+  const R nuA[3] = {sa * aa[0], sa * aa[1], sa * aa[2]}, nuB[3] = {sb * ab[0], sb * ab[1], sb * ab[2]};
+  const R cB[3] = {cb[0] + sb * h * ab[0], cb[1] + sb * h * ab[1], cb[2] + sb * h * ab[2]};
+  const R cab[3] = {(ca[0] + sa * h * aa[0]) - cB[0], (ca[1] + sa * h * aa[1]) - cB[1], (ca[2] + sa * h * aa[2]) - cB[2]};
+  const R nb = pc_dot(n[0], n[1], n[2], nuB[0], nuB[1], nuB[2]), na = -pc_dot(n[0], n[1], n[2], nuA[0], nuA[1], nuA[2]);
+  const R kf = R(0.7071067811865475244008443621048490);   // FACE_COS
+  const R cn = pc_dot(cab[0], cab[1], cab[2], n[0], n[1], n[2]);
+  const R dl[3] = {cab[0] - cn * n[0], cab[1] - cn * n[1], cab[2] - cn * n[2]};
+  const R s2 = pc_dot(dl[0], dl[1], dl[2], dl[0], dl[1], dl[2]);
+  if (!(nb >= kf && na >= kf && s2 < R(4) * r * r)) return false;
+  const R s = g_sqrt(s2);
+  R u[3];
+  if (s > R(1e-9)) {
+    u[0] = dl[0] / s; u[1] = dl[1] / s; u[2] = dl[2] / s;
+  } else {
+    R t2[3];
+    plane_space(n, u, t2);
+  }
+  const R v[3] = {n[1] * u[2] - n[2] * u[1], n[2] * u[0] - n[0] * u[2], n[0] * u[1] - n[1] * u[0]};
+  const R w2 = r * r - R(0.25) * s2;
+  const R w = g_sqrt(w2 > R(0) ? w2 : R(0));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const R cu = k == 0 ? s - r : (k == 1 ? r : R(0.5) * s);
+    const R cv = k == 2 ? w : (k == 3 ? -w : R(0));
+    const R p0 = cu * u[0] + cv * v[0], p1 = cu * u[1] + cv * v[1], p2 = cu * u[2] + cv * v[2];
+    const R tb = -pc_dot(p0, p1, p2, nuB[0], nuB[1], nuB[2]) / nb;
+    const R ta = pc_dot(cab[0] - p0, cab[1] - p1, cab[2] - p2, nuA[0], nuA[1], nuA[2]) / -na;
+    const R tm = tb + mg;
+    fp[k][0] = cB[0] + p0 + tm * n[0]; fp[k][1] = cB[1] + p1 + tm * n[1]; fp[k][2] = cB[2] + p2 + tm * n[2];
+    fd[k] = (ta - tb) - R(2) * mg;
+  }
+  return true;
 }
 #ifndef GPD_DC_DIAG
 #define GPD_DC_DIAG 0   // diagnostic builds only: 1 = broadphase only (no solve compiled),
@@ -428,19 +583,33 @@ __device__ __forceinline__ void pair_geometry(const R ca[3], const R aa[3], cons
                         // solve called but returning at once, 8 = narrowphase and rows, no iterations
 #endif
 enum { DC_CX, DC_CY, DC_CZ, DC_AX, DC_AY, DC_AZ, DC_PX, DC_PY, DC_PZ, DC_VX, DC_VY, DC_VZ, DC_WX, DC_WY, DC_WZ,
-       DC_I00, DC_I01, DC_I02, DC_I11, DC_I12, DC_I22, DC_DLX, DC_DLY, DC_DLZ, DC_DAX, DC_DAY, DC_DAZ, DC_N };
+       DC_I00, DC_I01, DC_I02, DC_I11, DC_I12, DC_I22, DC_DLX, DC_DLY, DC_DLZ, DC_DAX, DC_DAY, DC_DAZ,
+       DC_R0, DC_R1, DC_R3, DC_R4, DC_R6, DC_R7, DC_N };   // DC_R*: the basis entries beside the axis (Rm[2,5,8])
 constexpr int kDcChunks = 32;   // pair chunks of a block: <= 64 (D-1) / 2 / 64 + 1 for D <= 64
+constexpr int kDcPts = 5;       // contacts per pair: the closest point + the face manifold's four
+constexpr int kDcConPasses = kDcPts * kDcChunks;   // 64-contact passes of a block
+// a near pair's narrowphase, staged for the lanes that set up its contacts' rows
+enum { DS_N = 0, DS_PB = 3, DS_D = 6, DS_FP = 7, DS_FD = 19, DS_NUM = 23 };
+// an island drone's plane rows (bullet_mb._plane_rows_world): world arms, rhs, 1/jacDiag, jacDiag, impulses
+enum { DI_RW = 0, DI_RHS = 12, DI_JDI = 24, DI_JDN = 36, DI_LAM = 40, DI_NUM = 52 };
 template <typename R>
 struct DcLds {
   R dc[DC_N][kWave];                  // drone columns
-  unsigned long long nearw[kDcChunks], contw[kDcChunks];   // pairs in reach / in contact, by chunk
+  R st[DS_NUM][kWave];                // this pass's near pairs' narrowphases (normal, point, distance, face points)
+  R isl[DI_NUM][kWave];               // island drones' plane rows
+  R rim[4][7][kWave];                 // narrowphase: per near slot and rim, the best start's (x, y) and distance
+  unsigned long long nearw[kDcChunks], contw[kDcConPasses];   // pairs in reach (by chunk) / contacts (by pass)
   R eres[kWave];                      // per env: this iteration's largest squared residual
   int edone[kWave];                   // per env: solve finished
   int stouch[kWave];                  // drone in a contact
-  int cij[kWave], clev[kWave];        // pass 0: the lane's contact (i | j << 8) and its level
+  int island[kWave];                  // drone whose plane rows the solve takes (its own plane solve skipped)
+  int cij[kWave], clev[kWave];        // contacts 0..63: the lane's contact (i | j << 8) and its level
+  int cij1[kWave], clev1[kWave];      // contacts 64..127 (the lanes' second register row)
   int dlev[kWave];                    // per drone: the level of its last contact (level pass)
   int nsp[kWave], nsij[kWave];        // this pass's near pairs: pair index, i | j << 8
-  int ecnt[kWave], ek0[kWave], ek1[kWave];   // per env: contacts, their near-index range [ek0, ek1)
+  int qmap[kDcPts * kWave];           // this pass's contacts: near slot | point << 8 (0 closest, 1..4 face)
+  int npdone[kWave];                  // narrowphase: near slot resolved at an earlier margin level
+  int ecnt[kWave], ek0[kWave], ek1[kWave];   // per env: contacts, their contact-index range [ek0, ek1)
 };
 // one LDS block per instantiation, shared by the hook (inlined) and the solve (a call)
 template <typename R>
@@ -452,7 +621,7 @@ __device__ __forceinline__ DcLds<R>& dc_lds() {
 struct DcPairs {
   int npairs, P, D, nch;   // pairs of the block's whole envs, per env, drones per env, chunks
   int pij[4];              // chunks 0..3: this lane's pair as (lane i) | (lane j) << 8, -1 = none
-  int pmagic;              // p / P == (p * pmagic) >> 20 for p < npairs (host-checked)
+  int pmagic;              // p / P == (p * pmagic) >> 24 for p < npairs (host-checked)
   const int* tab;          // [P] pair q -> i | j << 8 (env-local drones), for chunks >= 4
   void* rows;              // this block's row store (chunks >= 1), or null
 };
@@ -477,7 +646,7 @@ __device__ __forceinline__ int dc_pair_of(const DcPairs& dp, int ch, int p) {
   return ch == 0 ? dp.pij[0] : (ch == 1 ? dp.pij[1] : (ch == 2 ? dp.pij[2] : dp.pij[3]));
 }
 __device__ __forceinline__ int dc_pair_lanes(const DcPairs& dp, int p) {
-  const int e = (p * dp.pmagic) >> 20;
+  const int e = (p * dp.pmagic) >> 24;
   const int t = dp.tab[p - e * dp.P];
   return ((t & 255) + e * dp.D) | (((t >> 8) + e * dp.D) << 8);
 }
@@ -522,23 +691,46 @@ __device__ __forceinline__ bool dc_near(const DcLds<R>& L, int i, int j, const C
   }
   return false;
 }
-// a contact's rows: directions (n, t1, t2), arms x direction for A (= i) and B (= j), I_w^-1 of
-// those, rhs, 1/jacDiag, the normal row's jacDiag, impulses
+// a contact's rows: directions (n, t1, t2), the arms of A (= i) and B (= j) from their COMs, rhs,
+// 1/jacDiag, the normal row's jacDiag, impulses - 25 reals (the angular Jacobians r x d and their
+// I_w^-1 images are formed at each use from the arms and the drones' inverse inertias, the same
+// operations as at the setup, so the values are the same bit for bit)
 template <typename R>
 struct DcRow {
-  R d[3][3], A[3][3], B[3][3], gA[3][3], gB[3][3], rhs[3], jdi[3], jdn, lam[3];
+  R d[3][3], ra[3], rb[3], rhs[3], jdi[3], jdn, lam[3];
   int i, j, env, rank;
 };
+constexpr int kRowReal = 25, kRowLam = 22;   // reals of a row; offset of lam
+// the world inverse inertias (symmetric: 00 01 02 11 12 22) of a row's two drones
+template <typename R>
+struct DcInv {
+  R a[6], b[6];
+};
+template <typename R>
+__device__ __forceinline__ void dc_inv(const DcLds<R>& L, int i, int j, DcInv<R>& I) {
+#pragma unroll
+  for (int x = 0; x < 6; ++x) { I.a[x] = L.dc[DC_I00 + x][i]; I.b[x] = L.dc[DC_I00 + x][j]; }
+}
+template <typename R>
+__device__ __forceinline__ void dc_cross(const R r[3], const R d[3], R o[3]) {
+  o[0] = r[1] * d[2] - r[2] * d[1]; o[1] = r[2] * d[0] - r[0] * d[2]; o[2] = r[0] * d[1] - r[1] * d[0];
+}
+template <typename R>
+__device__ __forceinline__ void dc_symv(const R m[6], const R v[3], R o[3]) {
+  o[0] = pc_dot(m[0], m[1], m[2], v[0], v[1], v[2]);
+  o[1] = pc_dot(m[1], m[3], m[4], v[0], v[1], v[2]);
+  o[2] = pc_dot(m[2], m[4], m[5], v[0], v[1], v[2]);
+}
 template <typename R>
 __device__ __forceinline__ void dc_row_setup(const DcLds<R>& L, int i, int j, const R n[3], const R pb[3], R dist,
                                              const Consts<R>& c, R inv_m, R idt, DcRow<R>& w) {
   const R pa[3] = {pb[0] + n[0] * dist, pb[1] + n[1] * dist, pb[2] + n[2] * dist};
-  const R ra[3] = {pa[0] - L.dc[DC_PX][i], pa[1] - L.dc[DC_PY][i], pa[2] - L.dc[DC_PZ][i]};
-  const R rb[3] = {pb[0] - L.dc[DC_PX][j], pb[1] - L.dc[DC_PY][j], pb[2] - L.dc[DC_PZ][j]};
+  w.ra[0] = pa[0] - L.dc[DC_PX][i]; w.ra[1] = pa[1] - L.dc[DC_PY][i]; w.ra[2] = pa[2] - L.dc[DC_PZ][i];
+  w.rb[0] = pb[0] - L.dc[DC_PX][j]; w.rb[1] = pb[1] - L.dc[DC_PY][j]; w.rb[2] = pb[2] - L.dc[DC_PZ][j];
   R t1[3], t2[3];
   plane_space(n, t1, t2);
-  const R ia[6] = {L.dc[DC_I00][i], L.dc[DC_I01][i], L.dc[DC_I02][i], L.dc[DC_I11][i], L.dc[DC_I12][i], L.dc[DC_I22][i]};
-  const R ib[6] = {L.dc[DC_I00][j], L.dc[DC_I01][j], L.dc[DC_I02][j], L.dc[DC_I11][j], L.dc[DC_I12][j], L.dc[DC_I22][j]};
+  DcInv<R> I;
+  dc_inv(L, i, j, I);
   const R dvx = L.dc[DC_VX][i] - L.dc[DC_VX][j], dvy = L.dc[DC_VY][i] - L.dc[DC_VY][j], dvz = L.dc[DC_VZ][i] - L.dc[DC_VZ][j];
   const R wa[3] = {L.dc[DC_WX][i], L.dc[DC_WY][i], L.dc[DC_WZ][i]};
   const R wb[3] = {L.dc[DC_WX][j], L.dc[DC_WY][j], L.dc[DC_WZ][j]};
@@ -546,18 +738,12 @@ __device__ __forceinline__ void dc_row_setup(const DcLds<R>& L, int i, int j, co
   for (int q = 0; q < 3; ++q) {
     const R* d = q == 0 ? n : (q == 1 ? t1 : t2);
     w.d[q][0] = d[0]; w.d[q][1] = d[1]; w.d[q][2] = d[2];
-    R* A = w.A[q];
-    R* B = w.B[q];
-    A[0] = ra[1] * d[2] - ra[2] * d[1]; A[1] = ra[2] * d[0] - ra[0] * d[2]; A[2] = ra[0] * d[1] - ra[1] * d[0];
-    B[0] = rb[1] * d[2] - rb[2] * d[1]; B[1] = rb[2] * d[0] - rb[0] * d[2]; B[2] = rb[0] * d[1] - rb[1] * d[0];
-    w.gA[q][0] = pc_dot(ia[0], ia[1], ia[2], A[0], A[1], A[2]);
-    w.gA[q][1] = pc_dot(ia[1], ia[3], ia[4], A[0], A[1], A[2]);
-    w.gA[q][2] = pc_dot(ia[2], ia[4], ia[5], A[0], A[1], A[2]);
-    w.gB[q][0] = pc_dot(ib[0], ib[1], ib[2], B[0], B[1], B[2]);
-    w.gB[q][1] = pc_dot(ib[1], ib[3], ib[4], B[0], B[1], B[2]);
-    w.gB[q][2] = pc_dot(ib[2], ib[4], ib[5], B[0], B[1], B[2]);
-    const R jd = (inv_m + inv_m + pc_dot(A[0], A[1], A[2], w.gA[q][0], w.gA[q][1], w.gA[q][2])) +
-                 pc_dot(B[0], B[1], B[2], w.gB[q][0], w.gB[q][1], w.gB[q][2]);
+    R A[3], B[3], gA[3], gB[3];
+    dc_cross(w.ra, d, A);
+    dc_cross(w.rb, d, B);
+    dc_symv(I.a, A, gA);
+    dc_symv(I.b, B, gB);
+    const R jd = (inv_m + inv_m + pc_dot(A[0], A[1], A[2], gA[0], gA[1], gA[2])) + pc_dot(B[0], B[1], B[2], gB[0], gB[1], gB[2]);
     const R rel = (pc_dot(d[0], d[1], d[2], dvx, dvy, dvz) + pc_dot(A[0], A[1], A[2], wa[0], wa[1], wa[2])) -
                   pc_dot(B[0], B[1], B[2], wb[0], wb[1], wb[2]);
     // 1/jd and x/dt as Newton-refined reciprocals (jd >= 2/m > 0): ~1 ulp from the quotients
@@ -579,33 +765,41 @@ __device__ __forceinline__ void dc_row_setup(const DcLds<R>& L, int i, int j, co
 // then angular)
 template <typename R>
 __device__ __forceinline__ R dc_jv(const DcRow<R>& w, int q, const R vi[6], const R vj[6]) {
+  R A[3], B[3];
+  dc_cross(w.ra, w.d[q], A);
+  dc_cross(w.rb, w.d[q], B);
   return (pc_dot(w.d[q][0], w.d[q][1], w.d[q][2], vi[0] - vj[0], vi[1] - vj[1], vi[2] - vj[2]) +
-          pc_dot(w.A[q][0], w.A[q][1], w.A[q][2], vi[3], vi[4], vi[5])) -
-         pc_dot(w.B[q][0], w.B[q][1], w.B[q][2], vj[3], vj[4], vj[5]);
+          pc_dot(A[0], A[1], A[2], vi[3], vi[4], vi[5])) -
+         pc_dot(B[0], B[1], B[2], vj[3], vj[4], vj[5]);
 }
 template <typename R>
-__device__ __forceinline__ void dc_apply(const DcRow<R>& w, int q, R delta, R inv_m, R vi[6], R vj[6]) {
+__device__ __forceinline__ void dc_apply(const DcRow<R>& w, int q, R delta, R inv_m, R vi[6], R vj[6], const DcInv<R>& I) {
+  R A[3], B[3], gA[3], gB[3];
+  dc_cross(w.ra, w.d[q], A);
+  dc_cross(w.rb, w.d[q], B);
+  dc_symv(I.a, A, gA);
+  dc_symv(I.b, B, gB);
   const R dm = inv_m * delta;
   vi[0] = vi[0] + w.d[q][0] * dm; vi[1] = vi[1] + w.d[q][1] * dm; vi[2] = vi[2] + w.d[q][2] * dm;
-  vi[3] = vi[3] + w.gA[q][0] * delta; vi[4] = vi[4] + w.gA[q][1] * delta; vi[5] = vi[5] + w.gA[q][2] * delta;
+  vi[3] = vi[3] + gA[0] * delta; vi[4] = vi[4] + gA[1] * delta; vi[5] = vi[5] + gA[2] * delta;
   vj[0] = vj[0] - w.d[q][0] * dm; vj[1] = vj[1] - w.d[q][1] * dm; vj[2] = vj[2] - w.d[q][2] * dm;
-  vj[3] = vj[3] - w.gB[q][0] * delta; vj[4] = vj[4] - w.gB[q][1] * delta; vj[5] = vj[5] - w.gB[q][2] * delta;
+  vj[3] = vj[3] - gB[0] * delta; vj[4] = vj[4] - gB[1] * delta; vj[5] = vj[5] - gB[2] * delta;
 }
 // one normal row (bullet_mb.drone_contact's normal loop); returns the row's squared residual
 template <typename R>
-__device__ __forceinline__ R dc_normal(DcRow<R>& w, R inv_m, R vi[6], R vj[6]) {
+__device__ __forceinline__ R dc_normal(DcRow<R>& w, R inv_m, R vi[6], R vj[6], const DcInv<R>& I) {
   R delta = w.rhs[0] - w.jdi[0] * dc_jv(w, 0, vi, vj);
   const R sum = w.lam[0] + delta;
   const bool neg = sum < R(0);
   delta = neg ? -w.lam[0] : delta;
   w.lam[0] = neg ? R(0) : sum;
-  dc_apply(w, 0, delta, inv_m, vi, vj);
+  dc_apply(w, 0, delta, inv_m, vi, vj, I);
   const R rr = delta * w.jdn;
   return rr * rr;
 }
 // one friction pair on the cone (only while the normal impulse is positive); squared residual
 template <typename R>
-__device__ __forceinline__ R dc_friction(DcRow<R>& w, R mu, R inv_m, R vi[6], R vj[6]) {
+__device__ __forceinline__ R dc_friction(DcRow<R>& w, R mu, R inv_m, R vi[6], R vj[6], const DcInv<R>& I) {
   if (!(w.lam[0] > R(0))) return R(0);
   const R lim = mu * w.lam[0];
   R s1 = w.lam[1] + (w.rhs[1] - w.jdi[1] * dc_jv(w, 1, vi, vj));
@@ -619,32 +813,33 @@ __device__ __forceinline__ R dc_friction(DcRow<R>& w, R mu, R inv_m, R vi[6], R 
   const R e1 = s1 - w.lam[1], e2 = s2 - w.lam[2];
   w.lam[1] = s1;
   w.lam[2] = s2;
-  dc_apply(w, 1, e1, inv_m, vi, vj);
-  dc_apply(w, 2, e2, inv_m, vi, vj);
+  dc_apply(w, 1, e1, inv_m, vi, vj, I);
+  dc_apply(w, 2, e2, inv_m, vi, vj, I);
   const R rr = e1 + e2;
   return rr * rr;
 }
-// the row store: per chunk, element x of lane ln at chunk[x * 64 + ln] (55 reals), then the four
-// ints (i, j, env, rank) at ints[k * 64 + ln] behind them
+// the row store: per chunk, element x of lane ln at chunk[x * 64 + ln] (kRowReal reals), then the
+// four ints (i, j, env, rank) at ints[k * 64 + ln] behind them
 template <typename R>
 __device__ __forceinline__ void dc_row_store(R* chunk, int ln, const DcRow<R>& w) {
   const R* src = &w.d[0][0];
 #pragma unroll
-  for (int x = 0; x < 55; ++x) chunk[x * kWave + ln] = src[x];
-  int* di = reinterpret_cast<int*>(chunk + 55 * kWave);
+  for (int x = 0; x < kRowReal; ++x) chunk[x * kWave + ln] = src[x];
+  int* di = reinterpret_cast<int*>(chunk + kRowReal * kWave);
   di[ln] = w.i; di[kWave + ln] = w.j; di[2 * kWave + ln] = w.env; di[3 * kWave + ln] = w.rank;
 }
 template <typename R>
 __device__ __forceinline__ void dc_row_load(const R* chunk, int ln, DcRow<R>& w) {
   R* dst = &w.d[0][0];
 #pragma unroll
-  for (int x = 0; x < 55; ++x) dst[x] = chunk[x * kWave + ln];
-  const int* si = reinterpret_cast<const int*>(chunk + 55 * kWave);
+  for (int x = 0; x < kRowReal; ++x) dst[x] = chunk[x * kWave + ln];
+  const int* si = reinterpret_cast<const int*>(chunk + kRowReal * kWave);
   w.i = si[ln]; w.j = si[kWave + ln]; w.env = si[2 * kWave + ln]; w.rank = si[3 * kWave + ln];
 }
-// R elements of one row in the store: 55 reals + 4 ints, column-major over the chunk's 64 lanes
+// R elements of one row in the store: kRowReal reals + 4 ints, column-major over the chunk's 64 lanes
 template <typename R>
-__host__ __device__ constexpr int dc_row_reals() { return 55 + (4 * 4 + (int)sizeof(R) - 1) / (int)sizeof(R); }
+__host__ __device__ constexpr int dc_row_reals() { return kRowReal + (4 * 4 + (int)sizeof(R) - 1) / (int)sizeof(R); }
+constexpr int kDcRegRows = 2;   // contacts 0..127 of a block in the lanes' registers (two rows a lane)
 
 // the setup and solve: a call, so that its registers stay out of the substep loop that almost
 // never enters it (the caller parks its own values in LDS around it: bullet_substep)
@@ -656,8 +851,312 @@ __host__ __device__ constexpr int dc_row_reals() { return 55 + (4 * 4 + (int)siz
 #else
 #define GPD_DC_ATTR __noinline__
 #endif
+// wave-wide exclusive prefix sum of small non-negative ints (and the total)
+__device__ __forceinline__ int wave_excl_scan(int x, int ln, int& total) {
+  int v = x;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int y = __shfl_up(v, o);
+    if (ln >= o) v += y;
+  }
+  total = __shfl(v, kWave - 1);
+  return v - x;
+}
+// an island drone's plane rows (bullet_mb._plane_rows_world; plane_contact_regs' world form): lane ln's
+// columns of L.isl; returns whether any of its four points is active
 template <typename R>
-__device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln, DcPairs dp) {
+__device__ __forceinline__ bool island_rows(DcLds<R>& L, int ln, const Consts<R>& c, R inv_m, R idt) {
+  const R Rm[9] = {L.dc[DC_R0][ln], L.dc[DC_R1][ln], L.dc[DC_AX][ln], L.dc[DC_R3][ln], L.dc[DC_R4][ln],
+                   L.dc[DC_AY][ln], L.dc[DC_R6][ln], L.dc[DC_R7][ln], L.dc[DC_AZ][ln]};
+  const R i00 = L.dc[DC_I00][ln], i01 = L.dc[DC_I01][ln], i02 = L.dc[DC_I02][ln], i11 = L.dc[DC_I11][ln],
+          i12 = L.dc[DC_I12][ln], i22 = L.dc[DC_I22][ln];
+  const R px = L.dc[DC_PX][ln], py = L.dc[DC_PY][ln], pz = L.dc[DC_PZ][ln];
+  const R vx = L.dc[DC_VX][ln], vy = L.dc[DC_VY][ln], vz = L.dc[DC_VZ][ln];
+  const R wx = L.dc[DC_WX][ln], wy = L.dc[DC_WY][ln], wz = L.dc[DC_WZ][ln];
+  const R zc = (-Rm[8] < R(0) ? -c.cyl_hh : c.cyl_hh) + c.cyl_zoff;
+  const R cr = c.cyl_r;
+  bool any = false;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const R rx = p == 0 ? cr : (p == 2 ? -cr : R(0)), ry = p == 1 ? cr : (p == 3 ? -cr : R(0));
+    const R rwx = pc_dot(Rm[0], Rm[1], Rm[2], rx, ry, zc);
+    const R rwy = pc_dot(Rm[3], Rm[4], Rm[5], rx, ry, zc);
+    const R rwz = pc_dot(Rm[6], Rm[7], Rm[8], rx, ry, zc);
+    L.isl[DI_RW + 3 * p][ln] = rwx; L.isl[DI_RW + 3 * p + 1][ln] = rwy; L.isl[DI_RW + 3 * p + 2][ln] = rwz;
+    const R dist = pz + rwz;
+    const bool act = dist < c.brk && g_abs(px + rwx) <= c.plane_half && g_abs(py + rwy) <= c.plane_half;
+    any = any || act;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const R ax = j == 0 ? rwy : (j == 1 ? rwz : R(0));
+      const R ay = j == 0 ? -rwx : (j == 1 ? R(0) : rwz);
+      const R az = j == 0 ? R(0) : (j == 1 ? -rwx : -rwy);
+      const R gx = pc_dot(i00, i01, i02, ax, ay, az), gy = pc_dot(i01, i11, i12, ax, ay, az),
+              gz = pc_dot(i02, i12, i22, ax, ay, az);
+      const R jd = inv_m + pc_dot(ax, ay, az, gx, gy, gz);
+      const R inv = g_rcp(jd);
+      const R vl = j == 0 ? vz : (j == 1 ? -vy : vx);
+      const R rel = vl + pc_dot(ax, ay, az, wx, wy, wz);
+      R r;
+      if (j == 0) {
+        const R pen = dist + c.slop;
+        r = pen > R(0) ? (-rel - pen * idt) * inv : (-pen * c.erp * idt - rel) * inv;
+        L.isl[DI_JDN + p][ln] = act ? jd : R(0);
+      } else {
+        r = -rel * inv;
+      }
+      L.isl[DI_JDI + 3 * p + j][ln] = act ? inv : R(0);
+      L.isl[DI_RHS + 3 * p + j][ln] = act ? r : R(0);
+      L.isl[DI_LAM + 3 * p + j][ln] = R(0);
+    }
+  }
+  return any;
+}
+// one sweep of an island drone's plane rows (normal rows or friction pairs) on its LDS deltas;
+// returns the largest squared residual
+template <typename R>
+__device__ __forceinline__ R island_sweep(DcLds<R>& L, int ln, bool friction, R mu, R inv_m) {
+  R dl0 = L.dc[DC_DLX][ln], dl1 = L.dc[DC_DLY][ln], dl2 = L.dc[DC_DLZ][ln];
+  R da0 = L.dc[DC_DAX][ln], da1 = L.dc[DC_DAY][ln], da2 = L.dc[DC_DAZ][ln];
+  const R i00 = L.dc[DC_I00][ln], i01 = L.dc[DC_I01][ln], i02 = L.dc[DC_I02][ln], i11 = L.dc[DC_I11][ln],
+          i12 = L.dc[DC_I12][ln], i22 = L.dc[DC_I22][ln];
+  R res = R(0);
+  for (int p = 0; p < 4; ++p) {
+    const R rwx = L.isl[DI_RW + 3 * p][ln], rwy = L.isl[DI_RW + 3 * p + 1][ln], rwz = L.isl[DI_RW + 3 * p + 2][ln];
+    if (!friction) {
+      if (!(L.isl[DI_JDN + p][ln] > R(0))) continue;   // inactive point (the oracle has no row)
+      const R ax = rwy, ay = -rwx;
+      const R jv = dl2 + (ax * da0 + ay * da1);
+      R delta = L.isl[DI_RHS + 3 * p][ln] - L.isl[DI_JDI + 3 * p][ln] * jv;
+      const R lam = L.isl[DI_LAM + 3 * p][ln];
+      const R sum = lam + delta;
+      const bool neg = sum < R(0);
+      delta = neg ? -lam : delta;
+      L.isl[DI_LAM + 3 * p][ln] = neg ? R(0) : sum;
+      dl2 = dl2 + inv_m * delta;
+      da0 = da0 + pc_dot(i00, i01, i02, ax, ay, R(0)) * delta;
+      da1 = da1 + pc_dot(i01, i11, i12, ax, ay, R(0)) * delta;
+      da2 = da2 + pc_dot(i02, i12, i22, ax, ay, R(0)) * delta;
+      const R rr = delta * L.isl[DI_JDN + p][ln];
+      res = g_fmax(res, rr * rr);
+    } else {
+      const R lnrm = L.isl[DI_LAM + 3 * p][ln];
+      if (!(lnrm > R(0))) continue;
+      const R lim = mu * lnrm;
+      const R l1 = L.isl[DI_LAM + 3 * p + 1][ln], l2 = L.isl[DI_LAM + 3 * p + 2][ln];
+      // (0,-1,0): a = (rz, 0, -rx); (1,0,0): a = (0, rz, -ry)
+      const R j1 = (rwz * da0 - rwx * da2) - dl1;
+      const R j2 = (rwz * da1 - rwy * da2) + dl0;
+      R s1 = l1 + (L.isl[DI_RHS + 3 * p + 1][ln] - L.isl[DI_JDI + 3 * p + 1][ln] * j1);
+      R s2 = l2 + (L.isl[DI_RHS + 3 * p + 2][ln] - L.isl[DI_JDI + 3 * p + 2][ln] * j2);
+      const R m2 = s1 * s1 + s2 * s2;
+      if (m2 > lim * lim) {
+        const R f = lim * g_rsqrt1(m2);
+        s1 = s1 * f;
+        s2 = s2 * f;
+      }
+      const R d1 = s1 - l1, d2 = s2 - l2;
+      L.isl[DI_LAM + 3 * p + 1][ln] = s1;
+      L.isl[DI_LAM + 3 * p + 2][ln] = s2;
+      dl1 = dl1 - inv_m * d1;
+      dl0 = dl0 + inv_m * d2;
+      da0 = da0 + pc_dot(i00, i01, i02, rwz, R(0), -rwx) * d1;
+      da1 = da1 + pc_dot(i01, i11, i12, rwz, R(0), -rwx) * d1;
+      da2 = da2 + pc_dot(i02, i12, i22, rwz, R(0), -rwx) * d1;
+      da0 = da0 + pc_dot(i00, i01, i02, R(0), rwz, -rwy) * d2;
+      da1 = da1 + pc_dot(i01, i11, i12, R(0), rwz, -rwy) * d2;
+      da2 = da2 + pc_dot(i02, i12, i22, R(0), rwz, -rwy) * d2;
+      const R rr = d1 + d2;
+      res = g_fmax(res, rr * rr);
+    }
+  }
+  L.dc[DC_DLX][ln] = dl0; L.dc[DC_DLY][ln] = dl1; L.dc[DC_DLZ][ln] = dl2;
+  L.dc[DC_DAX][ln] = da0; L.dc[DC_DAY][ln] = da1; L.dc[DC_DAZ][ln] = da2;
+  return res;
+}
+template <typename R>
+__device__ __forceinline__ void eres_max(DcLds<R>& L, int env, R rr) {
+  // the max through an LDS atomic on the bit pattern (non-negative floats order as unsigned integers)
+  if (sizeof(R) == 8)
+    atomicMax(reinterpret_cast<unsigned long long*>(&L.eres[env]), (unsigned long long)__double_as_longlong((double)rr));
+  else
+    atomicMax(reinterpret_cast<unsigned int*>(&L.eres[env]), (unsigned int)__float_as_uint((float)rr));
+}
+// The narrowphases of a pass's nthis near pairs (L.nsij[0..nthis)): bullet_mb.pair_geometry per pair,
+// its 4 x 8 rim Newton chains as 32 tasks over the lanes (task t: slot t / 32, rim (t / 8) % 4,
+// start t % 8; the best start per rim by a butterfly over 8 lanes, ties to the lower start), the
+// closed-form candidates and the selection by the pair's own lane (lane = slot), margin level by
+// margin level while some pair's cores overlap; then the fallback and the face manifold.  Lane
+// ln < nthis stages its pair's result in L.st and its face-point mask in L.nsp[ln] and returns its
+// contact count.  A call: its registers stay out of dc_solve's Gauss-Seidel loops.
+template <typename R>
+__device__ __noinline__ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthis) {
+  DcLds<R>& L = dc_lds<R>();
+  const Consts<R>& c = *cp;
+#ifdef GPD_CONTACT_STATS
+  unsigned long long tn0 = __builtin_readcyclecounter(), tn_task = 0, tn_sel = 0;
+#endif
+  const R margins[4] = {R(0.001), R(0.003), R(0.006), R(0.011)};
+  const bool mine = ln < nthis;
+  const int pij = mine ? L.nsij[ln] : 0;
+  const int mi = pij & 255, mj = pij >> 8;
+  const R ca[3] = {L.dc[DC_CX][mi], L.dc[DC_CY][mi], L.dc[DC_CZ][mi]}, aa[3] = {L.dc[DC_AX][mi], L.dc[DC_AY][mi], L.dc[DC_AZ][mi]};
+  const R cb[3] = {L.dc[DC_CX][mj], L.dc[DC_CY][mj], L.dc[DC_CZ][mj]}, ab[3] = {L.dc[DC_AX][mj], L.dc[DC_AY][mj], L.dc[DC_AZ][mj]};
+  NpPair<R> own;
+  np_pair(ca, aa, cb, ab, own);
+  bool found = !mine;
+  R n[3] = {R(0), R(0), R(1)}, pb[3] = {R(0), R(0), R(0)}, dist = R(0), mgf = R(-1);
+  R yl[3] = {R(0), R(0), R(0)};
+  L.npdone[ln] = found ? 1 : 0;
+  wave_lds_sync();
+  const int ntask = nthis * 32;
+#pragma unroll 1
+  for (int lv = 0; lv < 4; ++lv) {
+    if (__ballot(!found) == 0ull) break;
+    const R mg = margins[lv], r = c.cyl_r - mg, h = c.cyl_hh - mg;
+#pragma unroll 1
+    for (int t0 = 0; t0 < ntask; t0 += kWave) {
+      const int t = t0 + ln;
+      const int slot = (t >> 5) & 63, rim = (t >> 3) & 3, k = t & 7;
+      R f = R(INFINITY), x[3] = {R(0), R(0), R(0)}, y[3] = {R(0), R(0), R(0)};
+      bool need = false;
+      if (t < ntask && !L.npdone[slot]) {
+        const int pj = L.nsij[slot];
+        const int ti = pj & 255, tj = pj >> 8;
+        const R tca[3] = {L.dc[DC_CX][ti], L.dc[DC_CY][ti], L.dc[DC_CZ][ti]};
+        const R taa[3] = {L.dc[DC_AX][ti], L.dc[DC_AY][ti], L.dc[DC_AZ][ti]};
+        const R tcb[3] = {L.dc[DC_CX][tj], L.dc[DC_CY][tj], L.dc[DC_CZ][tj]};
+        const R tab[3] = {L.dc[DC_AX][tj], L.dc[DC_AY][tj], L.dc[DC_AZ][tj]};
+        NpPair<R> q;
+        np_pair(tca, taa, tcb, tab, q);
+        bool far_a, far_b;
+        np_far(q, r, h, far_a, far_b);
+        need = rim < 2 || (rim == 2 ? far_a : far_b);
+        if (need) np_rim_task(q, rim, k, r, h, f, x, y);
+      }
+      // the rim's result: the lowest start within RIM_SAME of the group's smallest f (bullet_mb.rim_closest)
+      R fmin = f;
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) fmin = g_min1(fmin, __shfl_xor(fmin, o));
+      const unsigned long long near = __ballot(f <= fmin * (R(1) + NpTol<R>::same));
+      const int g0 = ln & ~7;
+      const int src = g0 + __builtin_ctz((unsigned)((near >> g0) & 0xffull) | 0x100u);
+#pragma unroll
+      for (int e = 0; e < 3; ++e) { x[e] = __shfl(x[e], src); y[e] = __shfl(y[e], src); }
+      if (t < ntask && k == 0) {
+#pragma unroll
+        for (int e = 0; e < 3; ++e) { L.rim[rim][e][slot] = x[e]; L.rim[rim][3 + e][slot] = y[e]; }
+        L.rim[rim][6][slot] = need ? R(0) : R(INFINITY);   // a rim the pair does not need
+      }
+    }
+    wave_lds_sync();
+#ifdef GPD_CONTACT_STATS
+    const unsigned long long tn1 = __builtin_readcyclecounter();
+    tn_task += tn1 - tn0;
+#endif
+    if (!found) {
+      bool far_a, far_b;
+      np_far(own, r, h, far_a, far_b);
+      R cx[3][3], cy[3][3], cd[3];
+      np_closed(own, r, h, far_a, far_b, cx, cy, cd);
+      R ds[7];
+      ds[0] = cd[0]; ds[1] = cd[1]; ds[2] = cd[2];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const R dx = L.rim[m][0][ln] - L.rim[m][3][ln], dy = L.rim[m][1][ln] - L.rim[m][4][ln],
+                dz = L.rim[m][2][ln] - L.rim[m][5][ln];
+        ds[3 + m] = L.rim[m][6][ln] == R(0) ? g_sqrt(pc_dot(dx, dy, dz, dx, dy, dz)) : R(INFINITY);
+      }
+      R dmin = ds[0];
+#pragma unroll
+      for (int m = 1; m < 7; ++m) dmin = g_min1(dmin, ds[m]);
+      const R lim = dmin + NpTol<R>::tie;
+      int w = 6;
+#pragma unroll
+      for (int m = 6; m >= 0; --m) w = ds[m] <= lim ? m : w;
+      R bx[3], by[3], bd = ds[0];
+#pragma unroll
+      for (int e = 0; e < 3; ++e) { bx[e] = cx[0][e]; by[e] = cy[0][e]; }
+#pragma unroll
+      for (int m = 1; m < 7; ++m) {
+        if (w == m) {
+          bd = ds[m];
+#pragma unroll
+          for (int e = 0; e < 3; ++e) {
+            bx[e] = m < 3 ? cx[m < 3 ? m : 0][e] : L.rim[m >= 3 ? m - 3 : 0][e][ln];
+            by[e] = m < 3 ? cy[m < 3 ? m : 0][e] : L.rim[m >= 3 ? m - 3 : 0][3 + e][ln];
+          }
+        }
+      }
+      yl[0] = by[0]; yl[1] = by[1]; yl[2] = by[2];
+      if (bd > R(1e-4)) {
+        found = true;
+        mgf = mg;
+        const R ux = (bx[0] - by[0]) / bd, uy = (bx[1] - by[1]) / bd, uz = (bx[2] - by[2]) / bd;
+        n[0] = (ux * own.bp[0] + uy * own.bq[0]) + uz * ab[0];
+        n[1] = (ux * own.bp[1] + uy * own.bq[1]) + uz * ab[1];
+        n[2] = (ux * own.bp[2] + uy * own.bq[2]) + uz * ab[2];
+        const R wx = (by[0] * own.bp[0] + by[1] * own.bq[0]) + by[2] * ab[0],
+                wy = (by[0] * own.bp[1] + by[1] * own.bq[1]) + by[2] * ab[1],
+                wz = (by[0] * own.bp[2] + by[1] * own.bq[2]) + by[2] * ab[2];
+        pb[0] = cb[0] + (wx + n[0] * mg); pb[1] = cb[1] + (wy + n[1] * mg); pb[2] = cb[2] + (wz + n[2] * mg);
+        dist = bd - R(2) * mg;
+#ifdef GPD_CONTACT_STATS
+        atomicAdd(&g_pc_hist[249 + lv], 1ull);   // narrowphases ending at margin level lv
+#endif
+      }
+    }
+    L.npdone[ln] = found ? 1 : 0;
+    wave_lds_sync();
+#ifdef GPD_CONTACT_STATS
+    tn0 = __builtin_readcyclecounter();
+    tn_sel += tn0 - tn1;
+#endif
+  }
+#ifdef GPD_CONTACT_STATS
+  const unsigned long long tn2 = __builtin_readcyclecounter();
+#endif
+  if (!found) {   // cores overlapping at every level: the least-overlap fallback at the last level's point
+    pb[0] = cb[0] + ((yl[0] * own.bp[0] + yl[1] * own.bq[0]) + yl[2] * ab[0]);
+    pb[1] = cb[1] + ((yl[0] * own.bp[1] + yl[1] * own.bq[1]) + yl[2] * ab[1]);
+    pb[2] = cb[2] + ((yl[0] * own.bp[2] + yl[1] * own.bq[2]) + yl[2] * ab[2]);
+    np_fallback(ca, aa, cb, ab, c.cyl_r, c.cyl_hh, n, dist);
+#ifdef GPD_CONTACT_STATS
+    atomicAdd(&g_pc_hist[253], 1ull);   // narrowphases ending in the least-overlap fallback
+#endif
+  }
+#ifdef GPD_CONTACT_STATS
+  if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) {
+    atomicAdd(&g_pc_hist[kPcNp + 0], 1ull);          // passes
+    atomicAdd(&g_pc_hist[kPcNp + 1], tn_task);       // rim-task phases (all levels)
+    atomicAdd(&g_pc_hist[kPcNp + 2], tn_sel);        // selections (all levels)
+    atomicAdd(&g_pc_hist[kPcNp + 3], (unsigned long long)nthis);
+    atomicAdd(&g_pc_hist[kPcNp + 4], __builtin_readcyclecounter() - tn2);   // fallback + face points (to here)
+  }
+#endif
+  if (!mine) return 0;
+  const R brk = c.brk;
+  const bool con = dist < brk;
+  R fp[4][3], fd[4];
+  const bool face = con && mgf > R(0) && face_points(ca, aa, cb, ab, n, c.cyl_r, c.cyl_hh, mgf, fp, fd);
+  int fmask = 0;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) fmask |= (face && fd[m] < brk) ? (1 << m) : 0;
+  L.st[DS_N][ln] = n[0]; L.st[DS_N + 1][ln] = n[1]; L.st[DS_N + 2][ln] = n[2];
+  L.st[DS_PB][ln] = pb[0]; L.st[DS_PB + 1][ln] = pb[1]; L.st[DS_PB + 2][ln] = pb[2];
+  L.st[DS_D][ln] = dist;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    L.st[DS_FP + 3 * m][ln] = fp[m][0]; L.st[DS_FP + 3 * m + 1][ln] = fp[m][1]; L.st[DS_FP + 3 * m + 2][ln] = fp[m][2];
+    L.st[DS_FD + m][ln] = fd[m];
+  }
+  L.nsp[ln] = fmask;   // reused: the pair's face-point mask (its pair index is no longer needed)
+  return con ? 1 + __popc(fmask) : 0;
+}
+// plane: the ground plane is on (the island solve takes the plane rows of drones in a pair contact
+// that touch it, bullet_mb.drone_contact(plane=True)); nact: the block's drones
+template <typename R>
+__device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln, DcPairs dp, bool plane) {
 #ifdef GPD_CONTACT_STATS
   const unsigned long long t0 = __builtin_readcyclecounter();
   unsigned long long t1 = t0, t2 = t0, t_np = t0;
@@ -670,24 +1169,27 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
   L.dc[DC_DLX][ln] = R(0); L.dc[DC_DLY][ln] = R(0); L.dc[DC_DLZ][ln] = R(0);
   L.dc[DC_DAX][ln] = R(0); L.dc[DC_DAY][ln] = R(0); L.dc[DC_DAZ][ln] = R(0);
   L.stouch[ln] = 0;
+  L.island[ln] = 0;
 #if GPD_DC_DIAG == 7
   wave_lds_sync();
   return;   // diagnostic build: the call entered, nothing solved
 #endif
-  // ---- the near pairs compacted (pair order kept): near pair k to lane k % 64 of pass k / 64, so
-  // that one pass of narrowphases covers up to 64 near pairs from any of the block's pair chunks;
-  // each contact's rows set up by its lane - pass 0 in the lane's registers, later passes in the
-  // block's global row store
+  // ---- narrowphases: the near pairs compacted (pair order kept), near pair k to lane k % 64 of
+  // pass k / 64; each contact pair emits its closest point and its face manifold's points below the
+  // breaking threshold as consecutive contacts.  Contact c's rows are set up by lane c % 64: the
+  // first 128 contacts in the lanes' registers (two rows a lane), later ones in the block's global
+  // row store.
   int nnear = 0;
   for (int ch = 0; ch < dp.nch; ++ch) nnear += __popcll(L.nearw[ch]);
   if (ln < nenv) { L.ecnt[ln] = 0; L.ek0[ln] = 0x7fffffff; L.ek1[ln] = 0; }
   const int npass = (nnear + kWave - 1) / kWave;
-  DcRow<R> w0;
-  bool have0 = false;
-  w0.i = w0.j = 0;
-  w0.rank = 0;
+  DcRow<R> w0, w1;
+  bool have0 = false, have1 = false;
+  w0.i = w0.j = w1.i = w1.j = 0;
+  w0.rank = w1.rank = 0;
   R* rows = reinterpret_cast<R*>(dp.rows);
   constexpr int kRowR = dc_row_reals<R>();
+  int ncon = 0;   // contacts emitted so far (wave-uniform)
   for (int ps = 0; ps < npass; ++ps) {
     int base = -ps * kWave;
     for (int ch = 0; ch < dp.nch; ++ch) {
@@ -703,47 +1205,83 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
       base += __popcll(nw);
     }
     wave_lds_sync();
-    const int k = ps * kWave + ln;
-    bool con = false;
-    const int p = L.nsp[ln], pij = L.nsij[ln];
-    const int i = pij & 255, j = pij >> 8;
-    R n[3], pb[3], dist;
-    if (k < nnear) {
+    const int nthis = nnear - ps * kWave < kWave ? nnear - ps * kWave : kWave;
 #ifdef GPD_CONTACT_STATS
-      ++n_near;
+    n_near += ln < nthis ? 1 : 0;
 #endif
-      const R ca[3] = {L.dc[DC_CX][i], L.dc[DC_CY][i], L.dc[DC_CZ][i]}, aa[3] = {L.dc[DC_AX][i], L.dc[DC_AY][i], L.dc[DC_AZ][i]};
-      const R cb[3] = {L.dc[DC_CX][j], L.dc[DC_CY][j], L.dc[DC_CZ][j]}, ab[3] = {L.dc[DC_AX][j], L.dc[DC_AY][j], L.dc[DC_AZ][j]};
-      pair_geometry(ca, aa, cb, ab, c.cyl_r, c.cyl_hh, c.dc_beta, n, pb, dist);
-      con = dist < c.brk;
+    const int cnt = dc_narrow_pass<R>(cp, ln, nthis);
+    int total;
+    const int off = wave_excl_scan(cnt, ln, total);
+    if (cnt > 0) {
+      const int fmask = L.nsp[ln];
+      int q = off;
+      L.qmap[q++] = ln;
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        if ((fmask >> m) & 1) L.qmap[q++] = ln | ((m + 1) << 8);
     }
+    wave_lds_sync();
 #ifdef GPD_CONTACT_STATS
     if (ps == 0) t_np = __builtin_readcyclecounter();   // narrowphases of pass 0 done
 #endif
-    {
-      if (con) {
+    // the pass's contacts: contact c = ncon + q set up by lane c % 64
+    for (int t = 0; t * kWave < total; ++t) {
+      const int q = ((ln - ncon) & (kWave - 1)) + kWave * t;
+      if (q < total) {
+        const int cc = ncon + q;
+        const int qm = L.qmap[q];
+        const int sl = qm & 255, m = qm >> 8;
+        const int pj = L.nsij[sl];
+        const int i = pj & 255, j = pj >> 8;
+        const R n[3] = {L.st[DS_N][sl], L.st[DS_N + 1][sl], L.st[DS_N + 2][sl]};
+        R pb[3], dist;
+        if (m == 0) {
+          pb[0] = L.st[DS_PB][sl]; pb[1] = L.st[DS_PB + 1][sl]; pb[2] = L.st[DS_PB + 2][sl];
+          dist = L.st[DS_D][sl];
+        } else {
+          pb[0] = L.st[DS_FP + 3 * (m - 1)][sl]; pb[1] = L.st[DS_FP + 3 * (m - 1) + 1][sl];
+          pb[2] = L.st[DS_FP + 3 * (m - 1) + 2][sl];
+          dist = L.st[DS_FD + (m - 1)][sl];
+        }
         DcRow<R> w;
         dc_row_setup(L, i, j, n, pb, dist, c, inv_m, idt, w);
-        w.env = (p * dp.pmagic) >> 20;
+        w.env = i / dp.D;
         w.rank = 0;   // the level pass below re-ranks when some env holds two contacts
-        if (ps == 0) {
+        if (cc < kWave) {
           w0 = w;
           have0 = true;
-          L.cij[ln] = pij;
+          L.cij[ln] = pj;
+        } else if (cc < kDcRegRows * kWave) {
+          w1 = w;
+          have1 = true;
+          L.cij1[ln] = pj;
         } else {
-          dc_row_store(rows + (long long)(ps - 1) * kWave * kRowR, ln, w);
+          dc_row_store(rows + (long long)(cc / kWave - kDcRegRows) * kWave * kRowR, ln, w);
         }
         L.stouch[i] = 1;
         L.stouch[j] = 1;
         atomicAdd(&L.ecnt[w.env], 1);
-        atomicMin(&L.ek0[w.env], k);
-        atomicMax(&L.ek1[w.env], k + 1);
+        atomicMin(&L.ek0[w.env], cc);
+        atomicMax(&L.ek1[w.env], cc + 1);
       }
     }
-    const unsigned long long cw = __ballot(con);
-    if (ln == 0) L.contw[ps] = cw;
-    wave_lds_sync();   // this pass's near slots are rewritten by the next one
+    ncon += total;
+    wave_lds_sync();   // this pass's near slots and staging are rewritten by the next one
   }
+  const int ncpass = (ncon + kWave - 1) / kWave;
+  for (int x = ln; x < ncpass; x += kWave) {
+    const int lo = x * kWave, n_in = ncon - lo;
+    L.contw[x] = n_in >= kWave ? ~0ull : ((1ull << n_in) - 1ull);
+  }
+  // ---- the island: drones in a pair contact that touch the plane bring their plane rows
+  bool isl = false;
+  if (plane) {
+    wave_lds_sync();
+    if (L.stouch[ln]) isl = island_rows(L, ln, c, inv_m, idt);
+    L.island[ln] = isl ? 1 : 0;
+  }
+  const bool any_isl = __ballot(isl) != 0ull;
+  wave_lds_sync();
 #ifdef GPD_CONTACT_STATS
   t1 = __builtin_readcyclecounter();
 #endif
@@ -759,22 +1297,25 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
   // Contacts of one level share no drone, so solving a level's contacts at once and the levels in
   // order IS the sequential sweep over the env's contacts (non-adjacent rows of disjoint drones
   // commute) - a pile of contacts through one drone still takes one round per contact, independent
-  // pairs of one env take one.  An env's contacts are its near indices [ek0, ek1) with the contact bit.
+  // pairs of one env take one; a pair's points (same two drones) take one round each.
   int rounds = maxcnt;
   if (maxcnt > 1) {
     L.dlev[ln] = 0;
     L.clev[ln] = 0;
+    L.clev1[ln] = 0;
     wave_lds_sync();
     int lmax = ln < nenv && L.ecnt[ln] > 0 ? 1 : 0;
     if (ln < nenv && L.ecnt[ln] > 1) {
       for (int k = L.ek0[ln]; k < L.ek1[ln]; ++k) {
-        if (((L.contw[k >> 6] >> (k & 63)) & 1ull) == 0) continue;
         int pij;
         int* ints = nullptr;
         if (k < kWave) {
           pij = L.cij[k];
+        } else if (k < kDcRegRows * kWave) {
+          pij = L.cij1[k - kWave];
         } else {
-          ints = reinterpret_cast<int*>(rows + (long long)(k / kWave - 1) * kWave * kRowR + 55 * kWave) + (k & (kWave - 1));
+          ints = reinterpret_cast<int*>(rows + (long long)(k / kWave - kDcRegRows) * kWave * kRowR + kRowReal * kWave) +
+                 (k & (kWave - 1));
           pij = ints[0] | (ints[kWave] << 8);
         }
         const int i = pij & 255, j = pij >> 8;
@@ -783,6 +1324,7 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
         L.dlev[i] = lev;
         L.dlev[j] = lev;
         if (k < kWave) L.clev[k] = lev - 1;
+        else if (k < kDcRegRows * kWave) L.clev1[k - kWave] = lev - 1;
         else ints[3 * kWave] = lev - 1;
         lmax = lev > lmax ? lev : lmax;
       }
@@ -795,8 +1337,9 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
     rounds = lmax;
     wave_lds_sync();
     if (have0) w0.rank = L.clev[ln];
+    if (have1) w1.rank = L.clev1[ln];
   }
-  const R mu = c.dd_mu, resid = c.resid;
+  const R mu = c.dd_mu, resid = c.resid, pmu = c.mu;
   const int iters = c.iters;
 #ifdef GPD_CONTACT_STATS
   t2 = __builtin_readcyclecounter();
@@ -806,9 +1349,11 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
   if (true) {   // diagnostic build: narrowphase and rows, no iterations
   } else
 #endif
-  if (maxcnt <= 1 && npass <= 1) {
-    // ---- every env has at most one contact: its lane owns both drones' deltas
+  if (maxcnt <= 1 && ncpass <= 1 && !any_isl) {
+    // ---- every env has at most one contact and no island: its lane owns both drones' deltas
     R vi[6] = {R(0), R(0), R(0), R(0), R(0), R(0)}, vj[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+    DcInv<R> I0;
+    dc_inv(L, w0.i, w0.j, I0);
     bool done = !have0;
     for (int it = 0; it < iters; ++it) {
       if (__ballot(!done) == 0ull) break;
@@ -816,8 +1361,8 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
       it_used = it + 1;
 #endif
       if (!done) {
-        R res = dc_normal(w0, inv_m, vi, vj);
-        res = g_fmax(res, dc_friction(w0, mu, inv_m, vi, vj));
+        R res = dc_normal(w0, inv_m, vi, vj, I0);
+        res = g_fmax(res, dc_friction(w0, mu, inv_m, vi, vj, I0));
         done = res <= resid;
       }
     }
@@ -828,24 +1373,25 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
       L.dc[DC_DAX][w0.j] = vj[3]; L.dc[DC_DAY][w0.j] = vj[4]; L.dc[DC_DAZ][w0.j] = vj[5];
     }
   } else {
-    // ---- general case: round r solves the level-r contacts of every env; deltas through LDS
+    // ---- general case: per phase (normal rows, then friction pairs) the island drones' plane rows
+    // (one round: each drone's own rows), then round r solves the level-r contacts of every env;
+    // deltas through LDS (bullet_mb.drone_contact's order: plane normal, pair normal, plane
+    // friction, pair friction)
     if (ln < nenv) L.edone[ln] = L.ecnt[ln] == 0;
     wave_lds_sync();
     R vi[6], vj[6];
     auto visit = [&](DcRow<R>& w, bool friction) {
       if (L.edone[w.env]) return;
+      DcInv<R> I;
+      dc_inv(L, w.i, w.j, I);
 #pragma unroll
       for (int x = 0; x < 6; ++x) { vi[x] = L.dc[DC_DLX + x][w.i]; vj[x] = L.dc[DC_DLX + x][w.j]; }
-      const R rr = friction ? dc_friction(w, mu, inv_m, vi, vj) : dc_normal(w, inv_m, vi, vj);
+      const R rr = friction ? dc_friction(w, mu, inv_m, vi, vj, I) : dc_normal(w, inv_m, vi, vj, I);
 #pragma unroll
       for (int x = 0; x < 6; ++x) { L.dc[DC_DLX + x][w.i] = vi[x]; L.dc[DC_DLX + x][w.j] = vj[x]; }
-      // several rows of an env per round (one level): the max through an LDS atomic on the bit
-      // pattern (non-negative floats order as unsigned integers)
-      if (sizeof(R) == 8)
-        atomicMax(reinterpret_cast<unsigned long long*>(&L.eres[w.env]), (unsigned long long)__double_as_longlong((double)rr));
-      else
-        atomicMax(reinterpret_cast<unsigned int*>(&L.eres[w.env]), (unsigned int)__float_as_uint((float)rr));
+      eres_max(L, w.env, rr);
     };
+    const int my_env = ln / dp.D;
     for (int it = 0; it < iters; ++it) {
       if (__ballot(ln < nenv && !L.edone[ln]) == 0ull) break;
 #ifdef GPD_CONTACT_STATS
@@ -854,17 +1400,22 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
       if (ln < nenv) L.eres[ln] = R(0);
       wave_lds_sync();
       for (int ph = 0; ph < 2; ++ph) {              // normal rows, then friction pairs
+        if (any_isl) {
+          if (isl && !L.edone[my_env]) eres_max(L, my_env, island_sweep(L, ln, ph == 1, pmu, inv_m));
+          wave_lds_sync();
+        }
         for (int r = 0; r < rounds; ++r) {
           if (have0 && w0.rank == r) visit(w0, ph == 1);
-          for (int ch = 1; ch < npass; ++ch) {
+          if (have1 && w1.rank == r) visit(w1, ph == 1);
+          for (int ch = kDcRegRows; ch < ncpass; ++ch) {
             if (((L.contw[ch] >> ln) & 1ull) == 0) continue;
-            R* chunk = rows + (long long)(ch - 1) * kWave * kRowR;
+            R* chunk = rows + (long long)(ch - kDcRegRows) * kWave * kRowR;
+            if (reinterpret_cast<const int*>(chunk + kRowReal * kWave)[3 * kWave + ln] != r) continue;   // its rank
             DcRow<R> w;
             dc_row_load(chunk, ln, w);
-            if (w.rank != r) continue;
             visit(w, ph == 1);
 #pragma unroll
-            for (int q = 0; q < 3; ++q) chunk[(52 + q) * kWave + ln] = w.lam[q];
+            for (int q = 0; q < 3; ++q) chunk[(kRowLam + q) * kWave + ln] = w.lam[q];
           }
           wave_lds_sync();
         }
@@ -876,8 +1427,8 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
 #ifdef GPD_CONTACT_STATS
   {
     const unsigned long long t3 = __builtin_readcyclecounter();
-    int tot = n_near, nc = have0 ? 1 : 0;
-    for (int o = 32; o > 0; o >>= 1) { tot += __shfl_xor(tot, o); nc += __shfl_xor(nc, o); }
+    int tot = n_near;
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
     if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) {
       atomicAdd(&g_pc_hist[116], 1ull);
       atomicAdd(&g_pc_hist[117], t2 - t0);
@@ -885,8 +1436,11 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
       atomicAdd(&g_pc_hist[119], (unsigned long long)it_used);
       atomicAdd(&g_pc_hist[123], t1 - t0);
       atomicAdd(&g_pc_hist[254], t_np - t0);   // to the end of pass 0's narrowphases
-      atomicAdd(&g_pc_hist[126], (unsigned long long)nc);
+      atomicAdd(&g_pc_hist[126], (unsigned long long)ncon);
       atomicAdd(&g_pc_hist[127], (unsigned long long)tot);
+      atomicAdd(&g_pc_hist[124], any_isl ? 1ull : 0ull);                                   // island solves
+      atomicAdd(&g_pc_hist[125], (maxcnt <= 1 && ncpass <= 1 && !any_isl) ? 1ull : 0ull);  // register fast path
+      atomicAdd(&g_pc_hist[243], (unsigned long long)rounds);                               // GS rounds per phase
       const unsigned long long cyc = t3 - t0;
       atomicAdd(&g_pc_hist[128 + (63 - __clzll(cyc | 1ull))], 1ull);
       atomicAdd(&g_pc_hist[192 + it_used], 1ull);
@@ -902,10 +1456,12 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
 struct DcHook {
   int tid;
   DcPairs dp;
+  // returns whether this lane's drone joined the island (its plane rows were solved here)
   template <typename R, class PK>
-  __device__ __forceinline__ void operator()(Drone<R>& s, R* Rm, const Consts<R>& c, const DynK<R>& k, const PK& pk) const {
+  __device__ __forceinline__ bool operator()(Drone<R>& s, R* Rm, const Consts<R>& c, const DynK<R>& k, const PK& pk,
+                                             bool plane) const {
 #if GPD_DC_DIAG == 3
-    return;   // diagnostic build: no drone contact at all (the hook compiled in, its body not)
+    return false;   // diagnostic build: no drone contact at all (the hook compiled in, its body not)
 #endif
     DcLds<R>& L = dc_lds<R>();
     const DcPairs& P = dp;
@@ -914,7 +1470,7 @@ struct DcHook {
     L.dc[DC_CX][ln] = s.px + Rm[2] * zo; L.dc[DC_CY][ln] = s.py + Rm[5] * zo; L.dc[DC_CZ][ln] = s.pz + Rm[8] * zo;
     L.dc[DC_AX][ln] = Rm[2]; L.dc[DC_AY][ln] = Rm[5]; L.dc[DC_AZ][ln] = Rm[8];
     wave_lds_sync();
-    bool any = false;
+    bool any = false, isl = false;
     for (int ch = 0; ch < P.nch; ++ch) {
       const int p = ln + kWave * ch;
       bool near = false;
@@ -948,6 +1504,8 @@ struct DcHook {
       L.dc[DC_PX][ln] = s.px; L.dc[DC_PY][ln] = s.py; L.dc[DC_PZ][ln] = s.pz;
       L.dc[DC_VX][ln] = s.vx; L.dc[DC_VY][ln] = s.vy; L.dc[DC_VZ][ln] = s.vz;
       L.dc[DC_WX][ln] = s.wx; L.dc[DC_WY][ln] = s.wy; L.dc[DC_WZ][ln] = s.wz;
+      L.dc[DC_R0][ln] = Rm[0]; L.dc[DC_R1][ln] = Rm[1]; L.dc[DC_R3][ln] = Rm[3];
+      L.dc[DC_R4][ln] = Rm[4]; L.dc[DC_R6][ln] = Rm[6]; L.dc[DC_R7][ln] = Rm[7];
       const R inv_m = k.inv_m, dt = k.dt;
       const DcPairs dpc = P;
       wave_lds_sync();
@@ -959,11 +1517,12 @@ struct DcHook {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const unsigned long long tr2 = __builtin_readcyclecounter();
 #endif
-      dc_solve<R>(&c, inv_m, dt, ln, dpc);
+      dc_solve<R>(&c, inv_m, dt, ln, dpc, plane);
 #ifdef GPD_CONTACT_STATS
       const unsigned long long tr3 = __builtin_readcyclecounter();
 #endif
       pk.unpark();
+      isl = L.island[ln] != 0;
       if (L.stouch[ln]) {
         s.vx = s.vx + L.dc[DC_DLX][ln]; s.vy = s.vy + L.dc[DC_DLY][ln]; s.vz = s.vz + L.dc[DC_DLZ][ln];
         s.wx = s.wx + L.dc[DC_DAX][ln]; s.wy = s.wy + L.dc[DC_DAY][ln]; s.wz = s.wz + L.dc[DC_DAZ][ln];
@@ -983,6 +1542,7 @@ struct DcHook {
 #endif
     }
     wave_lds_sync();   // the centre columns are rewritten by the next substep
+    return isl;
   }
 };
 

