@@ -490,13 +490,6 @@ def _policy_mlp(n_in, n_out):
     return nn.Sequential(nn.Linear(n_in, 64), nn.Tanh(), nn.Linear(64, 64), nn.Tanh(), nn.Linear(64, n_out))
 
 
-def _free_port():
-    import socket
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        return sk.getsockname()[1]
-
-
 def handoff_leg(sim, global_envs, hmode, cap, gpool, G, rank, device, force=False):
     """One LearnerHandoff configuration timed over G steps (after 3 warm ones): ms per step, the
     bytes that land per step, how many steps needed the second (overflow) exchange and the
@@ -750,6 +743,12 @@ def main():
 
 
 def run(args):
+    # the JSON line is the only thing this process writes to stdout: native libraries write to fd 1
+    # directly (RCCL prints its version banner when it creates a communicator), so fd 1 points at
+    # stderr until the line is printed
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -958,6 +957,8 @@ def run(args):
             result["parity"] = {"error": str(exc)}
 
     if rank == 0:
+        sys.stdout.flush()
+        os.dup2(json_fd, 1)
         print(json.dumps(result), flush=True)
     sim.close()
     if world > 1:

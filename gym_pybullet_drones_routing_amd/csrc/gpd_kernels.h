@@ -595,9 +595,10 @@ enum { DI_RW = 0, DI_RHS = 12, DI_JDI = 24, DI_JDN = 36, DI_LAM = 40, DI_NUM = 5
 template <typename R>
 struct DcLds {
   R dc[DC_N][kWave];                  // drone columns
-  R st[DS_NUM][kWave];                // this pass's near pairs' narrowphases (normal, point, distance, face points)
-  R isl[DI_NUM][kWave];               // island drones' plane rows
-  R rim[4][7][kWave];                 // narrowphase: per near slot and rim, the best start's (x, y) and distance
+  // one area, three uses at different times: a pass's narrowphases (st: normal, point, distance,
+  // face points per near slot; rim: per near slot and rim the best start's (x, y) and whether the
+  // rim is needed), then, after the last pass, the island drones' plane rows (isl)
+  R u[DI_NUM][kWave];
   unsigned long long nearw[kDcChunks], contw[kDcConPasses];   // pairs in reach (by chunk) / contacts (by pass)
   R eres[kWave];                      // per env: this iteration's largest squared residual
   int edone[kWave];                   // per env: solve finished
@@ -611,6 +612,10 @@ struct DcLds {
   int npdone[kWave];                  // narrowphase: near slot resolved at an earlier margin level
   int ecnt[kWave], ek0[kWave], ek1[kWave];   // per env: contacts, their contact-index range [ek0, ek1)
 };
+static_assert(DS_NUM + 4 * 7 <= DI_NUM, "narrowphase staging fits the island rows' area");
+#define DC_ST(k) u[k]
+#define DC_RIM(m, e) u[DS_NUM + 7 * (m) + (e)]
+#define DC_ISL(k) u[k]
 // one LDS block per instantiation, shared by the hook (inlined) and the solve (a call)
 template <typename R>
 __device__ __forceinline__ DcLds<R>& dc_lds() {
@@ -882,7 +887,7 @@ __device__ __forceinline__ bool island_rows(DcLds<R>& L, int ln, const Consts<R>
     const R rwx = pc_dot(Rm[0], Rm[1], Rm[2], rx, ry, zc);
     const R rwy = pc_dot(Rm[3], Rm[4], Rm[5], rx, ry, zc);
     const R rwz = pc_dot(Rm[6], Rm[7], Rm[8], rx, ry, zc);
-    L.isl[DI_RW + 3 * p][ln] = rwx; L.isl[DI_RW + 3 * p + 1][ln] = rwy; L.isl[DI_RW + 3 * p + 2][ln] = rwz;
+    L.DC_ISL(DI_RW + 3 * p)[ln] = rwx; L.DC_ISL(DI_RW + 3 * p + 1)[ln] = rwy; L.DC_ISL(DI_RW + 3 * p + 2)[ln] = rwz;
     const R dist = pz + rwz;
     const bool act = dist < c.brk && g_abs(px + rwx) <= c.plane_half && g_abs(py + rwy) <= c.plane_half;
     any = any || act;
@@ -901,13 +906,13 @@ __device__ __forceinline__ bool island_rows(DcLds<R>& L, int ln, const Consts<R>
       if (j == 0) {
         const R pen = dist + c.slop;
         r = pen > R(0) ? (-rel - pen * idt) * inv : (-pen * c.erp * idt - rel) * inv;
-        L.isl[DI_JDN + p][ln] = act ? jd : R(0);
+        L.DC_ISL(DI_JDN + p)[ln] = act ? jd : R(0);
       } else {
         r = -rel * inv;
       }
-      L.isl[DI_JDI + 3 * p + j][ln] = act ? inv : R(0);
-      L.isl[DI_RHS + 3 * p + j][ln] = act ? r : R(0);
-      L.isl[DI_LAM + 3 * p + j][ln] = R(0);
+      L.DC_ISL(DI_JDI + 3 * p + j)[ln] = act ? inv : R(0);
+      L.DC_ISL(DI_RHS + 3 * p + j)[ln] = act ? r : R(0);
+      L.DC_ISL(DI_LAM + 3 * p + j)[ln] = R(0);
     }
   }
   return any;
@@ -921,34 +926,35 @@ __device__ __forceinline__ R island_sweep(DcLds<R>& L, int ln, bool friction, R 
   const R i00 = L.dc[DC_I00][ln], i01 = L.dc[DC_I01][ln], i02 = L.dc[DC_I02][ln], i11 = L.dc[DC_I11][ln],
           i12 = L.dc[DC_I12][ln], i22 = L.dc[DC_I22][ln];
   R res = R(0);
+#pragma unroll
   for (int p = 0; p < 4; ++p) {
-    const R rwx = L.isl[DI_RW + 3 * p][ln], rwy = L.isl[DI_RW + 3 * p + 1][ln], rwz = L.isl[DI_RW + 3 * p + 2][ln];
+    const R rwx = L.DC_ISL(DI_RW + 3 * p)[ln], rwy = L.DC_ISL(DI_RW + 3 * p + 1)[ln], rwz = L.DC_ISL(DI_RW + 3 * p + 2)[ln];
     if (!friction) {
-      if (!(L.isl[DI_JDN + p][ln] > R(0))) continue;   // inactive point (the oracle has no row)
+      if (!(L.DC_ISL(DI_JDN + p)[ln] > R(0))) continue;   // inactive point (the oracle has no row)
       const R ax = rwy, ay = -rwx;
       const R jv = dl2 + (ax * da0 + ay * da1);
-      R delta = L.isl[DI_RHS + 3 * p][ln] - L.isl[DI_JDI + 3 * p][ln] * jv;
-      const R lam = L.isl[DI_LAM + 3 * p][ln];
+      R delta = L.DC_ISL(DI_RHS + 3 * p)[ln] - L.DC_ISL(DI_JDI + 3 * p)[ln] * jv;
+      const R lam = L.DC_ISL(DI_LAM + 3 * p)[ln];
       const R sum = lam + delta;
       const bool neg = sum < R(0);
       delta = neg ? -lam : delta;
-      L.isl[DI_LAM + 3 * p][ln] = neg ? R(0) : sum;
+      L.DC_ISL(DI_LAM + 3 * p)[ln] = neg ? R(0) : sum;
       dl2 = dl2 + inv_m * delta;
       da0 = da0 + pc_dot(i00, i01, i02, ax, ay, R(0)) * delta;
       da1 = da1 + pc_dot(i01, i11, i12, ax, ay, R(0)) * delta;
       da2 = da2 + pc_dot(i02, i12, i22, ax, ay, R(0)) * delta;
-      const R rr = delta * L.isl[DI_JDN + p][ln];
+      const R rr = delta * L.DC_ISL(DI_JDN + p)[ln];
       res = g_fmax(res, rr * rr);
     } else {
-      const R lnrm = L.isl[DI_LAM + 3 * p][ln];
+      const R lnrm = L.DC_ISL(DI_LAM + 3 * p)[ln];
       if (!(lnrm > R(0))) continue;
       const R lim = mu * lnrm;
-      const R l1 = L.isl[DI_LAM + 3 * p + 1][ln], l2 = L.isl[DI_LAM + 3 * p + 2][ln];
+      const R l1 = L.DC_ISL(DI_LAM + 3 * p + 1)[ln], l2 = L.DC_ISL(DI_LAM + 3 * p + 2)[ln];
       // (0,-1,0): a = (rz, 0, -rx); (1,0,0): a = (0, rz, -ry)
       const R j1 = (rwz * da0 - rwx * da2) - dl1;
       const R j2 = (rwz * da1 - rwy * da2) + dl0;
-      R s1 = l1 + (L.isl[DI_RHS + 3 * p + 1][ln] - L.isl[DI_JDI + 3 * p + 1][ln] * j1);
-      R s2 = l2 + (L.isl[DI_RHS + 3 * p + 2][ln] - L.isl[DI_JDI + 3 * p + 2][ln] * j2);
+      R s1 = l1 + (L.DC_ISL(DI_RHS + 3 * p + 1)[ln] - L.DC_ISL(DI_JDI + 3 * p + 1)[ln] * j1);
+      R s2 = l2 + (L.DC_ISL(DI_RHS + 3 * p + 2)[ln] - L.DC_ISL(DI_JDI + 3 * p + 2)[ln] * j2);
       const R m2 = s1 * s1 + s2 * s2;
       if (m2 > lim * lim) {
         const R f = lim * g_rsqrt1(m2);
@@ -956,8 +962,8 @@ __device__ __forceinline__ R island_sweep(DcLds<R>& L, int ln, bool friction, R 
         s2 = s2 * f;
       }
       const R d1 = s1 - l1, d2 = s2 - l2;
-      L.isl[DI_LAM + 3 * p + 1][ln] = s1;
-      L.isl[DI_LAM + 3 * p + 2][ln] = s2;
+      L.DC_ISL(DI_LAM + 3 * p + 1)[ln] = s1;
+      L.DC_ISL(DI_LAM + 3 * p + 2)[ln] = s2;
       dl1 = dl1 - inv_m * d1;
       dl0 = dl0 + inv_m * d2;
       da0 = da0 + pc_dot(i00, i01, i02, rwz, R(0), -rwx) * d1;
@@ -1045,8 +1051,8 @@ __device__ __noinline__ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthi
       for (int e = 0; e < 3; ++e) { x[e] = __shfl(x[e], src); y[e] = __shfl(y[e], src); }
       if (t < ntask && k == 0) {
 #pragma unroll
-        for (int e = 0; e < 3; ++e) { L.rim[rim][e][slot] = x[e]; L.rim[rim][3 + e][slot] = y[e]; }
-        L.rim[rim][6][slot] = need ? R(0) : R(INFINITY);   // a rim the pair does not need
+        for (int e = 0; e < 3; ++e) { L.DC_RIM(rim, e)[slot] = x[e]; L.DC_RIM(rim, 3 + e)[slot] = y[e]; }
+        L.DC_RIM(rim, 6)[slot] = need ? R(0) : R(INFINITY);   // a rim the pair does not need
       }
     }
     wave_lds_sync();
@@ -1063,9 +1069,9 @@ __device__ __noinline__ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthi
       ds[0] = cd[0]; ds[1] = cd[1]; ds[2] = cd[2];
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-        const R dx = L.rim[m][0][ln] - L.rim[m][3][ln], dy = L.rim[m][1][ln] - L.rim[m][4][ln],
-                dz = L.rim[m][2][ln] - L.rim[m][5][ln];
-        ds[3 + m] = L.rim[m][6][ln] == R(0) ? g_sqrt(pc_dot(dx, dy, dz, dx, dy, dz)) : R(INFINITY);
+        const R dx = L.DC_RIM(m, 0)[ln] - L.DC_RIM(m, 3)[ln], dy = L.DC_RIM(m, 1)[ln] - L.DC_RIM(m, 4)[ln],
+                dz = L.DC_RIM(m, 2)[ln] - L.DC_RIM(m, 5)[ln];
+        ds[3 + m] = L.DC_RIM(m, 6)[ln] == R(0) ? g_sqrt(pc_dot(dx, dy, dz, dx, dy, dz)) : R(INFINITY);
       }
       R dmin = ds[0];
 #pragma unroll
@@ -1083,8 +1089,8 @@ __device__ __noinline__ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthi
           bd = ds[m];
 #pragma unroll
           for (int e = 0; e < 3; ++e) {
-            bx[e] = m < 3 ? cx[m < 3 ? m : 0][e] : L.rim[m >= 3 ? m - 3 : 0][e][ln];
-            by[e] = m < 3 ? cy[m < 3 ? m : 0][e] : L.rim[m >= 3 ? m - 3 : 0][3 + e][ln];
+            bx[e] = m < 3 ? cx[m < 3 ? m : 0][e] : L.DC_RIM(m >= 3 ? m - 3 : 0, e)[ln];
+            by[e] = m < 3 ? cy[m < 3 ? m : 0][e] : L.DC_RIM(m >= 3 ? m - 3 : 0, 3 + e)[ln];
           }
         }
       }
@@ -1142,13 +1148,13 @@ __device__ __noinline__ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthi
   int fmask = 0;
 #pragma unroll
   for (int m = 0; m < 4; ++m) fmask |= (face && fd[m] < brk) ? (1 << m) : 0;
-  L.st[DS_N][ln] = n[0]; L.st[DS_N + 1][ln] = n[1]; L.st[DS_N + 2][ln] = n[2];
-  L.st[DS_PB][ln] = pb[0]; L.st[DS_PB + 1][ln] = pb[1]; L.st[DS_PB + 2][ln] = pb[2];
-  L.st[DS_D][ln] = dist;
+  L.DC_ST(DS_N)[ln] = n[0]; L.DC_ST(DS_N + 1)[ln] = n[1]; L.DC_ST(DS_N + 2)[ln] = n[2];
+  L.DC_ST(DS_PB)[ln] = pb[0]; L.DC_ST(DS_PB + 1)[ln] = pb[1]; L.DC_ST(DS_PB + 2)[ln] = pb[2];
+  L.DC_ST(DS_D)[ln] = dist;
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
-    L.st[DS_FP + 3 * m][ln] = fp[m][0]; L.st[DS_FP + 3 * m + 1][ln] = fp[m][1]; L.st[DS_FP + 3 * m + 2][ln] = fp[m][2];
-    L.st[DS_FD + m][ln] = fd[m];
+    L.DC_ST(DS_FP + 3 * m)[ln] = fp[m][0]; L.DC_ST(DS_FP + 3 * m + 1)[ln] = fp[m][1]; L.DC_ST(DS_FP + 3 * m + 2)[ln] = fp[m][2];
+    L.DC_ST(DS_FD + m)[ln] = fd[m];
   }
   L.nsp[ln] = fmask;   // reused: the pair's face-point mask (its pair index is no longer needed)
   return con ? 1 + __popc(fmask) : 0;
@@ -1233,15 +1239,15 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
         const int sl = qm & 255, m = qm >> 8;
         const int pj = L.nsij[sl];
         const int i = pj & 255, j = pj >> 8;
-        const R n[3] = {L.st[DS_N][sl], L.st[DS_N + 1][sl], L.st[DS_N + 2][sl]};
+        const R n[3] = {L.DC_ST(DS_N)[sl], L.DC_ST(DS_N + 1)[sl], L.DC_ST(DS_N + 2)[sl]};
         R pb[3], dist;
         if (m == 0) {
-          pb[0] = L.st[DS_PB][sl]; pb[1] = L.st[DS_PB + 1][sl]; pb[2] = L.st[DS_PB + 2][sl];
-          dist = L.st[DS_D][sl];
+          pb[0] = L.DC_ST(DS_PB)[sl]; pb[1] = L.DC_ST(DS_PB + 1)[sl]; pb[2] = L.DC_ST(DS_PB + 2)[sl];
+          dist = L.DC_ST(DS_D)[sl];
         } else {
-          pb[0] = L.st[DS_FP + 3 * (m - 1)][sl]; pb[1] = L.st[DS_FP + 3 * (m - 1) + 1][sl];
-          pb[2] = L.st[DS_FP + 3 * (m - 1) + 2][sl];
-          dist = L.st[DS_FD + (m - 1)][sl];
+          pb[0] = L.DC_ST(DS_FP + 3 * (m - 1))[sl]; pb[1] = L.DC_ST(DS_FP + 3 * (m - 1) + 1)[sl];
+          pb[2] = L.DC_ST(DS_FP + 3 * (m - 1) + 2)[sl];
+          dist = L.DC_ST(DS_FD + (m - 1))[sl];
         }
         DcRow<R> w;
         dc_row_setup(L, i, j, n, pb, dist, c, inv_m, idt, w);
@@ -1441,6 +1447,9 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
       atomicAdd(&g_pc_hist[124], any_isl ? 1ull : 0ull);                                   // island solves
       atomicAdd(&g_pc_hist[125], (maxcnt <= 1 && ncpass <= 1 && !any_isl) ? 1ull : 0ull);  // register fast path
       atomicAdd(&g_pc_hist[243], (unsigned long long)rounds);                               // GS rounds per phase
+      atomicMax(&g_pc_hist[255], (unsigned long long)ncon);                                 // most contacts of a solve
+      atomicAdd(&g_pc_hist[kPcNp + 5], ncon > kDcRegRows * kWave ? 1ull : 0ull);           // solves using the row store
+      atomicAdd(&g_pc_hist[kPcNp + 6], (unsigned long long)ncpass);
       const unsigned long long cyc = t3 - t0;
       atomicAdd(&g_pc_hist[128 + (63 - __clzll(cyc | 1ull))], 1ull);
       atomicAdd(&g_pc_hist[192 + it_used], 1ull);

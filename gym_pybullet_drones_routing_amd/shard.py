@@ -97,17 +97,18 @@ class LearnerHandoff:
        never clears the action buffer on reset (``BaseRLAviary`` has no ``reset`` override, SURVEY
        a13), so a finished env's terminal observation and its auto-reset observation share the 15
        history columns; the receiving ranks rebuild the terminal row from the gathered obs (48 B per
-       drone instead of 288 B with RPM actions).  Every rank compacts the state columns of its envs
-       that finished this step on the device (a prefix sum over its done flags, ``index_copy_``)
-       into a fixed block of ``terminal_capacity`` rows, and that block goes the prefix's way
-       (``gather`` / ``all_gather_into_tensor``); the receivers place row j of rank r at rank r's
-       j-th finished env, from the gathered flags on the device.  With the default capacity (the
-       shard's env count) every size is fixed and nothing waits for the device: no ``.item()`` /
-       boolean indexing (round 3 sized the exchange from the done counts, two host syncs per step,
-       each longer than the ~5 us step).  A smaller ``terminal_capacity`` sends fewer rows first and
-       never drops one: an all-reduce of the largest finished count follows (read on the host - one
-       synchronisation per step, the price of the smaller block), and when some rank finished more
-       envs than the capacity a second exchange of exactly the missing rows runs in the same step.
+       drone instead of 288 B with RPM actions).  With the default capacity (the shard's env count)
+       nothing is compacted: every env's state columns ride in the prefix's own record (ONE
+       collective per step, E*D*48 extra bytes per rank) and the receivers keep the finished envs'
+       rows; every size is fixed and nothing waits for the device (round 3 sized the exchange from
+       the done counts, two host syncs per step, each longer than the ~5 us step).  A smaller
+       ``terminal_capacity`` compacts the state columns of the envs that finished this step on the
+       device (a prefix sum over the done flags, ``index_copy_``) into a block of that many rows,
+       exchanged after the prefix; the receivers place row j of rank r at rank r's j-th finished
+       env.  It never drops a row: an all-reduce of the largest finished count follows (read on the
+       host - one synchronisation per step, the price of the smaller block), and when some rank
+       finished more envs than the capacity a second exchange of exactly the missing rows runs in
+       the same step.
     ``step`` returns (obs [E, D, W], reward [E], terminated [E], truncated [E], terminal_obs or
     None) - freshly allocated tensors, so a caller may keep them across steps - on the learner
     rank ("gather") or every rank ("all_gather"), None elsewhere.  Rows of ``terminal_obs`` whose
@@ -140,7 +141,6 @@ class LearnerHandoff:
         self.device = dev
         self._gloo = dist.is_initialized() and dist.get_backend() == "gloo"
         self._coll = dist.is_initialized() and (self.world > 1 or force_collectives)
-        self.pack_all = torch.empty((self.world * self.nbytes,), dtype=torch.uint8, device=dev)
         D, A = sim.drones_per_env, sim.act_width
         self.local_actions = torch.empty((self.count, D, A), dtype=torch.float32, device=dev)
         C = self.count if terminal_capacity is None else int(terminal_capacity)
@@ -151,10 +151,18 @@ class LearnerHandoff:
         if W < self.STATE_COLS:
             raise ValueError(f"observation rows of width {W} have no {self.STATE_COLS} state columns")
         S = self.STATE_COLS
-        # the compacted block of state columns (+ one scratch row that the envs still running write
-        # to) and the gathered blocks of every rank
-        self._tblock = torch.zeros((self.count + 1, D * S), dtype=torch.float32, device=dev)
-        self._trows = torch.zeros((self.world * C, D * S), dtype=torch.float32, device=dev)
+        # the default capacity (the whole shard) needs no compaction: every env's 12 state columns
+        # ride in the same exchange as the pack prefix (one collective per step); a smaller capacity
+        # compacts the finished envs' columns into a block (+ one scratch row that the envs still
+        # running write to) exchanged on its own
+        self._fused = terminal_obs and C == self.count
+        self.sbytes = self.count * D * S * 4 if self._fused else 0
+        self.rec = self.nbytes + self.sbytes          # bytes of one rank's record in the exchange
+        self._send = torch.empty((self.rec,), dtype=torch.uint8, device=dev) if self._fused else None
+        self.pack_all = torch.empty((self.world * self.rec,), dtype=torch.uint8, device=dev)
+        if not self._fused:
+            self._tblock = torch.zeros((self.count + 1, D * S), dtype=torch.float32, device=dev)
+            self._trows = torch.zeros((self.world * C, D * S), dtype=torch.float32, device=dev)
         self.terminal_bytes = 0     # terminal-row bytes received by the learner so far (all steps)
         self.second_exchanges = 0   # steps that needed the overflow exchange (capacity < shard)
         self.finished = 0           # finished envs seen (receiving ranks; counted only with a capacity < shard)
@@ -200,15 +208,25 @@ class LearnerHandoff:
         else:
             dist.scatter(self.local_actions, [p.contiguous() for p in parts] if parts else None, src=self.learner)
 
-    def _gather_prefix(self):
-        self._exchange(self.sim.out_pack[:self.nbytes], self.pack_all)
+    def _gather_prefix(self, with_state=False):
+        """The pack prefix of every rank (and with ``with_state`` its envs' terminal state columns,
+        in the same record) -> ``pack_all`` on the receiving ranks."""
+        if not with_state:
+            self._exchange(self.sim.out_pack[:self.nbytes], self.pack_all[:self.world * self.nbytes])
+            return
+        E, D, W, S = self.count, self.sim.drones_per_env, self.sim.obs_width, self.STATE_COLS
+        self._send[:self.nbytes].copy_(self.sim.out_pack[:self.nbytes])
+        self._send[self.nbytes:].view(torch.float32).view(E, D, S).copy_(
+            self._local("terminal_obs", torch.float32, (E, D, W))[:, :, :S])
+        self._exchange(self._send, self.pack_all)
 
-    def _field(self, name, dtype, shape):
+    def _field(self, name, dtype, shape, rec=None):
         """Field `name` of every rank's gathered pack, as ONE fresh tensor [G*E, ...]."""
         G, E = self.world, self.count
-        off, n = self.layout[name]
+        rec = self.nbytes if rec is None else rec
+        off, n = (self.nbytes, self.sbytes) if name == "state" else self.layout[name]
         out = torch.empty((G, n), dtype=torch.uint8, device=self.device)
-        out.copy_(self.pack_all.view(G, self.nbytes)[:, off:off + n])
+        out.copy_(self.pack_all[:G * rec].view(G, rec)[:, off:off + n])
         return out.view(dtype).reshape((G * E,) + shape)
 
     def _local(self, name, dtype, shape):
@@ -249,9 +267,9 @@ class LearnerHandoff:
 
     def _terminal_rows(self, obs, te, tr):
         """Terminal rows of the envs that finished this step ([G*E, D, W], zero elsewhere) on the
-        ranks that receive; None elsewhere.  obs / te / tr: the gathered batch (receiving ranks).
-        With the default capacity, fixed sizes and device-side indices only: nothing here waits for
-        the device."""
+        ranks that receive; None elsewhere, for a ``terminal_capacity`` below the shard size (the
+        default capacity rides in the prefix's record, ``step``).  obs / te / tr: the gathered
+        batch (receiving ranks)."""
         G, E, D, W = self.world, self.count, self.sim.drones_per_env, self.sim.obs_width
         C, S = self.capacity, self.STATE_COLS
         ldone = (self._local("terminated", torch.uint8, (E,)) | self._local("truncated", torch.uint8, (E,))).bool()
@@ -261,15 +279,13 @@ class LearnerHandoff:
         self._tblock.index_copy_(0, torch.where(ldone, j, torch.full_like(j, E)), lrows)
         self._exchange(self._tblock[:C], self._trows)
         self.terminal_bytes += G * C * D * S * 4
-        need = C
-        if C < E:
-            # a smaller first block: rows past it follow in a second exchange of exactly their count
-            need = self._max_finished(ldone)
-            if need > C:
-                extra = torch.empty((G * (need - C), D * S), dtype=torch.float32, device=self.device)
-                self._exchange(self._tblock[C:need], extra)
-                self.terminal_bytes += G * (need - C) * D * S * 4
-                self.second_exchanges += 1
+        # rows past the block follow in a second exchange of exactly their count
+        need = self._max_finished(ldone)
+        if need > C:
+            extra = torch.empty((G * (need - C), D * S), dtype=torch.float32, device=self.device)
+            self._exchange(self._tblock[C:need], extra)
+            self.terminal_bytes += G * (need - C) * D * S * 4
+            self.second_exchanges += 1
         if not self.receives:
             return None
         done_all = (te | tr).bool().reshape(G, E)
@@ -284,13 +300,13 @@ class LearnerHandoff:
         out = torch.where(done_all.reshape(-1, 1, 1), full, torch.zeros((), dtype=full.dtype, device=self.device))
         return out
 
-    def _views(self):
+    def _views(self, rec=None):
         """The learner's global batch, reassembled from the gathered packs (rank order)."""
         D, W = self.sim.drones_per_env, self.sim.obs_width
-        obs = self._field("obs", torch.float32, (D, W))
-        rew = self._field("reward", torch.float32, ())
-        te = self._field("terminated", torch.uint8, ())
-        tr = self._field("truncated", torch.uint8, ())
+        obs = self._field("obs", torch.float32, (D, W), rec)
+        rew = self._field("reward", torch.float32, (), rec)
+        te = self._field("terminated", torch.uint8, (), rec)
+        tr = self._field("truncated", torch.uint8, (), rec)
         return obs, rew, te, tr
 
     def reset(self):
@@ -304,8 +320,21 @@ class LearnerHandoff:
         """One env.step of every env of every rank driven by the learner's ``global_actions``."""
         self._scatter_actions(global_actions)
         self.sim.step(self.local_actions, terminal_obs=self.terminal_obs)
-        self._gather_prefix()
         self.steps += 1
+        if self._fused:
+            # one exchange: pack prefix + every env's terminal state columns
+            self._gather_prefix(with_state=True)
+            G, D, S = self.world, self.sim.drones_per_env, self.STATE_COLS
+            self.terminal_bytes += G * self.sbytes
+            if not self.receives:
+                return None
+            obs, rew, te, tr = self._views(self.rec)
+            state = self._field("state", torch.float32, (D, S), self.rec)
+            done = (te | tr).bool().reshape(-1, 1, 1)
+            full = torch.cat([state, obs[:, :, S:]], 2)  # the history columns: the reset obs's (shared)
+            tobs = torch.where(done, full, torch.zeros((), dtype=full.dtype, device=self.device))
+            return obs, rew, te, tr, tobs
+        self._gather_prefix()
         if self.receives:
             obs, rew, te, tr = self._views()
         else:

@@ -113,6 +113,8 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
             print(f"   narrowphase levels: {[int(x) for x in h[249:253]]}, least-overlap fallback {h[253]}", flush=True)
             npb = 256 + 4 * 4096
             if h[npb]:
+                print(f"   contacts: most in one solve {h[255]}, solves past the register rows {h[npb + 5]}, "
+                      f"contact passes per solve {h[npb + 6] / h[116]:.2f}", flush=True)
                 print(f"   narrowphase passes {h[npb]}: near pairs {h[npb + 3] / h[npb]:.2f}, rim tasks "
                       f"{h[npb + 1] / h[npb]:.0f}, selection {h[npb + 2] / h[npb]:.0f}, fallback + face points "
                       f"{h[npb + 4] / h[npb]:.0f} cycles per pass", flush=True)
