@@ -889,10 +889,12 @@ def run(args):
             result["handoff"] = {
                 "mode": f"learner hand-off per step ({coll}{', one rank, collectives forced' if one_rank else ''}): "
                         "scatter of actions from rank 0, eager shard step, gather / all_gather_into_tensor of the "
-                        "output-pack prefixes, then the finished envs' terminal rows (12 state columns per drone; the "
-                        "history columns are the auto-reset obs's): a block of terminal_capacity rows per rank, and "
-                        "with a capacity below the shard an all-reduce of the largest finished count (one host sync) "
-                        "and, when it overflows, a second exchange of exactly the missing rows",
+                        "output-pack prefixes with the terminal rows' 12 state columns per drone (the history columns "
+                        "are the auto-reset obs's): capshard = every env's columns in the prefix's own record (one "
+                        "collective, no host sync); a smaller terminal_capacity = the finished envs' columns "
+                        "compacted into a block of that many rows per rank, exchanged after the prefix, an all-reduce "
+                        "of the largest finished count (one host sync) and, when it overflows, a second exchange of "
+                        "exactly the missing rows",
                 "step_only_ms": 1000.0 * eager_wall / args.steps, "legs": legs}
             if one_rank:
                 torch.distributed.destroy_process_group()

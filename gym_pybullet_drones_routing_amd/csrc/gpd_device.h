@@ -907,12 +907,16 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
 #ifndef GPD_CONTACT_PARK
 #define GPD_CONTACT_PARK 1   // 0: diagnostic builds (A/B of the parking)
 #endif
+// kStage: the drone <-> drone solve stages its sweeps' operands in LDS (gpd_kernels.h DcStage) -
+// the parking callers are the compiled-in PYB flag-set kernels, whose LDS has the room
 struct NoPark {
+  static constexpr bool kStage = false;
   __device__ void park() const {}
   __device__ void unpark() const {}
 };
 template <class A, class B>
 struct ParkFns {
+  static constexpr bool kStage = true;
   A a;
   B b;
   __device__ void park() const { a(); }

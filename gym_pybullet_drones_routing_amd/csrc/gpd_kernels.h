@@ -612,6 +612,26 @@ struct DcLds {
   int npdone[kWave];                  // narrowphase: near slot resolved at an earlier margin level
   int ecnt[kWave], ek0[kWave], ek1[kWave];   // per env: contacts, their contact-index range [ek0, ek1)
 };
+// The Gauss-Seidel sweeps' staging (the compiled-in PYB flag-set kernels, STAGE = true; the
+// run-time-flag kernels, which serve the long observation tiles, recompute instead): operands that
+// do not change over a solve's iterations, formed once at the setup - the same operations on the
+// same operands as the recomputation, so the same bits.
+//   ig: an island drone's plane points: the inverse-inertia images of the angular Jacobians, per
+//       point p: normal G (3 p ..), friction along (0,-1,0) H, along (1,0,0) K;
+//   pj: a first register row's (contacts 0..63) angular Jacobians and images per direction q (n,
+//       t1, t2): pj[12 q + x][contact], x = A 0..2 (r_A x d), B 3..5 (r_B x d), gA 6..8, gB 9..11.
+enum { DG_G = 0, DG_H = 12, DG_K = 24, DG_NUM = 36 };
+constexpr int kPj = 36;
+template <typename R>
+struct DcStage {
+  R ig[DG_NUM][kWave];
+  R pj[kPj][kWave];
+};
+template <typename R>
+__device__ __forceinline__ DcStage<R>& dc_stage() {
+  __shared__ DcStage<R> x;
+  return x;
+}
 static_assert(DS_NUM + 4 * 7 <= DI_NUM, "narrowphase staging fits the island rows' area");
 #define DC_ST(k) u[k]
 #define DC_RIM(m, e) u[DS_NUM + 7 * (m) + (e)]
@@ -726,9 +746,9 @@ __device__ __forceinline__ void dc_symv(const R m[6], const R v[3], R o[3]) {
   o[1] = pc_dot(m[1], m[3], m[4], v[0], v[1], v[2]);
   o[2] = pc_dot(m[2], m[4], m[5], v[0], v[1], v[2]);
 }
-template <typename R>
+template <bool STAGE, typename R>
 __device__ __forceinline__ void dc_row_setup(const DcLds<R>& L, int i, int j, const R n[3], const R pb[3], R dist,
-                                             const Consts<R>& c, R inv_m, R idt, DcRow<R>& w) {
+                                             const Consts<R>& c, R inv_m, R idt, DcRow<R>& w, int slot) {
   const R pa[3] = {pb[0] + n[0] * dist, pb[1] + n[1] * dist, pb[2] + n[2] * dist};
   w.ra[0] = pa[0] - L.dc[DC_PX][i]; w.ra[1] = pa[1] - L.dc[DC_PY][i]; w.ra[2] = pa[2] - L.dc[DC_PZ][i];
   w.rb[0] = pb[0] - L.dc[DC_PX][j]; w.rb[1] = pb[1] - L.dc[DC_PY][j]; w.rb[2] = pb[2] - L.dc[DC_PZ][j];
@@ -748,6 +768,14 @@ __device__ __forceinline__ void dc_row_setup(const DcLds<R>& L, int i, int j, co
     dc_cross(w.rb, d, B);
     dc_symv(I.a, A, gA);
     dc_symv(I.b, B, gB);
+    if (STAGE && slot >= 0) {   // a first register row: the sweeps read these instead of recomputing them
+      DcStage<R>& G = dc_stage<R>();
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        G.pj[12 * q + e][slot] = A[e]; G.pj[12 * q + 3 + e][slot] = B[e];
+        G.pj[12 * q + 6 + e][slot] = gA[e]; G.pj[12 * q + 9 + e][slot] = gB[e];
+      }
+    }
     const R jd = (inv_m + inv_m + pc_dot(A[0], A[1], A[2], gA[0], gA[1], gA[2])) + pc_dot(B[0], B[1], B[2], gB[0], gB[1], gB[2]);
     const R rel = (pc_dot(d[0], d[1], d[2], dvx, dvy, dvz) + pc_dot(A[0], A[1], A[2], wa[0], wa[1], wa[2])) -
                   pc_dot(B[0], B[1], B[2], wb[0], wb[1], wb[2]);
@@ -766,24 +794,43 @@ __device__ __forceinline__ void dc_row_setup(const DcLds<R>& L, int i, int j, co
   w.i = i;
   w.j = j;
 }
+// a row's angular Jacobians A = r_A x d_q, B = r_B x d_q and their images I_A^-1 A, I_B^-1 B: recomputed
+// from the arms and the drones' inverse inertias (rows in the row store), or read from the setup's
+// staging (register rows, L.pj) - the same operations on the same operands, so the same bits
+template <typename R>
+struct DcJacRow {
+  const DcRow<R>& w;
+  const DcInv<R>& I;
+  __device__ __forceinline__ void operator()(int q, R A[3], R B[3], R gA[3], R gB[3]) const {
+    dc_cross(w.ra, w.d[q], A);
+    dc_cross(w.rb, w.d[q], B);
+    dc_symv(I.a, A, gA);
+    dc_symv(I.b, B, gB);
+  }
+};
+template <typename R>
+struct DcJacLds {
+  const DcStage<R>& G;
+  int slot;
+  __device__ __forceinline__ void operator()(int q, R A[3], R B[3], R gA[3], R gB[3]) const {
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      A[e] = G.pj[12 * q + e][slot]; B[e] = G.pj[12 * q + 3 + e][slot];
+      gA[e] = G.pj[12 * q + 6 + e][slot]; gB[e] = G.pj[12 * q + 9 + e][slot];
+    }
+  }
+};
 // the rows' Jacobian products and impulse application (vi / vj: the two drones' deltas, linear
 // then angular)
 template <typename R>
-__device__ __forceinline__ R dc_jv(const DcRow<R>& w, int q, const R vi[6], const R vj[6]) {
-  R A[3], B[3];
-  dc_cross(w.ra, w.d[q], A);
-  dc_cross(w.rb, w.d[q], B);
+__device__ __forceinline__ R dc_jv(const DcRow<R>& w, int q, const R A[3], const R B[3], const R vi[6], const R vj[6]) {
   return (pc_dot(w.d[q][0], w.d[q][1], w.d[q][2], vi[0] - vj[0], vi[1] - vj[1], vi[2] - vj[2]) +
           pc_dot(A[0], A[1], A[2], vi[3], vi[4], vi[5])) -
          pc_dot(B[0], B[1], B[2], vj[3], vj[4], vj[5]);
 }
 template <typename R>
-__device__ __forceinline__ void dc_apply(const DcRow<R>& w, int q, R delta, R inv_m, R vi[6], R vj[6], const DcInv<R>& I) {
-  R A[3], B[3], gA[3], gB[3];
-  dc_cross(w.ra, w.d[q], A);
-  dc_cross(w.rb, w.d[q], B);
-  dc_symv(I.a, A, gA);
-  dc_symv(I.b, B, gB);
+__device__ __forceinline__ void dc_apply(const DcRow<R>& w, int q, R delta, R inv_m, const R gA[3], const R gB[3], R vi[6],
+                                         R vj[6]) {
   const R dm = inv_m * delta;
   vi[0] = vi[0] + w.d[q][0] * dm; vi[1] = vi[1] + w.d[q][1] * dm; vi[2] = vi[2] + w.d[q][2] * dm;
   vi[3] = vi[3] + gA[0] * delta; vi[4] = vi[4] + gA[1] * delta; vi[5] = vi[5] + gA[2] * delta;
@@ -791,24 +838,29 @@ __device__ __forceinline__ void dc_apply(const DcRow<R>& w, int q, R delta, R in
   vj[3] = vj[3] - gB[0] * delta; vj[4] = vj[4] - gB[1] * delta; vj[5] = vj[5] - gB[2] * delta;
 }
 // one normal row (bullet_mb.drone_contact's normal loop); returns the row's squared residual
-template <typename R>
-__device__ __forceinline__ R dc_normal(DcRow<R>& w, R inv_m, R vi[6], R vj[6], const DcInv<R>& I) {
-  R delta = w.rhs[0] - w.jdi[0] * dc_jv(w, 0, vi, vj);
+template <typename R, typename J>
+__device__ __forceinline__ R dc_normal(DcRow<R>& w, R inv_m, R vi[6], R vj[6], const J& jac) {
+  R A[3], B[3], gA[3], gB[3];
+  jac(0, A, B, gA, gB);
+  R delta = w.rhs[0] - w.jdi[0] * dc_jv(w, 0, A, B, vi, vj);
   const R sum = w.lam[0] + delta;
   const bool neg = sum < R(0);
   delta = neg ? -w.lam[0] : delta;
   w.lam[0] = neg ? R(0) : sum;
-  dc_apply(w, 0, delta, inv_m, vi, vj, I);
+  dc_apply(w, 0, delta, inv_m, gA, gB, vi, vj);
   const R rr = delta * w.jdn;
   return rr * rr;
 }
 // one friction pair on the cone (only while the normal impulse is positive); squared residual
-template <typename R>
-__device__ __forceinline__ R dc_friction(DcRow<R>& w, R mu, R inv_m, R vi[6], R vj[6], const DcInv<R>& I) {
+template <typename R, typename J>
+__device__ __forceinline__ R dc_friction(DcRow<R>& w, R mu, R inv_m, R vi[6], R vj[6], const J& jac) {
   if (!(w.lam[0] > R(0))) return R(0);
+  R A1[3], B1[3], gA1[3], gB1[3], A2[3], B2[3], gA2[3], gB2[3];
+  jac(1, A1, B1, gA1, gB1);
+  jac(2, A2, B2, gA2, gB2);
   const R lim = mu * w.lam[0];
-  R s1 = w.lam[1] + (w.rhs[1] - w.jdi[1] * dc_jv(w, 1, vi, vj));
-  R s2 = w.lam[2] + (w.rhs[2] - w.jdi[2] * dc_jv(w, 2, vi, vj));
+  R s1 = w.lam[1] + (w.rhs[1] - w.jdi[1] * dc_jv(w, 1, A1, B1, vi, vj));
+  R s2 = w.lam[2] + (w.rhs[2] - w.jdi[2] * dc_jv(w, 2, A2, B2, vi, vj));
   const R m2 = s1 * s1 + s2 * s2;
   if (m2 > lim * lim) {
     const R f = lim * g_rsqrt1(m2);   // one Newton step: ~1e-14 relative on the projected impulse
@@ -818,8 +870,8 @@ __device__ __forceinline__ R dc_friction(DcRow<R>& w, R mu, R inv_m, R vi[6], R 
   const R e1 = s1 - w.lam[1], e2 = s2 - w.lam[2];
   w.lam[1] = s1;
   w.lam[2] = s2;
-  dc_apply(w, 1, e1, inv_m, vi, vj, I);
-  dc_apply(w, 2, e2, inv_m, vi, vj, I);
+  dc_apply(w, 1, e1, inv_m, gA1, gB1, vi, vj);
+  dc_apply(w, 2, e2, inv_m, gA2, gB2, vi, vj);
   const R rr = e1 + e2;
   return rr * rr;
 }
@@ -869,7 +921,7 @@ __device__ __forceinline__ int wave_excl_scan(int x, int ln, int& total) {
 }
 // an island drone's plane rows (bullet_mb._plane_rows_world; plane_contact_regs' world form): lane ln's
 // columns of L.isl; returns whether any of its four points is active
-template <typename R>
+template <bool STAGE, typename R>
 __device__ __forceinline__ bool island_rows(DcLds<R>& L, int ln, const Consts<R>& c, R inv_m, R idt) {
   const R Rm[9] = {L.dc[DC_R0][ln], L.dc[DC_R1][ln], L.dc[DC_AX][ln], L.dc[DC_R3][ln], L.dc[DC_R4][ln],
                    L.dc[DC_AY][ln], L.dc[DC_R6][ln], L.dc[DC_R7][ln], L.dc[DC_AZ][ln]};
@@ -898,6 +950,11 @@ __device__ __forceinline__ bool island_rows(DcLds<R>& L, int ln, const Consts<R>
       const R az = j == 0 ? R(0) : (j == 1 ? -rwx : -rwy);
       const R gx = pc_dot(i00, i01, i02, ax, ay, az), gy = pc_dot(i01, i11, i12, ax, ay, az),
               gz = pc_dot(i02, i12, i22, ax, ay, az);
+      if (STAGE) {
+        DcStage<R>& G = dc_stage<R>();
+        const int gk = (j == 0 ? DG_G : (j == 1 ? DG_H : DG_K)) + 3 * p;
+        G.ig[gk][ln] = gx; G.ig[gk + 1][ln] = gy; G.ig[gk + 2][ln] = gz;
+      }
       const R jd = inv_m + pc_dot(ax, ay, az, gx, gy, gz);
       const R inv = g_rcp(jd);
       const R vl = j == 0 ? vz : (j == 1 ? -vy : vx);
@@ -918,62 +975,93 @@ __device__ __forceinline__ bool island_rows(DcLds<R>& L, int ln, const Consts<R>
   return any;
 }
 // one sweep of an island drone's plane rows (normal rows or friction pairs) on its LDS deltas;
-// returns the largest squared residual
-template <typename R>
+// returns the largest squared residual.  Branch-free: every operand is loaded before the chain
+// starts, and a point the oracle skips (inactive: no row; a friction pair whose normal impulse is
+// not positive) takes a zero step - the same values bit for bit (x + 0 * y == x for finite y).
+template <bool STAGE, typename R>
 __device__ __forceinline__ R island_sweep(DcLds<R>& L, int ln, bool friction, R mu, R inv_m) {
+  const DcStage<R>& G = dc_stage<R>();
   R dl0 = L.dc[DC_DLX][ln], dl1 = L.dc[DC_DLY][ln], dl2 = L.dc[DC_DLZ][ln];
   R da0 = L.dc[DC_DAX][ln], da1 = L.dc[DC_DAY][ln], da2 = L.dc[DC_DAZ][ln];
   const R i00 = L.dc[DC_I00][ln], i01 = L.dc[DC_I01][ln], i02 = L.dc[DC_I02][ln], i11 = L.dc[DC_I11][ln],
           i12 = L.dc[DC_I12][ln], i22 = L.dc[DC_I22][ln];
+  R rw[4][3], lam[4][3], rhs[4][3], jdi[4][3], jdn[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      rw[p][e] = L.DC_ISL(DI_RW + 3 * p + e)[ln];
+      lam[p][e] = L.DC_ISL(DI_LAM + 3 * p + e)[ln];
+      rhs[p][e] = L.DC_ISL(DI_RHS + 3 * p + e)[ln];
+      jdi[p][e] = L.DC_ISL(DI_JDI + 3 * p + e)[ln];
+    }
+    jdn[p] = L.DC_ISL(DI_JDN + p)[ln];
+  }
   R res = R(0);
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    const R rwx = L.DC_ISL(DI_RW + 3 * p)[ln], rwy = L.DC_ISL(DI_RW + 3 * p + 1)[ln], rwz = L.DC_ISL(DI_RW + 3 * p + 2)[ln];
+    const R rwx = rw[p][0], rwy = rw[p][1], rwz = rw[p][2];
     if (!friction) {
-      if (!(L.DC_ISL(DI_JDN + p)[ln] > R(0))) continue;   // inactive point (the oracle has no row)
+      // an inactive point has rhs = jdi = jdn = 0 and lam = 0: delta = 0
       const R ax = rwy, ay = -rwx;
+      const R g0 = STAGE ? G.ig[DG_G + 3 * p][ln] : pc_dot(i00, i01, i02, ax, ay, R(0));
+      const R g1 = STAGE ? G.ig[DG_G + 3 * p + 1][ln] : pc_dot(i01, i11, i12, ax, ay, R(0));
+      const R g2 = STAGE ? G.ig[DG_G + 3 * p + 2][ln] : pc_dot(i02, i12, i22, ax, ay, R(0));
       const R jv = dl2 + (ax * da0 + ay * da1);
-      R delta = L.DC_ISL(DI_RHS + 3 * p)[ln] - L.DC_ISL(DI_JDI + 3 * p)[ln] * jv;
-      const R lam = L.DC_ISL(DI_LAM + 3 * p)[ln];
-      const R sum = lam + delta;
+      R delta = rhs[p][0] - jdi[p][0] * jv;
+      const R sum = lam[p][0] + delta;
       const bool neg = sum < R(0);
-      delta = neg ? -lam : delta;
-      L.DC_ISL(DI_LAM + 3 * p)[ln] = neg ? R(0) : sum;
+      delta = neg ? -lam[p][0] : delta;
+      lam[p][0] = neg ? R(0) : sum;
       dl2 = dl2 + inv_m * delta;
-      da0 = da0 + pc_dot(i00, i01, i02, ax, ay, R(0)) * delta;
-      da1 = da1 + pc_dot(i01, i11, i12, ax, ay, R(0)) * delta;
-      da2 = da2 + pc_dot(i02, i12, i22, ax, ay, R(0)) * delta;
-      const R rr = delta * L.DC_ISL(DI_JDN + p)[ln];
+      da0 = da0 + g0 * delta;
+      da1 = da1 + g1 * delta;
+      da2 = da2 + g2 * delta;
+      const R rr = delta * jdn[p];
       res = g_fmax(res, rr * rr);
     } else {
-      const R lnrm = L.DC_ISL(DI_LAM + 3 * p)[ln];
-      if (!(lnrm > R(0))) continue;
+      const R lnrm = lam[p][0];
+      const bool act = lnrm > R(0);
       const R lim = mu * lnrm;
-      const R l1 = L.DC_ISL(DI_LAM + 3 * p + 1)[ln], l2 = L.DC_ISL(DI_LAM + 3 * p + 2)[ln];
+      const R l1 = lam[p][1], l2 = lam[p][2];
       // (0,-1,0): a = (rz, 0, -rx); (1,0,0): a = (0, rz, -ry)
+      const R h0 = STAGE ? G.ig[DG_H + 3 * p][ln] : pc_dot(i00, i01, i02, rwz, R(0), -rwx);
+      const R h1 = STAGE ? G.ig[DG_H + 3 * p + 1][ln] : pc_dot(i01, i11, i12, rwz, R(0), -rwx);
+      const R h2 = STAGE ? G.ig[DG_H + 3 * p + 2][ln] : pc_dot(i02, i12, i22, rwz, R(0), -rwx);
+      const R k0 = STAGE ? G.ig[DG_K + 3 * p][ln] : pc_dot(i00, i01, i02, R(0), rwz, -rwy);
+      const R k1 = STAGE ? G.ig[DG_K + 3 * p + 1][ln] : pc_dot(i01, i11, i12, R(0), rwz, -rwy);
+      const R k2 = STAGE ? G.ig[DG_K + 3 * p + 2][ln] : pc_dot(i02, i12, i22, R(0), rwz, -rwy);
       const R j1 = (rwz * da0 - rwx * da2) - dl1;
       const R j2 = (rwz * da1 - rwy * da2) + dl0;
-      R s1 = l1 + (L.DC_ISL(DI_RHS + 3 * p + 1)[ln] - L.DC_ISL(DI_JDI + 3 * p + 1)[ln] * j1);
-      R s2 = l2 + (L.DC_ISL(DI_RHS + 3 * p + 2)[ln] - L.DC_ISL(DI_JDI + 3 * p + 2)[ln] * j2);
+      R s1 = l1 + (rhs[p][1] - jdi[p][1] * j1);
+      R s2 = l2 + (rhs[p][2] - jdi[p][2] * j2);
       const R m2 = s1 * s1 + s2 * s2;
-      if (m2 > lim * lim) {
-        const R f = lim * g_rsqrt1(m2);
-        s1 = s1 * f;
-        s2 = s2 * f;
-      }
-      const R d1 = s1 - l1, d2 = s2 - l2;
-      L.DC_ISL(DI_LAM + 3 * p + 1)[ln] = s1;
-      L.DC_ISL(DI_LAM + 3 * p + 2)[ln] = s2;
+      const bool cap = m2 > lim * lim;
+      const R f = cap ? lim * g_rsqrt1(cap ? m2 : R(1)) : R(1);
+      s1 = s1 * f;
+      s2 = s2 * f;
+      const R d1 = act ? s1 - l1 : R(0), d2 = act ? s2 - l2 : R(0);
+      lam[p][1] = act ? s1 : l1;
+      lam[p][2] = act ? s2 : l2;
       dl1 = dl1 - inv_m * d1;
       dl0 = dl0 + inv_m * d2;
-      da0 = da0 + pc_dot(i00, i01, i02, rwz, R(0), -rwx) * d1;
-      da1 = da1 + pc_dot(i01, i11, i12, rwz, R(0), -rwx) * d1;
-      da2 = da2 + pc_dot(i02, i12, i22, rwz, R(0), -rwx) * d1;
-      da0 = da0 + pc_dot(i00, i01, i02, R(0), rwz, -rwy) * d2;
-      da1 = da1 + pc_dot(i01, i11, i12, R(0), rwz, -rwy) * d2;
-      da2 = da2 + pc_dot(i02, i12, i22, R(0), rwz, -rwy) * d2;
+      da0 = da0 + h0 * d1;
+      da1 = da1 + h1 * d1;
+      da2 = da2 + h2 * d1;
+      da0 = da0 + k0 * d2;
+      da1 = da1 + k1 * d2;
+      da2 = da2 + k2 * d2;
       const R rr = d1 + d2;
       res = g_fmax(res, rr * rr);
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if (!friction) {
+      L.DC_ISL(DI_LAM + 3 * p)[ln] = lam[p][0];
+    } else {
+      L.DC_ISL(DI_LAM + 3 * p + 1)[ln] = lam[p][1];
+      L.DC_ISL(DI_LAM + 3 * p + 2)[ln] = lam[p][2];
     }
   }
   L.dc[DC_DLX][ln] = dl0; L.dc[DC_DLY][ln] = dl1; L.dc[DC_DLZ][ln] = dl2;
@@ -1161,7 +1249,7 @@ __device__ __noinline__ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthi
 }
 // plane: the ground plane is on (the island solve takes the plane rows of drones in a pair contact
 // that touch it, bullet_mb.drone_contact(plane=True)); nact: the block's drones
-template <typename R>
+template <typename R, bool STAGE>
 __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln, DcPairs dp, bool plane) {
 #ifdef GPD_CONTACT_STATS
   const unsigned long long t0 = __builtin_readcyclecounter();
@@ -1250,7 +1338,7 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
           dist = L.DC_ST(DS_FD + (m - 1))[sl];
         }
         DcRow<R> w;
-        dc_row_setup(L, i, j, n, pb, dist, c, inv_m, idt, w);
+        dc_row_setup<STAGE>(L, i, j, n, pb, dist, c, inv_m, idt, w, cc < kWave ? cc : -1);
         w.env = i / dp.D;
         w.rank = 0;   // the level pass below re-ranks when some env holds two contacts
         if (cc < kWave) {
@@ -1283,7 +1371,7 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
   bool isl = false;
   if (plane) {
     wave_lds_sync();
-    if (L.stouch[ln]) isl = island_rows(L, ln, c, inv_m, idt);
+    if (L.stouch[ln]) isl = island_rows<STAGE>(L, ln, c, inv_m, idt);
     L.island[ln] = isl ? 1 : 0;
   }
   const bool any_isl = __ballot(isl) != 0ull;
@@ -1359,7 +1447,7 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
     // ---- every env has at most one contact and no island: its lane owns both drones' deltas
     R vi[6] = {R(0), R(0), R(0), R(0), R(0), R(0)}, vj[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
     DcInv<R> I0;
-    dc_inv(L, w0.i, w0.j, I0);
+    if (!STAGE) dc_inv(L, w0.i, w0.j, I0);
     bool done = !have0;
     for (int it = 0; it < iters; ++it) {
       if (__ballot(!done) == 0ull) break;
@@ -1367,8 +1455,16 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
       it_used = it + 1;
 #endif
       if (!done) {
-        R res = dc_normal(w0, inv_m, vi, vj, I0);
-        res = g_fmax(res, dc_friction(w0, mu, inv_m, vi, vj, I0));
+        R res;
+        if (STAGE) {
+          const DcJacLds<R> J0{dc_stage<R>(), ln};
+          res = dc_normal(w0, inv_m, vi, vj, J0);
+          res = g_fmax(res, dc_friction(w0, mu, inv_m, vi, vj, J0));
+        } else {
+          const DcJacRow<R> J0{w0, I0};
+          res = dc_normal(w0, inv_m, vi, vj, J0);
+          res = g_fmax(res, dc_friction(w0, mu, inv_m, vi, vj, J0));
+        }
         done = res <= resid;
       }
     }
@@ -1383,52 +1479,96 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
     // (one round: each drone's own rows), then round r solves the level-r contacts of every env;
     // deltas through LDS (bullet_mb.drone_contact's order: plane normal, pair normal, plane
     // friction, pair friction)
-    if (ln < nenv) L.edone[ln] = L.ecnt[ln] == 0;
+    if (ln < nenv) { L.edone[ln] = L.ecnt[ln] == 0; L.eres[ln] = R(0); }
     wave_lds_sync();
     R vi[6], vj[6];
-    auto visit = [&](DcRow<R>& w, bool friction) {
-      if (L.edone[w.env]) return;
-      DcInv<R> I;
-      dc_inv(L, w.i, w.j, I);
+    // one row: deltas from LDS, the row's step, deltas back; its squared residual
+    auto visit = [&](DcRow<R>& w, bool friction, int slot) -> R {
 #pragma unroll
       for (int x = 0; x < 6; ++x) { vi[x] = L.dc[DC_DLX + x][w.i]; vj[x] = L.dc[DC_DLX + x][w.j]; }
-      const R rr = friction ? dc_friction(w, mu, inv_m, vi, vj, I) : dc_normal(w, inv_m, vi, vj, I);
+      R rr;
+      if (STAGE && slot >= 0) {
+        const DcJacLds<R> J{dc_stage<R>(), slot};
+        rr = friction ? dc_friction(w, mu, inv_m, vi, vj, J) : dc_normal(w, inv_m, vi, vj, J);
+      } else {
+        DcInv<R> I;
+        dc_inv(L, w.i, w.j, I);
+        const DcJacRow<R> J{w, I};
+        rr = friction ? dc_friction(w, mu, inv_m, vi, vj, J) : dc_normal(w, inv_m, vi, vj, J);
+      }
 #pragma unroll
       for (int x = 0; x < 6; ++x) { L.dc[DC_DLX + x][w.i] = vi[x]; L.dc[DC_DLX + x][w.j] = vj[x]; }
-      eres_max(L, w.env, rr);
+      return rr;
     };
     const int my_env = ln / dp.D;
+#ifdef GPD_CONTACT_STATS
+    unsigned long long tg_isl = 0, tg_nrm = 0, tg_fr = 0, tg_end = 0, tg0 = __builtin_readcyclecounter();
+#endif
     for (int it = 0; it < iters; ++it) {
+      // edone / eres of every env are settled here (the previous iteration's end)
       if (__ballot(ln < nenv && !L.edone[ln]) == 0ull) break;
 #ifdef GPD_CONTACT_STATS
       it_used = it + 1;
 #endif
-      if (ln < nenv) L.eres[ln] = R(0);
-      wave_lds_sync();
+      // the envs still iterating, read once per iteration; each lane's residuals per env in registers
+      const bool live0 = have0 && !L.edone[w0.env], live1 = have1 && !L.edone[w1.env];
+      const bool livei = isl && !L.edone[my_env];
+      R res0 = R(0), res1 = R(0), resi = R(0);
       for (int ph = 0; ph < 2; ++ph) {              // normal rows, then friction pairs
+#ifdef GPD_CONTACT_STATS
+        const unsigned long long tga = __builtin_readcyclecounter();
+        tg_end += tga - tg0;
+#endif
         if (any_isl) {
-          if (isl && !L.edone[my_env]) eres_max(L, my_env, island_sweep(L, ln, ph == 1, pmu, inv_m));
+          if (livei) resi = g_fmax(resi, island_sweep<STAGE>(L, ln, ph == 1, pmu, inv_m));
           wave_lds_sync();
         }
+#ifdef GPD_CONTACT_STATS
+        const unsigned long long tgb = __builtin_readcyclecounter();
+        tg_isl += tgb - tga;
+#endif
         for (int r = 0; r < rounds; ++r) {
-          if (have0 && w0.rank == r) visit(w0, ph == 1);
-          if (have1 && w1.rank == r) visit(w1, ph == 1);
+          if (live0 && w0.rank == r) res0 = g_fmax(res0, visit(w0, ph == 1, ln));
+          if (live1 && w1.rank == r) res1 = g_fmax(res1, visit(w1, ph == 1, -1));
           for (int ch = kDcRegRows; ch < ncpass; ++ch) {
             if (((L.contw[ch] >> ln) & 1ull) == 0) continue;
             R* chunk = rows + (long long)(ch - kDcRegRows) * kWave * kRowR;
             if (reinterpret_cast<const int*>(chunk + kRowReal * kWave)[3 * kWave + ln] != r) continue;   // its rank
             DcRow<R> w;
             dc_row_load(chunk, ln, w);
-            visit(w, ph == 1);
+            if (L.edone[w.env]) continue;
+            eres_max(L, w.env, visit(w, ph == 1, -1));
 #pragma unroll
             for (int q = 0; q < 3; ++q) chunk[(kRowLam + q) * kWave + ln] = w.lam[q];
           }
           wave_lds_sync();
         }
+#ifdef GPD_CONTACT_STATS
+        tg0 = __builtin_readcyclecounter();
+        if (ph == 0) tg_nrm += tg0 - tgb; else tg_fr += tg0 - tgb;
+#endif
       }
-      if (ln < nenv && !L.edone[ln]) L.edone[ln] = L.eres[ln] <= resid;
+      if (live0) eres_max(L, w0.env, res0);
+      if (live1) eres_max(L, w1.env, res1);
+      if (livei) eres_max(L, my_env, resi);
+      wave_lds_sync();
+      if (ln < nenv) {
+        if (!L.edone[ln]) L.edone[ln] = L.eres[ln] <= resid;
+        L.eres[ln] = R(0);
+      }
       wave_lds_sync();
     }
+#ifdef GPD_CONTACT_STATS
+    tg_end += __builtin_readcyclecounter() - tg0;
+    if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) {
+      atomicAdd(&g_pc_hist[kPcNp + 7], tg_isl);    // general path: island sweeps
+      atomicAdd(&g_pc_hist[kPcNp + 8], tg_nrm);    // normal rounds
+      atomicAdd(&g_pc_hist[kPcNp + 9], tg_fr);     // friction rounds
+      atomicAdd(&g_pc_hist[kPcNp + 10], tg_end);   // iteration ends (convergence checks)
+      atomicAdd(&g_pc_hist[kPcNp + 11], (unsigned long long)it_used * rounds);   // rounds per phase run
+      atomicAdd(&g_pc_hist[kPcNp + 12], (unsigned long long)it_used);            // general-path iterations
+    }
+#endif
   }
 #ifdef GPD_CONTACT_STATS
   {
@@ -1526,7 +1666,7 @@ struct DcHook {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const unsigned long long tr2 = __builtin_readcyclecounter();
 #endif
-      dc_solve<R>(&c, inv_m, dt, ln, dpc, plane);
+      dc_solve<R, PK::kStage>(&c, inv_m, dt, ln, dpc, plane);
 #ifdef GPD_CONTACT_STATS
       const unsigned long long tr3 = __builtin_readcyclecounter();
 #endif

@@ -115,6 +115,11 @@ def run(case, E=4096, warm=int(os.environ.get("PROBE_WARM", 60)), steps=int(os.e
             if h[npb]:
                 print(f"   contacts: most in one solve {h[255]}, solves past the register rows {h[npb + 5]}, "
                       f"contact passes per solve {h[npb + 6] / h[116]:.2f}", flush=True)
+                if h[npb + 12]:
+                    gi = h[npb + 12]
+                    print(f"   general-path iterations {gi}: per iteration island sweeps {h[npb + 7] / gi:.0f}, "
+                          f"normal rounds {h[npb + 8] / gi:.0f}, friction rounds {h[npb + 9] / gi:.0f}, ends "
+                          f"{h[npb + 10] / gi:.0f} cycles; rounds per phase {h[npb + 11] / gi:.2f}", flush=True)
                 print(f"   narrowphase passes {h[npb]}: near pairs {h[npb + 3] / h[npb]:.2f}, rim tasks "
                       f"{h[npb + 1] / h[npb]:.0f}, selection {h[npb + 2] / h[npb]:.0f}, fallback + face points "
                       f"{h[npb + 4] / h[npb]:.0f} cycles per pass", flush=True)
