@@ -1084,7 +1084,15 @@ __device__ __forceinline__ void eres_max(DcLds<R>& L, int env, R rr) {
 // ln < nthis stages its pair's result in L.st and its face-point mask in L.nsp[ln] and returns its
 // contact count.  A call: its registers stay out of dc_solve's Gauss-Seidel loops.
 template <typename R>
-__device__ __noinline__ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthis) {
+#ifndef GPD_NP_INLINE
+#define GPD_NP_INLINE 0   // A/B builds: 1 = the narrowphase pass inlined into dc_solve
+#endif
+#if GPD_NP_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+int dc_narrow_pass(const Consts<R>* cp, int ln, int nthis) {
   DcLds<R>& L = dc_lds<R>();
   const Consts<R>& c = *cp;
 #ifdef GPD_CONTACT_STATS
@@ -1371,7 +1379,15 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
   bool isl = false;
   if (plane) {
     wave_lds_sync();
-    if (L.stouch[ln]) isl = island_rows<STAGE>(L, ln, c, inv_m, idt);
+    // a drone in contact whose lowest plane candidate is above the breaking threshold has no plane
+    // row (the plane solve's own gate, contact_low, with its margin): no island, rows not formed
+    bool low = false;
+    if (L.stouch[ln]) {
+      const R r8 = L.dc[DC_AZ][ln], h67 = g_max1(g_abs(L.dc[DC_R6][ln]), g_abs(L.dc[DC_R7][ln]));
+      const R zc = (-r8 < R(0) ? -c.cyl_hh : c.cyl_hh) + c.cyl_zoff;
+      low = (L.dc[DC_PZ][ln] + r8 * zc) - c.cyl_r * h67 < c.brk + R(1e-6);
+    }
+    if (__ballot(low) != 0ull && low) isl = island_rows<STAGE>(L, ln, c, inv_m, idt);
     L.island[ln] = isl ? 1 : 0;
   }
   const bool any_isl = __ballot(isl) != 0ull;
