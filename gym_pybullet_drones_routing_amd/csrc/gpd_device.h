@@ -10,6 +10,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 namespace gpd {
 
@@ -1167,7 +1168,10 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, R rpm[4], R W[4], R 
   // so the loop's register allocation does not see it.  The reload goes through an opaque lane
   // offset, so nothing forwards the stored values past the solve; a memory clobber keeps the
   // stores ahead of it.
-  constexpr int kPark = 15 + 12 + 4 + 12, kParkRm = 9;
+  // (the basis columns only where the drone <-> drone hook parks it: single-drone kernels keep
+  // the 43 columns of the plane solve)
+  constexpr bool kDcPark = !std::is_same<HK, NoDc>::value;
+  constexpr int kPark = 15 + 12 + 4 + 12, kParkRm = kDcPark ? 9 : 0;
   __shared__ R pk[kPark + kParkRm][kWaveLanes];
   const int pl = threadIdx.x & (kWaveLanes - 1);
   auto each = [&](auto&& f) {
@@ -1194,7 +1198,7 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, R rpm[4], R W[4], R 
   auto park_dc = [&]() {
     park();
 #pragma unroll
-    for (int j = 0; j < 9; ++j) pk[kPark + j][pl] = Rm[j];
+    for (int j = 0; j < kParkRm; ++j) pk[kPark + j][pl] = Rm[j];
     asm volatile("" ::: "memory");
   };
   auto unpark_dc = [&]() {
@@ -1202,7 +1206,7 @@ __device__ __forceinline__ void bullet_substep(Drone<R>& s, R rpm[4], R W[4], R 
     int o = pl;
     asm volatile("" : "+v"(o));
 #pragma unroll
-    for (int j = 0; j < 9; ++j) Rm[j] = pk[kPark + j][o];
+    for (int j = 0; j < kParkRm; ++j) Rm[j] = pk[kPark + j][o];
   };
   // island: this drone's plane rows were solved with its pair contacts (the hook's island solve)
   bool island = false;
