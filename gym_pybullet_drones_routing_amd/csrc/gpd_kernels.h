@@ -1000,6 +1000,9 @@ __device__ __forceinline__ R island_sweep(DcLds<R>& L, int ln, bool friction, R 
   R res = R(0);
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
+    // a point no island lane of the wave has a row for (inactive, or a friction pair whose normal
+    // impulse is not positive) is skipped by the whole wave: its zero step changes nothing
+    if (__ballot(friction ? lam[p][0] > R(0) : jdn[p] > R(0)) == 0ull) continue;
     const R rwx = rw[p][0], rwy = rw[p][1], rwz = rw[p][2];
     if (!friction) {
       // an inactive point has rhs = jdi = jdn = 0 and lam = 0: delta = 0
