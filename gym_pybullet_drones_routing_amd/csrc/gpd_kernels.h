@@ -280,7 +280,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 //     give the normal (B -> A) and distance core - 2 x margin, with thicker margins for deeper
 //     overlaps (up to ~2 cm), beyond that the least overlap over the centre line and the two axes;
 //   * a cap-to-cap contact adds its face manifold (face_points: four points spanning the caps'
-//     overlap), each point below the breaking threshold a contact of the pair;
+//     overlap), each point below the breaking threshold a contact of the pair; at most four points
+//     per pair (Bullet's MANIFOLD_CACHE_SIZE): with four face points the closest point replaces the
+//     one sortCachedPoints would (manifold_replace);
 //   * EVERY pair whose distance is below the breaking threshold is in contact (up to kDcPts
 //     contacts per pair), solved in (i, j) order;
 //   * rows (normal, btPlaneSpace1 friction pair) between two bodies: effective mass
@@ -577,6 +579,37 @@ __device__ __forceinline__ bool face_points(const R ca[3], const R aa[3], const 
   }
   return true;
 }
+// bullet_mb.manifold_replace (btPersistentManifold::sortCachedPoints): the slot of the full cache
+// (the four face points: point on B fp, distance fd) the closest point (pb, dist) replaces - never
+// a cached point deeper than it, else the slot whose replacement spans the largest quad (Bullet's
+// pairing of the cached points on A), the first of a tie; the ties (depth, area) keep rounding
+// from deciding a symmetric manifold
+template <typename R> struct MfTol;
+template <> struct MfTol<double> { static constexpr double depth = 1e-9, area = 1e-9; };   // MANIFOLD_*_TIE
+template <> struct MfTol<float> { static constexpr float depth = 1e-6f, area = 1e-4f; };
+template <typename R>
+__device__ __forceinline__ int manifold_replace(const R pb[3], R dist, const R n[3], const R fp[4][3], const R fd[4]) {
+  const R nw[3] = {pb[0] + n[0] * dist, pb[1] + n[1] * dist, pb[2] + n[2] * dist};
+  R ca[4][3];
+  R maxpen = dist;
+  int imax = -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    ca[k][0] = fp[k][0] + n[0] * fd[k]; ca[k][1] = fp[k][1] + n[1] * fd[k]; ca[k][2] = fp[k][2] + n[2] * fd[k];
+    if (fd[k] < maxpen - MfTol<R>::depth) { maxpen = fd[k]; imax = k; }
+  }
+  R res[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {   // res_k = |(new - c_a) x (c_b - c_c)|^2, (a, b, c) = (1,3,2) (0,3,2) (0,3,1) (0,2,1)
+    const int a = k == 0 ? 1 : 0, b = k < 3 ? 3 : 2, c = k < 2 ? 2 : 1;
+    const R x0 = nw[0] - ca[a][0], x1 = nw[1] - ca[a][1], x2 = nw[2] - ca[a][2];
+    const R y0 = ca[b][0] - ca[c][0], y1 = ca[b][1] - ca[c][1], y2 = ca[b][2] - ca[c][2];
+    const R z0 = x1 * y2 - x2 * y1, z1 = x2 * y0 - x0 * y2, z2 = x0 * y1 - x1 * y0;
+    res[k] = k == imax ? R(0) : pc_dot(z0, z1, z2, z0, z1, z2);
+  }
+  const R top = g_max1(g_max1(res[0], res[1]), g_max1(res[2], res[3])) * (R(1) - MfTol<R>::area);
+  return res[0] >= top ? 0 : (res[1] >= top ? 1 : (res[2] >= top ? 2 : 3));
+}
 #ifndef GPD_DC_DIAG
 #define GPD_DC_DIAG 0   // diagnostic builds only: 1 = broadphase only (no solve compiled),
                         // 3 = no drone contact, 6 = the solve compiled but never entered, 7 = the
@@ -586,7 +619,7 @@ enum { DC_CX, DC_CY, DC_CZ, DC_AX, DC_AY, DC_AZ, DC_PX, DC_PY, DC_PZ, DC_VX, DC_
        DC_I00, DC_I01, DC_I02, DC_I11, DC_I12, DC_I22, DC_DLX, DC_DLY, DC_DLZ, DC_DAX, DC_DAY, DC_DAZ,
        DC_R0, DC_R1, DC_R3, DC_R4, DC_R6, DC_R7, DC_N };   // DC_R*: the basis entries beside the axis (Rm[2,5,8])
 constexpr int kDcChunks = 32;   // pair chunks of a block: <= 64 (D-1) / 2 / 64 + 1 for D <= 64
-constexpr int kDcPts = 5;       // contacts per pair: the closest point + the face manifold's four
+constexpr int kDcPts = 4;       // contacts per pair: Bullet's MANIFOLD_CACHE_SIZE (bullet_mb.pair_manifold)
 constexpr int kDcConPasses = kDcPts * kDcChunks;   // 64-contact passes of a block
 // a near pair's narrowphase, staged for the lanes that set up its contacts' rows
 enum { DS_N = 0, DS_PB = 3, DS_D = 6, DS_FP = 7, DS_FD = 19, DS_NUM = 23 };
@@ -1247,6 +1280,9 @@ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthis) {
   int fmask = 0;
 #pragma unroll
   for (int m = 0; m < 4; ++m) fmask |= (face && fd[m] < brk) ? (1 << m) : 0;
+  // at most four points per pair, Bullet's MANIFOLD_CACHE_SIZE (bullet_mb.pair_manifold): with all
+  // four face points the closest point takes the slot btPersistentManifold::sortCachedPoints frees
+  const int rep = fmask == 15 ? manifold_replace(pb, dist, n, fp, fd) : -1;
   L.DC_ST(DS_N)[ln] = n[0]; L.DC_ST(DS_N + 1)[ln] = n[1]; L.DC_ST(DS_N + 2)[ln] = n[2];
   L.DC_ST(DS_PB)[ln] = pb[0]; L.DC_ST(DS_PB + 1)[ln] = pb[1]; L.DC_ST(DS_PB + 2)[ln] = pb[2];
   L.DC_ST(DS_D)[ln] = dist;
@@ -1255,8 +1291,9 @@ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthis) {
     L.DC_ST(DS_FP + 3 * m)[ln] = fp[m][0]; L.DC_ST(DS_FP + 3 * m + 1)[ln] = fp[m][1]; L.DC_ST(DS_FP + 3 * m + 2)[ln] = fp[m][2];
     L.DC_ST(DS_FD + m)[ln] = fd[m];
   }
-  L.nsp[ln] = fmask;   // reused: the pair's face-point mask (its pair index is no longer needed)
-  return con ? 1 + __popc(fmask) : 0;
+  L.nsp[ln] = fmask | ((rep + 1) << 4);   // reused (the pair index is no longer needed): face-point
+                                          // mask, and 1 + the slot the closest point replaces (0: none)
+  return con ? (rep >= 0 ? 4 : 1 + __popc(fmask)) : 0;
 }
 // plane: the ground plane is on (the island solve takes the plane rows of drones in a pair contact
 // that touch it, bullet_mb.drone_contact(plane=True)); nact: the block's drones
@@ -1318,12 +1355,12 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
     int total;
     const int off = wave_excl_scan(cnt, ln, total);
     if (cnt > 0) {
-      const int fmask = L.nsp[ln];
+      const int fmask = L.nsp[ln] & 15, rep = (L.nsp[ln] >> 4) - 1;
       int q = off;
-      L.qmap[q++] = ln;
+      if (rep < 0) L.qmap[q++] = ln;          // the closest point first, then the face points
 #pragma unroll
       for (int m = 0; m < 4; ++m)
-        if ((fmask >> m) & 1) L.qmap[q++] = ln | ((m + 1) << 8);
+        if ((fmask >> m) & 1) L.qmap[q++] = m == rep ? ln : ln | ((m + 1) << 8);
     }
     wave_lds_sync();
 #ifdef GPD_CONTACT_STATS

@@ -612,12 +612,61 @@ def face_points(ca, aa, cb, ab, n, radius, half_height, mg):
     return out
 
 
+MANIFOLD_CACHE_SIZE = 4     # btPersistentManifold's point capacity
+MANIFOLD_DEPTH_TIE = 1e-9   # a cached point counts as deeper than the new one only beyond this (m)
+MANIFOLD_AREA_TIE = 1e-9    # areas within this fraction of the largest count as tied: the first wins
+
+
+def manifold_replace(new_a, new_d, cache):
+    """btPersistentManifold::sortCachedPoints: the cache slot a new point replaces when the cache
+    is full.  ``new_a``: the new point on A, ``new_d`` its distance; ``cache``: 4 (point on A,
+    distance).  The deepest point (KEEP_DEEPEST_POINT: a cached point deeper than the new one) is
+    never replaced; for every other slot the "area" |(new - c_a) x (c_b - c_c)|^2 of the quad with
+    that slot replaced (Bullet's pairing of the cached points), and the slot of the largest wins
+    (btVector4::closestAxis4: the first maximum).  The two comparisons carry ties
+    (MANIFOLD_DEPTH_TIE, MANIFOLD_AREA_TIE): a symmetric manifold (a level stack: every point at the
+    same distance, two equal areas) must not be decided by rounding, so the GPU's f64 and f32
+    builds take the same slot as this restatement."""
+    maxpen, imax = new_d, -1
+    for i, (_, d) in enumerate(cache):
+        if d < maxpen - MANIFOLD_DEPTH_TIE:
+            maxpen, imax = d, i
+    c = [np.asarray(a, dtype=np.float64) for a, _ in cache]
+    pairs = ((1, 3, 2), (0, 3, 2), (0, 3, 1), (0, 2, 1))     # res_k = |(new - c_a) x (c_b - c_c)|^2
+    res = []
+    for k, (a, b, cc) in enumerate(pairs):
+        if k == imax:
+            res.append(0.0)
+            continue
+        x = np.cross(new_a - c[a], c[b] - c[cc])
+        res.append(float(x @ x))
+    top = max(res)
+    return next(k for k, v in enumerate(res) if v >= top * (1.0 - MANIFOLD_AREA_TIE))
+
+
+def pair_manifold(pb, dist, n, face):
+    """A contact pair's points, at most MANIFOLD_CACHE_SIZE like Bullet's manifold: the closest
+    point (pb, dist) and the face points ``face`` (already below the breaking threshold).  With
+    four face points the closest point takes the slot ``manifold_replace`` picks (Bullet adding a
+    point to a full cache); with fewer, the closest point comes first and the face points follow.
+    Round 5 kept all five: the closest point of a level stack is the cap centre, inside the lens the
+    face points span, so every face contact had five nearly dependent normal rows - one more than
+    Bullet can hold - and where Gauss-Seidel stopped depended on rounding."""
+    if len(face) < MANIFOLD_CACHE_SIZE:
+        return [(pb, dist)] + list(face)
+    k = manifold_replace(pb + n * dist, dist, [(p + n * d, d) for p, d in face])
+    out = list(face)
+    out[k] = (pb, dist)
+    return out
+
+
 def drone_contacts(pos, rot_bw, radius, half_height, z_offset):
     """The env's contacts in solve order: pairs (i, j), i < j, lexicographic, that pass the
     broadphase (``pair_near``) and whose distance is below the breaking threshold - every such
     pair, however many (up to D (D - 1) / 2; round 3 kept at most D).  Per pair: the closest
-    points (``pair_geometry``), then for a cap-to-cap contact its face manifold (``face_points``)
-    points below the breaking threshold, as further contacts of the same pair (i, j, n, pb, dist)."""
+    points (``pair_geometry``) and, for a cap-to-cap contact, its face manifold (``face_points``)
+    points below the breaking threshold - at most four points per pair (``pair_manifold``) - as
+    contacts of the same pair (i, j, n, pb, dist)."""
     D = pos.shape[0]
     brk = breaking_threshold(radius, half_height)
     axes = [rot_bw[i][:, 2].copy() for i in range(D)]
@@ -629,11 +678,11 @@ def drone_contacts(pos, rot_bw, radius, half_height, z_offset):
                 continue
             n, pb, dist, mg = pair_geometry(cent[i], axes[i], cent[j], axes[j], radius, half_height, with_margin=True)
             if dist < brk:
-                out.append((i, j, n, pb, dist))
-                if mg is not None:
-                    for pb2, d2 in face_points(cent[i], axes[i], cent[j], axes[j], n, radius, half_height, mg):
-                        if d2 < brk:
-                            out.append((i, j, n, pb2, d2))
+                face = [] if mg is None else \
+                    [(p, d) for p, d in face_points(cent[i], axes[i], cent[j], axes[j], n, radius, half_height, mg)
+                     if d < brk]
+                for p, d in pair_manifold(pb, dist, n, face):
+                    out.append((i, j, n, p, d))
     return out
 
 

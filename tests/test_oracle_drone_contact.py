@@ -4,7 +4,7 @@ import math
 
 import numpy as np
 
-from oracle.bullet_mb import (LINEAR_SLOP, breaking_threshold, cyl_project, drone_contact, drone_contacts, pair_geometry,
+from oracle.bullet_mb import (CORE_MARGINS, LINEAR_SLOP, breaking_threshold, cyl_project, drone_contact, drone_contacts, pair_geometry,
                               pair_near, plane_space)
 from oracle.bullet_math import quat_from_euler, quat_to_mat
 from oracle.params import derived
@@ -101,12 +101,19 @@ def _pairs(cons):
 
 def test_contact_order_and_no_cap():
     # five drones stacked tightly: 4 adjacent contacts (+ none at two levels apart), in (i, j) order;
-    # each a cap-to-cap contact: the closest point and the four points of its face manifold
+    # each a cap-to-cap contact: four points, Bullet's manifold capacity - the face manifold's four
+    # with the closest point (the cap centre) in the slot btPersistentManifold::sortCachedPoints
+    # frees: slot 0 (the lens tip (s - r) u; areas 4 r^4, 4 r^4, r^4, r^4, the first of the tie)
     pos = np.array([[0, 0, 1.0 + 0.0245 * k] for k in range(5)])
     rot = np.array([np.eye(3)] * 5)
     cons = drone_contacts(pos, rot, R_, HH, ZO)
     assert _pairs(cons) == [(0, 1), (1, 2), (2, 3), (3, 4)]
-    assert len(cons) == 4 * 5 and all(abs(c[4] - (0.0245 - 2 * HH)) < 1e-15 for c in cons)
+    assert len(cons) == 4 * 4 and all(abs(c[4] - (0.0245 - 2 * HH)) < 1e-15 for c in cons)
+    for k in range(4):
+        centre = cons[4 * k][3]
+        assert abs(centre[0]) < 1e-15 and abs(centre[1]) < 1e-15      # the cap centre took slot 0
+        for c in cons[4 * k + 1:4 * k + 4]:
+            assert math.hypot(c[3][0], c[3][1]) > 0.9 * (R_ - CORE_MARGINS[0])   # three rim points kept
     # four drones, six contacts (more than the env's D): a touching triangle with a fourth drone
     # resting on all three - every pair is kept
     tri = [[0, 0, 1.0], [0.1195, 0, 1.0], [0.05975, 0.1035, 1.0]]
@@ -119,6 +126,30 @@ def test_contact_order_and_no_cap():
     cons = drone_contacts(cube, np.array([np.eye(3)] * 8), R_, HH, ZO)
     assert len(_pairs(cons)) >= 12 and all(c[4] < breaking_threshold(R_, HH) for c in cons)
     assert breaking_threshold(R_, HH) < 0.002
+    per = {}
+    for c in cons:
+        per[(c[0], c[1])] = per.get((c[0], c[1]), 0) + 1
+    assert max(per.values()) == 4                      # never more than Bullet's MANIFOLD_CACHE_SIZE
+
+
+def test_manifold_replace_rule():
+    """bullet_mb.manifold_replace restates btPersistentManifold::sortCachedPoints: a cached point
+    deeper than the new one is never replaced, otherwise the slot whose replacement spans the
+    largest quad (|(new - c_a) x (c_b - c_c)|^2, Bullet's pairing) wins, the first of a tie."""
+    from oracle.bullet_mb import manifold_replace, pair_manifold
+    sq = [np.array(p, dtype=float) for p in ((-1, 0, 0), (1, 0, 0), (0, 1, 0), (0, -1, 0))]
+    # the new point at the centre, all equally deep: res = (4, 4, 1, 1) -> slot 0 (tie: the first)
+    assert manifold_replace(np.zeros(3), 0.0, [(p, 0.0) for p in sq]) == 0
+    # rounding-level depth differences do not protect a slot (MANIFOLD_DEPTH_TIE)
+    assert manifold_replace(np.zeros(3), 0.0, [(sq[0], -1e-13)] + [(p, 0.0) for p in sq[1:]]) == 0
+    # a truly deeper slot 0 is kept: the best of the others (res1 = 4) replaced
+    assert manifold_replace(np.zeros(3), 0.0, [(sq[0], -1e-3)] + [(p, 0.0) for p in sq[1:]]) == 1
+    # a new point far out along +x spans the largest quad in place of slot 1 (res1 = |(new - c0) x (c3 - c2)|^2)
+    assert manifold_replace(np.array([3.0, 0, 0]), 0.0, [(p, 0.0) for p in sq]) == 1
+    # fewer than four face points: the closest point first, then the face points (no replacement)
+    n = np.array([0, 0, 1.0])
+    got = pair_manifold(np.zeros(3), 0.0, n, [(sq[0], 0.0), (sq[1], 0.0)])
+    assert len(got) == 3 and got[0][1] == 0.0 and np.array_equal(got[1][0], sq[0])
 
 
 def test_face_manifold_points():
