@@ -491,63 +491,101 @@ def _policy_mlp(n_in, n_out):
 
 
 def handoff_leg(sim, global_envs, hmode, cap, gpool, G, rank, device, force=False):
-    """One LearnerHandoff configuration timed over G steps (after 3 warm ones): ms per step, the
-    bytes that land per step, how many steps needed the second (overflow) exchange and the
-    finished-env rate of the batch (mean / max envs per step, from the gathered done flags)."""
+    """One LearnerHandoff configuration, per step: eager ``step()`` calls (G steps after 3 warm
+    ones, wall clock, max over ranks); with the default capacity also the same calls replaying
+    the captured one-step hipGraph (``LearnerHandoff.capture``: scatter + shard step + pack +
+    collective + unpack) - ``ms_per_step`` - and a graph of 32 hand-off steps timed by HIP events
+    (the device-side cost per step, no host launch).  Also the bytes that land per step, how many
+    steps needed the second (overflow) exchange and the finished-env rate of the batch."""
     import torch.distributed as dist
 
     from gym_pybullet_drones_routing_amd.shard import LearnerHandoff, max_over_ranks
     h = LearnerHandoff(sim, global_envs, mode=hmode, force_collectives=force, terminal_capacity=cap)
-    for k in range(3):
-        h.step(gpool[k % 8] if rank == 0 else None)
-    torch.cuda.synchronize(device)
-    dist.barrier()
-    torch.cuda.synchronize(device)
-    h.terminal_bytes, h.steps, h.second_exchanges = 0, 0, 0
     fin = torch.zeros((G,), dtype=torch.int64, device=device)
-    t0 = time.perf_counter()
-    for k in range(G):
-        r = h.step(gpool[k % 8] if rank == 0 else None)
-        if r is not None:
-            fin[k] = (r[2] | r[3]).sum()
-    torch.cuda.synchronize(device)
-    gw = max_over_ranks(time.perf_counter() - t0, device)
-    out = dict(h.stats(), ms_per_step=1000 * gw / G)
+
+    def timed():
+        for k in range(3):
+            h.step(gpool[k % 8] if rank == 0 else None)
+        torch.cuda.synchronize(device)
+        dist.barrier()
+        torch.cuda.synchronize(device)
+        h.terminal_bytes, h.steps, h.second_exchanges = 0, 0, 0
+        t0 = time.perf_counter()
+        for k in range(G):
+            r = h.step(gpool[k % 8] if rank == 0 else None)
+            if r is not None:
+                fin[k] = (r[2] | r[3]).sum()
+        torch.cuda.synchronize(device)
+        return max_over_ranks(time.perf_counter() - t0, device)
+
+    eager = timed()
+    out = dict(h.stats(), eager_ms_per_step=1000 * eager / G)
+    if not h.host_sync_per_step and not h._stage:
+        g32 = h.capture(n_steps=32, install=False)
+        g32.replay()
+        torch.cuda.synchronize(device)
+        dist.barrier()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        for _ in range(4):
+            g32.replay()
+        ev1.record()
+        torch.cuda.synchronize(device)
+        out["graph32_us_per_step"] = max_over_ranks(1000.0 * ev0.elapsed_time(ev1) / (4 * 32), device)
+        del g32
+        h.capture()                       # step() replays one captured hand-off step from now on
+        out["ms_per_step"] = 1000 * timed() / G
+        out["graphed"] = True
+    else:
+        out["ms_per_step"] = out["eager_ms_per_step"]
     if rank == 0:
         f = fin.double()
         out["finished_envs_per_step"] = {"mean": float(f.mean()), "max": int(fin.max()),
                                          "frac_mean": float(f.mean()) / global_envs}
+    h.close()
     return out
 
 
 def rollout_leg(device, precision, act, E, K=64, reps=8, store_policy=2):
     """What an RL caller pays per env.step (the caller: examples/learn.py's PPO rollout, the
-    reference's learn.py:52-94 through SB3): ONE hipGraph of K x (actor and critic MLP forward on
-    the observation, Normal sample, clamp, gpd_step, the rollout-buffer copies) at E envs, against
-    the same graph without gpd_step.  Per step: the whole sequence, the policy part, and their
-    difference = the step's cost inside a rollout (its kernel plus the boundary, with the policy's
-    kernels between consecutive steps instead of another step), by HIP events over graph replays.
-    ``store_policy``: gpd_config::store_policy (0 = the library's choice); 2 (write-through rows),
-    what examples/learn.py sets: between the policy's kernels it measured 6.12 vs 6.40 us per step
-    against the back-to-back default 3 (five alternations, profiles/r4/rollout_policy/)."""
+    reference's learn.py:52-94 through SB3): ONE hipGraph of K x (policy, gpd_step) at E envs,
+    against the same graph without gpd_step, by HIP events over graph replays.  The policy is the
+    fused rollout kernel (``policy.MlpPolicyKernel``: actor + critic 64-64 tanh forward, Normal
+    sample, clip, the rollout-buffer rows and the previous step's time-limit bootstrap in one
+    launch; what examples/learn.py runs) and, beside it under ``torch_policy``, the same work as
+    torch library calls (nn.Linear / tanh / randn / clamp / copies).  ``store_policy``:
+    gpd_config::store_policy; 2 (write-through rows), what examples/learn.py sets (between the
+    policy's kernels it measured 6.12 vs 6.40 us per step against the default 3,
+    profiles/r4/rollout_policy/)."""
     from gym_pybullet_drones_routing_amd.enums import ActionType
+    from gym_pybullet_drones_routing_amd.policy import MlpPolicyKernel
     from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
     tuning = {"store_policy": store_policy} if store_policy else None
     sim = BatchedAviarySim(n_envs=E, task="hover", act=ActionType(act), precision=precision, autoreset=True,
                            device=device, tuning=tuning)
     W, A = sim.obs_width, sim.act_width
     torch.manual_seed(0)
-    pi, vf = _policy_mlp(W, A).to(device), _policy_mlp(W, 1).to(device)
-    log_std = torch.zeros(A, device=device)
+
+    class _AC(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.pi, self.vf = _policy_mlp(W, A), _policy_mlp(W, 1)
+            self.log_std = torch.nn.Parameter(torch.zeros(A))
+
+    ac = _AC().to(device)
+    pi, vf, log_std = ac.pi, ac.vf, ac.log_std.detach()
     obs = sim.obs.view(E, W)                      # sim-owned, rewritten in place by every step
+    tobs = sim.terminal_obs.view(E, W)
     act_buf = torch.zeros((E, 1, A), device=device)
     buf_obs = torch.zeros((K, E, W), device=device)
     buf_act = torch.zeros((K, E, A), device=device)
     buf_val = torch.zeros((K, E), device=device)
+    buf_logp = torch.zeros((K, E), device=device)
     buf_rew = torch.zeros((K, E), device=device)
     buf_done = torch.zeros((K, E), device=device)
+    kern = MlpPolicyKernel(ac, seed=1)
 
-    def seq(with_step):
+    def seq_torch(with_step):
         for t in range(K):
             mu = pi(obs)
             v = vf(obs).squeeze(-1)
@@ -560,11 +598,20 @@ def rollout_leg(device, precision, act, E, K=64, reps=8, store_policy=2):
                 sim.step(act_buf)
             buf_rew[t].copy_(sim.reward)
             buf_done[t].copy_(torch.logical_or(sim.terminated, sim.truncated))
-    out = {}
-    with torch.no_grad():
+
+    def seq_fused(with_step):
+        for t in range(K):
+            prev = (sim.reward, sim.terminated, sim.truncated, tobs) if t else None
+            kern.step(obs, act_buf.view(E, A), buf_obs[t], buf_act[t], buf_logp[t], buf_val[t], prev=prev,
+                      buf_rew=buf_rew[t - 1] if t else None, buf_done=buf_done[t - 1] if t else None)
+            if with_step:
+                sim.step(act_buf)
+
+    def measure(seq):
+        res = {}
         side = torch.cuda.Stream(device)
         side.wait_stream(torch.cuda.current_stream(device))
-        with torch.cuda.stream(side):             # warm the MLP's library kernels before capture
+        with torch.cuda.stream(side):             # warm the library kernels before capture
             seq(False)
         torch.cuda.current_stream(device).wait_stream(side)
         for name, with_step in (("policy_only", False), ("rollout", True)):
@@ -573,13 +620,19 @@ def rollout_leg(device, precision, act, E, K=64, reps=8, store_policy=2):
                 seq(with_step)
             g.replay()
             g.replay()
-            us = _event_region_us(device, g.replay, K, min_launches=K * reps)
-            out[name + "_us_per_step"] = us
+            res[name + "_us_per_step"] = _event_region_us(device, g.replay, K, min_launches=K * reps)
             del g
-    out["step_in_rollout_us"] = out["rollout_us_per_step"] - out["policy_only_us_per_step"]
+        res["step_in_rollout_us"] = res["rollout_us_per_step"] - res["policy_only_us_per_step"]
+        return res
+
+    with torch.no_grad():
+        out = measure(seq_fused)
+        out["torch_policy"] = measure(seq_torch)
     out.update({"n_envs": E, "steps_per_graph": K, "store_policy": store_policy or "library default",
-                "what": "one hipGraph of K x (actor + critic 64-64 tanh MLP forward, Normal sample, clamp, gpd_step, "
-                        "rollout-buffer copies) vs the same without gpd_step; step_in_rollout = the difference"})
+                "what": "one hipGraph of K x (fused policy kernel: actor + critic 64-64 tanh MLP forward, Normal "
+                        "sample, clip, rollout-buffer rows, previous step's bootstrap; gpd_step) vs the same without "
+                        "gpd_step; step_in_rollout = the difference; torch_policy = the policy as torch library "
+                        "calls"})
     sim.close()
     torch.cuda.synchronize(device)
     return out
@@ -745,10 +798,22 @@ def main():
 def run(args):
     # the JSON line is the only thing this process writes to stdout: native libraries write to fd 1
     # directly (RCCL prints its version banner when it creates a communicator), so fd 1 points at
-    # stderr until the line is printed
+    # stderr until the line is printed; restored whatever happens
     sys.stdout.flush()
     json_fd = os.dup(1)
     os.dup2(2, 1)
+    try:
+        result = _run(args)
+    finally:
+        sys.stdout.flush()
+        os.dup2(json_fd, 1)
+        os.close(json_fd)
+    if result is not None:
+        print(json.dumps(result), flush=True)
+
+
+def _run(args):
+    """One rank's bench; rank 0 returns the result dict (None elsewhere)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -868,35 +933,47 @@ def run(args):
         del sp
     if world > 1 or (rank == 0 and not args.no_handoff):
         # config 5: the learner hand-off (shard.LearnerHandoff): rank 0 scatters the global action
-        # batch, every rank steps its shard, the output-pack prefixes (obs, reward, terminated,
-        # truncated) go to the learner ("gather") or to every rank ("all_gather"), then the finished
-        # envs' terminal rows (their 12 state columns).  One GPU: a one-rank RCCL group with the
-        # collectives forced, so the same calls run as on a node
+        # batch, every rank steps its shard and packs its record (obs, reward, terminated,
+        # truncated, the finished envs' 12 state columns), ONE collective brings the records to the
+        # learner ("gather") or to every rank ("all_gather"), one kernel unpacks them.  One GPU: a
+        # one-rank RCCL group with the collectives forced, so the same calls run as on a node.  An
+        # optional leg: a failure is recorded, never the end of the run
         one_rank = world == 1
-        if one_rank and args.dist_backend == "nccl" and not torch.distributed.is_initialized():
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ["MASTER_PORT"] = str(_free_port())
-            torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=device)
-        if torch.distributed.is_initialized():
-            gpool = make_pool(E * world, A, device, seed=11, pool=8) if rank == 0 else None
-            G = max(30, args.steps // 3)
-            coll = "RCCL" if args.dist_backend == "nccl" else "gloo (rehearsal, through host memory)"
-            legs = {}
-            for hmode in ("gather", "all_gather"):
-                for cap in (None, max(1, E // 8)):
-                    legs[f"{hmode}_cap{'shard' if cap is None else cap}"] = handoff_leg(
-                        sim, E * world, hmode, cap, gpool, G, rank, device, force=one_rank)
-            result["handoff"] = {
-                "mode": f"learner hand-off per step ({coll}{', one rank, collectives forced' if one_rank else ''}): "
-                        "scatter of actions from rank 0, eager shard step, gather / all_gather_into_tensor of the "
-                        "output-pack prefixes with the terminal rows' 12 state columns per drone (the history columns "
-                        "are the auto-reset obs's): capshard = every env's columns in the prefix's own record (one "
-                        "collective, no host sync); a smaller terminal_capacity = the finished envs' columns "
-                        "compacted into a block of that many rows per rank, exchanged after the prefix, an all-reduce "
-                        "of the largest finished count (one host sync) and, when it overflows, a second exchange of "
-                        "exactly the missing rows",
-                "step_only_ms": 1000.0 * eager_wall / args.steps, "legs": legs}
-            if one_rank:
+        created = False
+        try:
+            if one_rank and args.dist_backend == "nccl" and not torch.distributed.is_initialized():
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ["MASTER_PORT"] = str(_free_port())
+                torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=device)
+                created = True
+            if torch.distributed.is_initialized():
+                gpool = make_pool(E * world, A, device, seed=11, pool=8) if rank == 0 else None
+                G = max(30, args.steps // 3)
+                coll = "RCCL" if args.dist_backend == "nccl" else "gloo (rehearsal, through host memory)"
+                legs = {hmode: handoff_leg(sim, E * world, hmode, None, gpool, G, rank, device, force=one_rank)
+                        for hmode in ("gather", "all_gather")}
+                cap = max(1, E // 8)
+                sync_legs = {f"{hmode}_cap{cap}": handoff_leg(sim, E * world, hmode, cap, gpool, G, rank, device,
+                                                              force=one_rank)
+                             for hmode in ("gather", "all_gather")}
+                result["handoff"] = {
+                    "mode": f"learner hand-off per step ({coll}{', one rank, collectives forced' if one_rank else ''}): "
+                            "action all_to_all_single from rank 0, shard step, pack kernel (the finished envs' 12 "
+                            "state columns into the record), ONE collective of the records (gather = "
+                            "all_to_all_single to the learner, all_gather = all_gather_into_tensor), unpack kernel; "
+                            "ms_per_step = step() replaying the captured one-step hipGraph, eager_ms_per_step = the "
+                            "same calls without the graph, graph32_us_per_step = 32 hand-off steps in one graph "
+                            "(HIP events: the device-side cost)",
+                    "step_only_ms": 1000.0 * eager_wall / args.steps, "legs": legs,
+                    "synchronising_legs": sync_legs,
+                    "synchronising_legs_note": f"terminal_capacity {cap} < shard: the finished envs' columns compacted "
+                                               "into a fixed block, the largest finished count read ON THE HOST every "
+                                               "step (one synchronisation; not capturable), a second exchange on "
+                                               "overflow"}
+        except Exception as exc:
+            result["handoff"] = {"error": f"{type(exc).__name__}: {exc}"}
+        finally:
+            if created:
                 torch.distributed.destroy_process_group()
 
     if rank == 0 and world == 1 and not args.no_latency_model:
@@ -958,13 +1035,10 @@ def run(args):
         except Exception as exc:
             result["parity"] = {"error": str(exc)}
 
-    if rank == 0:
-        sys.stdout.flush()
-        os.dup2(json_fd, 1)
-        print(json.dumps(result), flush=True)
     sim.close()
     if world > 1:
         torch.distributed.destroy_process_group()
+    return result if rank == 0 else None
 
 
 if __name__ == "__main__":

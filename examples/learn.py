@@ -140,8 +140,13 @@ def make_env(multiagent, n_envs, act, physics, device, seed=0, distributed=False
         kw["num_drones"] = DEFAULT_AGENTS
     # store policy 2 (write-through rows): between the policy's kernels the step measured 6.12 vs
     # 6.40 us (bench.py rollout leg, profiles/r4/rollout_policy/); the back-to-back default is 3
+    extra = {}
+    if distributed:
+        import torch.distributed as dist
+        # RCCL: the hand-off (scatter, shard step, pack, gather, unpack) replays one hipGraph per step
+        extra["graph"] = dist.is_initialized() and dist.get_backend() == "nccl"
     return make_vec_env(env_cls, env_kwargs=kw, n_envs=n_envs, seed=seed, output="torch", device=device,
-                        distributed=distributed, tuning={"store_policy": 2})
+                        distributed=distributed, tuning={"store_policy": 2}, **extra)
 
 
 class GraphedMinibatch:
@@ -205,17 +210,61 @@ class GraphedMinibatch:
         self.graph.replay()
 
 
+class FusedRollout:
+    """The rollout on the HIP path: per env.step ONE fused policy kernel (actor + critic forward,
+    Normal sample, clip, the buffer rows, and the previous step's time-limit bootstrap;
+    ``policy.MlpPolicyKernel``) and ONE ``gpd_step``, the whole n_steps sequence captured in one
+    hipGraph and replayed every PPO iteration (the parameters are read in place, so the optimizer's
+    in-place updates reach the graph); then the last value and GAE (``gpd_policy_gae``, bit-identical
+    to the torch loop of ``train``).  The same quantities as the eager loop, drawn from a Philox
+    stream instead of torch's generator."""
+
+    def __init__(self, policy, sim, n_steps, gamma, gae_lambda, seed, bufs):
+        from gym_pybullet_drones_routing_amd.policy import MlpPolicyKernel
+        self.k = MlpPolicyKernel(policy, seed=seed)
+        self.sim, self.T, self.gamma, self.lam = sim, n_steps, gamma, gae_lambda
+        E = sim.n_envs
+        n_obs = sim.drones_per_env * sim.obs_width
+        self.obs = sim.obs.view(E, n_obs)                 # sim-owned, rewritten in place by every step
+        self.tobs = sim.terminal_obs.view(E, n_obs)
+        self.act = torch.zeros((E, sim.drones_per_env, sim.act_width), device=sim.device)
+        self.b = bufs
+        self.last_v = torch.zeros(E, device=sim.device)
+        self.graph = None
+
+    def _seq(self):
+        b, k, sim = self.b, self.k, self.sim
+        for t in range(self.T):
+            prev = (sim.reward, sim.terminated, sim.truncated, self.tobs) if t else None
+            k.step(self.obs, self.act.view(self.obs.shape[0], -1), b["obs"][t], b["act"][t], b["logp"][t],
+                   b["val"][t], prev=prev, gamma=self.gamma, buf_rew=b["rew"][t - 1] if t else None,
+                   buf_done=b["done"][t - 1] if t else None)
+            sim.step(self.act, terminal_obs=True)
+        k.step(self.obs, buf_val=self.last_v, prev=(sim.reward, sim.terminated, sim.truncated, self.tobs),
+               gamma=self.gamma, buf_rew=b["rew"][self.T - 1], buf_done=b["done"][self.T - 1])
+        k.gae(b["rew"], b["val"], b["done"], self.last_v, self.gamma, self.lam, b["adv"], b["ret"])
+
+    def run(self):
+        if self.graph is None:
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._seq()
+        self.graph.replay()
+
+
 def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), lr=3e-4, epochs=10,
           minibatch=16384, gamma=0.99, gae_lambda=0.95, clip=0.2, vf_coef=0.5, max_grad_norm=0.5,
           eval_every=1, seed=0, device="cuda:0", act=DEFAULT_ACT, target_reward=None, max_seconds=None,
-          log=print, physics=Physics.PYB, env=None, world=1, rank=0, graph=False):
+          log=print, physics=Physics.PYB, env=None, world=1, rank=0, graph=False, fused=False):
     """PPO on the batched env.  ``env``: an already built torch-output VecEnv (e.g. the
     multi-GPU ``ShardedAviaryVecEnv``); by default one ``AviaryVecEnv`` on ``device``.
     world > 1: per-rank learners under torch.distributed — this rank trains on its own
     ``n_envs`` envs with ``minibatch / world`` samples per minibatch, gradients are averaged over
     the ranks (sync_grads), rank 0 evaluates and decides when every rank stops; ``timesteps``
     and the history count all ranks' samples.  ``graph``: the minibatch steps as one captured
-    hipGraph (``GraphedMinibatch``; world == 1 and full minibatches only)."""
+    hipGraph (``GraphedMinibatch``; world == 1 and full minibatches only).  ``fused``: the rollout
+    as ``FusedRollout`` (one policy kernel + one gpd_step per env.step, one hipGraph per rollout;
+    a single-GPU ``AviaryVecEnv``)."""
     import torch.distributed as dist
     torch.manual_seed(seed)
     physics = Physics(physics)
@@ -246,36 +295,49 @@ def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), l
     buf_rew = torch.zeros((n_steps, E), device=device)
     buf_done = torch.zeros((n_steps, E), device=device)
     obs = env.reset().reshape(E, -1)
+    fr = None
+    if fused:
+        if not hasattr(env, "sim") or getattr(env, "handoff", None) is not None:
+            raise ValueError("fused=True needs a single-GPU AviaryVecEnv")
+        adv_buf, ret_buf = torch.zeros((n_steps, E), device=device), torch.zeros((n_steps, E), device=device)
+        fr = FusedRollout(policy, env.sim, n_steps, gamma, gae_lambda, seed,
+                          {"obs": buf_obs, "act": buf_act, "logp": buf_logp, "val": buf_val, "rew": buf_rew,
+                           "done": buf_done, "adv": adv_buf, "ret": ret_buf})
     history = []
     t0 = time.time()
     timesteps, it = 0, 0
     best = -1e9
     while timesteps < total_timesteps:
         t_roll = time.time()
-        with torch.no_grad():
-            for t in range(n_steps):
-                d = policy.dist(obs)
-                a = d.sample()
-                v = policy.value(obs)
-                o2, r, done, info = env.step(a.clamp(-1, 1))            # SB3 clips to the Box
-                o2 = o2.reshape(E, -1)
-                trunc = info["TimeLimit.truncated"]
-                if bool(trunc.any()):                                 # bootstrap time limits
-                    tv = policy.value(info["terminal_observation"].reshape(E, -1))
-                    r = r + gamma * tv * trunc.float()
-                buf_obs[t], buf_act[t], buf_logp[t], buf_val[t] = obs, a, d.log_prob(a).sum(-1), v
-                buf_rew[t], buf_done[t] = r, done.float()
-                obs = o2
-            last_v = policy.value(obs)
-            adv = torch.zeros_like(buf_rew)
-            g = torch.zeros(E, device=device)
-            for t in reversed(range(n_steps)):
-                nv = last_v if t == n_steps - 1 else buf_val[t + 1]
-                nonterm = 1.0 - buf_done[t]
-                delta = buf_rew[t] + gamma * nv * nonterm - buf_val[t]
-                g = delta + gamma * gae_lambda * nonterm * g
-                adv[t] = g
-            ret = adv + buf_val
+        if fr is not None:
+            with torch.no_grad():
+                fr.run()
+            adv, ret = fr.b["adv"], fr.b["ret"]
+        else:
+            with torch.no_grad():
+                for t in range(n_steps):
+                    d = policy.dist(obs)
+                    a = d.sample()
+                    v = policy.value(obs)
+                    o2, r, done, info = env.step(a.clamp(-1, 1))            # SB3 clips to the Box
+                    o2 = o2.reshape(E, -1)
+                    trunc = info["TimeLimit.truncated"]
+                    if bool(trunc.any()):                                 # bootstrap time limits
+                        tv = policy.value(info["terminal_observation"].reshape(E, -1))
+                        r = r + gamma * tv * trunc.float()
+                    buf_obs[t], buf_act[t], buf_logp[t], buf_val[t] = obs, a, d.log_prob(a).sum(-1), v
+                    buf_rew[t], buf_done[t] = r, done.float()
+                    obs = o2
+                last_v = policy.value(obs)
+                adv = torch.zeros_like(buf_rew)
+                g = torch.zeros(E, device=device)
+                for t in reversed(range(n_steps)):
+                    nv = last_v if t == n_steps - 1 else buf_val[t + 1]
+                    nonterm = 1.0 - buf_done[t]
+                    delta = buf_rew[t] + gamma * nv * nonterm - buf_val[t]
+                    g = delta + gamma * gae_lambda * nonterm * g
+                    adv[t] = g
+                ret = adv + buf_val
         t_upd = time.time()
         N = n_steps * E
         b_obs, b_act, b_logp = buf_obs.reshape(N, -1), buf_act.reshape(N, -1), buf_logp.reshape(N)
@@ -348,6 +410,10 @@ def parse_args(argv=None):
                    help="replay each PPO minibatch step as one captured hipGraph (faster update; same "
                         "arithmetic up to rounding, so a different training trajectory than the default "
                         "eager loop, which reproduces the recorded runs step for step)")
+    p.add_argument("--rollout", default="fused", choices=["fused", "eager"],
+                   help="fused (one GPU): one policy kernel + one gpd_step per env.step, the rollout replayed as "
+                        "one hipGraph (FusedRollout); eager: the torch policy step by step (the loop that "
+                        "reproduces the recorded round-4/5 runs)")
     p.add_argument("--learner", default="rank0", choices=["rank0", "per-rank"],
                    help="rank0: one learner on the gathered batch (ShardedAviaryVecEnv); per-rank: a learner "
                         "per GPU on its own env shard, gradients all-reduced")
@@ -394,10 +460,12 @@ def run(a):
             env.serve()
             dist.destroy_process_group()
             return
+    fused = a.rollout == "fused" and world == 1
     policy, hist, best, target = train(multiagent=multi, n_envs=a.n_envs, total_timesteps=int(a.total_timesteps),
                                        max_seconds=a.max_seconds, physics=Physics(a.physics), device=device, env=env,
-                                       graph=a.graph, seed=a.seed)
+                                       graph=a.graph, seed=a.seed, fused=fused)
     out = {"multiagent": multi, "physics": a.physics, "n_envs": a.n_envs, "gpus": world, "target_reward": target,
+           "rollout": "fused" if fused else "eager",
            "best_eval_return": best, "reached": best >= target, "history": hist}
     print(json.dumps({k: v for k, v in out.items() if k != "history"}), flush=True)
     if a.output:

@@ -11,7 +11,7 @@ PKG_DIR = pathlib.Path(__file__).resolve().parent
 CSRC = PKG_DIR / "csrc"
 INCLUDE = PKG_DIR.parent / "include"
 LIB_PATH = PKG_DIR / "libgpd.so"
-SOURCES = [CSRC / "gpd.hip", CSRC / "gpd_kernels.h", CSRC / "gpd_device.h", CSRC / "gpd_ctrl.h", INCLUDE / "gpd.h"]
+SOURCES = [CSRC / "gpd.hip", CSRC / "gpd_kernels.h", CSRC / "gpd_device.h", CSRC / "gpd_ctrl.h", CSRC / "gpd_handoff.h", INCLUDE / "gpd.h"]
 ARCH = os.environ.get("GPD_OFFLOAD_ARCH", "gfx950")
 
 
@@ -56,5 +56,29 @@ def build(force=False, verbose=False, stamps=False, variant=None, defines=()):
     return out
 
 
+POLICY_LIB = PKG_DIR / "libgpd_policy.so"
+POLICY_SOURCES = [CSRC / "gpd_policy.hip", INCLUDE / "gpd_policy.h"]
+
+
+def build_policy(force=False, verbose=False):
+    """Compile csrc/gpd_policy.hip (the fused rollout policy, include/gpd_policy.h) into
+    libgpd_policy.so for gfx950.  -ffp-contract=off: the parts written "as torch computes them"
+    (Normal sample and log-density, the time-limit bootstrap, GAE) round every operation."""
+    if not force and POLICY_LIB.exists() and all(src.stat().st_mtime <= POLICY_LIB.stat().st_mtime
+                                                 for src in POLICY_SOURCES):
+        return POLICY_LIB
+    tmp = POLICY_LIB.with_suffix(".so.tmp")
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-mcode-object-version=5", "-O3", "-std=c++17", "-ffp-contract=off",
+           "-fPIC", "-shared", "-Wall", f"-I{INCLUDE}", "-o", str(tmp), str(CSRC / "gpd_policy.hip")]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + " ".join(cmd) + "\n" + res.stdout + res.stderr)
+    if verbose and (res.stdout or res.stderr):
+        print(res.stdout + res.stderr)
+    os.replace(tmp, POLICY_LIB)
+    return POLICY_LIB
+
+
 if __name__ == "__main__":
     print(build(force=True, verbose=True))
+    print(build_policy(force=True, verbose=True))

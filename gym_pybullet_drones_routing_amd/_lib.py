@@ -22,7 +22,7 @@ GPD_EUNSUPPORTED = -4
 
 GPD_MODEL_CF2X, GPD_MODEL_CF2P, GPD_MODEL_RACE = 0, 1, 2
 GPD_ACT_RPM, GPD_ACT_ONE_D_RPM, GPD_ACT_PID, GPD_ACT_VEL, GPD_ACT_ONE_D_PID = 0, 1, 2, 3, 4
-GPD_ABI_VERSION = 5
+GPD_ABI_VERSION = 6
 CTRL_COMPS = 9  # integral_pos_e(3) integral_rpy_e(3) last_rpy(3)
 GPD_TASK_NONE, GPD_TASK_HOVER, GPD_TASK_MULTIHOVER = 0, 1, 2
 GPD_F_GND, GPD_F_DRAG, GPD_F_DW, GPD_F_GEOM_WRENCH, GPD_F_BULLET, GPD_F_NO_PLANE = 1, 2, 4, 8, 16, 32
@@ -35,7 +35,7 @@ EXPORTED = ("gpd_abi_version", "gpd_last_error", "gpd_default_params", "gpd_crea
             "gpd_get_raw_state", "gpd_set_raw_state", "gpd_get_step_counters",
             "gpd_set_step_counters", "gpd_state_bytes", "gpd_save_state", "gpd_load_state",
             "gpd_default_pid_params", "gpd_set_pid_params", "gpd_get_ctrl_state", "gpd_set_ctrl_state",
-            "gpd_nonfinite")
+            "gpd_nonfinite", "gpd_pack_layout_of", "gpd_handoff_pack", "gpd_handoff_unpack")
 
 
 class GpdLibraryError(RuntimeError):
@@ -71,6 +71,13 @@ class Config(ctypes.Structure):
                 ("init_xyzs_host", ctypes.POINTER(ctypes.c_double)),
                 ("init_rpys_host", ctypes.POINTER(ctypes.c_double)),
                 ("drones_per_block", ctypes.c_int), ("step_waves", ctypes.c_int), ("store_policy", ctypes.c_int)]
+
+
+class PackLayout(ctypes.Structure):
+    """gpd_pack_layout: byte offsets of a shard's output pack (include/gpd.h)."""
+    _fields_ = [(n, ctypes.c_int) for n in ("n_envs", "drones_per_env", "obs_width", "state_cols")] + \
+        [(n, ctypes.c_longlong) for n in ("obs", "reward", "terminated", "truncated", "terminal_state",
+                                          "terminal_obs", "prefix", "prefix_aligned", "record", "total")]
 
 
 class Constants(ctypes.Structure):
@@ -121,6 +128,9 @@ def load():
         "gpd_get_ctrl_state": (ci, [vp, vp, vp]),
         "gpd_set_ctrl_state": (ci, [vp, vp, vp]),
         "gpd_nonfinite": (ci, [vp, vp, vp]),
+        "gpd_pack_layout_of": (ci, [i, i, i, ctypes.POINTER(PackLayout)]),
+        "gpd_handoff_pack": (ci, [vp, ctypes.POINTER(PackLayout), vp]),
+        "gpd_handoff_unpack": (ci, [vp, i, ctypes.c_longlong, ctypes.POINTER(PackLayout), vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name) and os.environ.get("GPD_ALLOW_ABI_MISMATCH"):

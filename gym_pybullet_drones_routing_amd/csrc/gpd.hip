@@ -17,6 +17,7 @@
 
 #include "../../include/gpd.h"
 #include "gpd_kernels.h"
+#include "gpd_handoff.h"
 
 using namespace gpd;
 
@@ -1022,6 +1023,107 @@ int gpd_load_state(gpd_sim* sim, const void* blob_host, void* stream) {
   }
   if (sim->wt & 4) HIP_TRY(hipMemsetAsync(sim->d_ctr + sim->E, 0, sizeof(int2), st));   // saved settled
   HIP_TRY(hipStreamSynchronize(st));
+  return GPD_OK;
+}
+
+// ---- config-5 learner hand-off (gpd_handoff.h; SURVEY §8(e), caller examples/learn.py:52-94)
+namespace {
+constexpr long long kPackAlign = 256;
+inline long long align_up(long long n) { return (n + kPackAlign - 1) / kPackAlign * kPackAlign; }
+
+int check_layout(const gpd_pack_layout* L, const char* fn) {
+  if (!L) return fail(GPD_EINVAL, std::string(fn) + ": NULL layout");
+  if (L->n_envs < 1 || L->drones_per_env < 1 || L->obs_width < kHandoffStateCols ||
+      L->state_cols != kHandoffStateCols)
+    return fail(GPD_EINVAL, std::string(fn) + ": layout not made by gpd_pack_layout_of");
+  gpd_pack_layout ref;
+  gpd_pack_layout_of(L->n_envs, L->drones_per_env, L->obs_width, &ref);
+  if (std::memcmp(&ref, L, sizeof(ref)) != 0)
+    return fail(GPD_EINVAL, std::string(fn) + ": layout offsets differ from gpd_pack_layout_of's");
+  return GPD_OK;
+}
+
+HandoffView handoff_view(const gpd_pack_layout* L, long long stride, int n_ranks) {
+  HandoffView v;
+  v.obs = L->obs; v.reward = L->reward; v.term = L->terminated; v.trunc = L->truncated;
+  v.tstate = L->terminal_state; v.tobs = L->terminal_obs; v.stride = stride;
+  v.E = L->n_envs; v.D = L->drones_per_env; v.W = L->obs_width; v.G = n_ranks;
+  return v;
+}
+}  // namespace
+
+int gpd_pack_layout_of(int n_envs, int drones_per_env, int obs_width, gpd_pack_layout* out) {
+  if (!out || n_envs < 1 || drones_per_env < 1 || obs_width < kHandoffStateCols)
+    return fail(GPD_EINVAL, "gpd_pack_layout_of: invalid argument");
+  const long long E = n_envs, D = drones_per_env, W = obs_width;
+  gpd_pack_layout L;
+  std::memset(&L, 0, sizeof(L));
+  L.n_envs = n_envs; L.drones_per_env = drones_per_env; L.obs_width = obs_width;
+  L.state_cols = kHandoffStateCols;
+  long long off = 0;
+  L.obs = off;            off += align_up(E * D * W * 4);
+  L.reward = off;         off += align_up(E * 4);
+  L.terminated = off;     off += align_up(E);
+  L.truncated = off;
+  L.prefix = off + E;
+  L.prefix_aligned = align_up(L.prefix);
+  off += align_up(E);
+  L.terminal_state = off; off += align_up(E * D * kHandoffStateCols * 4);
+  L.record = off;
+  L.terminal_obs = off;   off += align_up(E * D * W * 4);
+  L.total = off;
+  *out = L;
+  return GPD_OK;
+}
+
+int gpd_handoff_pack(uint8_t* pack, const gpd_pack_layout* layout, void* stream) {
+  const int rc = check_layout(layout, "gpd_handoff_pack");
+  if (rc != GPD_OK) return rc;
+  if (!pack) return fail(GPD_EINVAL, "gpd_handoff_pack: NULL pack");
+  const HandoffView v = handoff_view(layout, layout->record, 1);
+  const long long n = (long long)v.E * v.D * kHandoffStateCols;
+  if (n >= (1ll << 31)) return fail(GPD_EINVAL, "gpd_handoff_pack: shard too large");
+  hipLaunchKernelGGL(handoff_pack_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, pack, v);
+  HIP_TRY(hipGetLastError());
+  return GPD_OK;
+}
+
+int gpd_handoff_unpack(const uint8_t* gathered, int n_ranks, long long stride, const gpd_pack_layout* layout,
+                       float* obs, float* reward, uint8_t* terminated, uint8_t* truncated, float* terminal_obs,
+                       void* stream) {
+  const int rc = check_layout(layout, "gpd_handoff_unpack");
+  if (rc != GPD_OK) return rc;
+  if (!gathered || !obs || !reward || !terminated || !truncated || n_ranks < 1)
+    return fail(GPD_EINVAL, "gpd_handoff_unpack: NULL output or n_ranks < 1");
+  if (stride != layout->prefix_aligned && stride != layout->record)
+    return fail(GPD_EINVAL, "gpd_handoff_unpack: stride must be the layout's prefix_aligned or record");
+  if (terminal_obs && stride != layout->record)
+    return fail(GPD_EINVAL, "gpd_handoff_unpack: terminal rows need whole records (stride = record)");
+  const HandoffView v = handoff_view(layout, stride, n_ranks);
+  const long long rows = (long long)v.E * v.D;
+  if (rows * v.W * n_ranks >= (1ll << 31))
+    return fail(GPD_EINVAL, "gpd_handoff_unpack: gathered batch too large");
+  hipStream_t st = (hipStream_t)stream;
+  const bool vec4 = v.W % 4 == 0 && aligned16(obs) && (!terminal_obs || aligned16(terminal_obs)) && aligned16(gathered);
+  const long long nvec = rows * v.W / (vec4 ? 4 : 1) * n_ranks;
+  const long long nthr = std::max(nvec, (long long)v.E * n_ranks);
+  const dim3 grid(grid_for(nthr, 256)), block(256);
+  if (vec4) {
+    if (terminal_obs)
+      hipLaunchKernelGGL((handoff_unpack_kernel<4, true>), grid, block, 0, st, gathered, v, obs, reward, terminated,
+                         truncated, terminal_obs);
+    else
+      hipLaunchKernelGGL((handoff_unpack_kernel<4, false>), grid, block, 0, st, gathered, v, obs, reward, terminated,
+                         truncated, terminal_obs);
+  } else {
+    if (terminal_obs)
+      hipLaunchKernelGGL((handoff_unpack_kernel<1, true>), grid, block, 0, st, gathered, v, obs, reward, terminated,
+                         truncated, terminal_obs);
+    else
+      hipLaunchKernelGGL((handoff_unpack_kernel<1, false>), grid, block, 0, st, gathered, v, obs, reward, terminated,
+                         truncated, terminal_obs);
+  }
+  HIP_TRY(hipGetLastError());
   return GPD_OK;
 }
 

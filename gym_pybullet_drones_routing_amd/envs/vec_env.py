@@ -148,10 +148,16 @@ class ShardedAviaryVecEnv:
     SB3's ``terminal_observation`` / ``TimeLimit.truncated``.  Each call broadcasts a one-word
     command, then ``shard.LearnerHandoff`` scatters the actions and gathers the shards' output
     packs (and the finished envs' terminal rows) to rank 0.  Every other rank runs ``serve()``, which answers commands until ``close()``.
+
+    Mode "gather" (one learner): on a fully connected xGMI node every rank's 1.4 MB record
+    reaches rank 0 over its own link (~9 us at ~153 GB/s), where a ring all-gather would pass
+    G-1 records through each link and land them on every rank.  ``graph=True``
+    (RCCL only): from the second step on, every step replays the hand-off's captured hipGraph
+    (``LearnerHandoff.capture``), on every rank at the same step.
     """
     STEP, RESET, STOP = 0, 1, 2
 
-    def __init__(self, num_envs, **kw):
+    def __init__(self, num_envs, graph=False, **kw):
         import torch.distributed as dist
 
         from ..shard import LearnerHandoff, env_shard
@@ -170,9 +176,16 @@ class ShardedAviaryVecEnv:
         self.output = "torch"
         gloo = dist.is_initialized() and dist.get_backend() == "gloo"
         self._cmd = torch.zeros((1,), dtype=torch.int32, device="cpu" if gloo else self.sim.device)
-        self._actions = torch.zeros((num_envs, self.num_drones, self.sim.act_width), dtype=torch.float32,
-                                    device=self.sim.device)
+        self._actions = self.handoff.global_actions if self.rank == 0 else None
+        self._graph = bool(graph) and not gloo
+        self._steps = 0
         self._open = True
+
+    def _handoff_step(self, actions):
+        if self._graph and self._steps == 1:
+            self.handoff.capture()          # every rank, at its second step
+        self._steps += 1
+        return self.handoff.step(actions)
 
     def _send(self, cmd):
         if self.world > 1:
@@ -182,15 +195,18 @@ class ShardedAviaryVecEnv:
 
     def reset(self):
         self._send(self.RESET)
-        return self.handoff.reset()
+        return self.handoff.reset().clone()
 
     def step(self, actions):
         self._actions.copy_(torch.as_tensor(actions, dtype=torch.float32).reshape(self._actions.shape))
         self._send(self.STEP)
-        obs, rew, te, tr, tobs = self.handoff.step(self._actions)
+        obs, rew, te, tr, tobs = self._handoff_step(self._actions)
+        # the hand-off's buffers are rewritten by the next step: the VecEnv hands out copies (as
+        # AviaryVecEnv(output="torch") does)
         done = (te | tr).bool()
-        infos = {"terminal_observation": tobs, "TimeLimit.truncated": (tr.bool() & ~te.bool()), "done_mask": done}
-        return obs, rew, done, infos
+        infos = {"terminal_observation": tobs.clone(), "TimeLimit.truncated": (tr.bool() & ~te.bool()),
+                 "done_mask": done}
+        return obs.clone(), rew.clone(), done, infos
 
     def serve(self):
         """Non-learner ranks: step / reset this rank's shard on the learner's command."""
@@ -199,11 +215,12 @@ class ShardedAviaryVecEnv:
             dist.broadcast(self._cmd, src=0)
             cmd = int(self._cmd.item())
             if cmd == self.STOP:
+                self.handoff.close()
                 break
             if cmd == self.RESET:
                 self.handoff.reset()
             else:
-                self.handoff.step(None)
+                self._handoff_step(None)
         self.local.close()
         self._open = False
 
@@ -211,5 +228,6 @@ class ShardedAviaryVecEnv:
         if self._open:
             if self.rank == 0:
                 self._send(self.STOP)
+            self.handoff.close()
             self.local.close()
             self._open = False

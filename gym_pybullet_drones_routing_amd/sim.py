@@ -91,17 +91,26 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+STATE_COLS = 12   # KIN observation: pos, rpy, vel, ang_v (BaseRLAviary.py:313-316) before the history
+
+
 def pack_layout(n_envs, drones_per_env, obs_width, align=256):
-    """Byte layout of a sim's output pack: {field: (offset, nbytes)}, "total", and "prefix" = the
-    bytes up to the end of the truncated flags (the hand-off without terminal rows)."""
+    """Byte layout of a sim's output pack, ``gpd_pack_layout_of`` (include/gpd.h) restated:
+    {field: (offset, nbytes)} for obs | reward | terminated | truncated | terminal_state |
+    terminal_obs (each 256-B aligned), "prefix" = the end of the truncated flags,
+    "prefix_aligned" = that rounded up to 256, "record" = the end of terminal_state (one rank's
+    hand-off record, ``shard.LearnerHandoff``) and "total"."""
     E, D, W = n_envs, drones_per_env, obs_width
     out, off = {}, 0
     for name, nbytes in (("obs", E * D * W * 4), ("reward", E * 4), ("terminated", E), ("truncated", E),
-                         ("terminal_obs", E * D * W * 4)):
+                         ("terminal_state", E * D * STATE_COLS * 4), ("terminal_obs", E * D * W * 4)):
         out[name] = (off, nbytes)
         if name == "truncated":
             out["prefix"] = off + nbytes
+            out["prefix_aligned"] = -(-(off + nbytes) // align) * align
         off += -(-nbytes // align) * align
+        if name == "terminal_state":
+            out["record"] = off
     out["total"] = off
     return out
 

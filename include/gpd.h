@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define GPD_ABI_VERSION 5
+#define GPD_ABI_VERSION 6
 
 /* return codes */
 #define GPD_OK 0
@@ -226,6 +226,44 @@ int gpd_set_step_counters(gpd_sim* sim, const int32_t* in, void* stream);
 size_t gpd_state_bytes(const gpd_sim* sim);
 int gpd_save_state(gpd_sim* sim, void* blob_host, void* stream);
 int gpd_load_state(gpd_sim* sim, const void* blob_host, void* stream);
+
+/* ---- Config-5 learner hand-off.  Replaces the reference's stepping loop
+ * examples/learn.py:52-94, where SB3 steps one process's VecEnv and hands obs / reward / done /
+ * infos["terminal_observation"] to PPO.  Here each rank (one per GPU) steps its env shard into
+ * one output pack; one collective moves every rank's RECORD = [obs | reward | terminated |
+ * truncated | terminal_state] to the learner; gpd_handoff_unpack rebuilds the global batch.
+ *
+ * Pack layout of a shard of E envs x D drones, obs rows of W floats (every field 256-B aligned,
+ * offsets in bytes):  obs [E][D][W] f32 | reward [E] f32 | terminated [E] u8 | truncated [E] u8 |
+ * terminal_state [E][D][12] f32 | terminal_obs [E][D][W] f32.  gpd_step writes obs, reward, the
+ * flags and terminal_obs into their fields; gpd_handoff_pack fills terminal_state. */
+typedef struct gpd_pack_layout {
+  int n_envs, drones_per_env, obs_width, state_cols; /* state_cols = 12 (pos, rpy, vel, ang_v) */
+  long long obs, reward, terminated, truncated, terminal_state, terminal_obs;
+  long long prefix;          /* end of the truncated flags */
+  long long prefix_aligned;  /* prefix rounded up to 256: a record without terminal rows */
+  long long record;          /* end of terminal_state (256-aligned): one rank's hand-off record */
+  long long total;           /* bytes of the whole pack */
+} gpd_pack_layout;
+
+int gpd_pack_layout_of(int n_envs, int drones_per_env, int obs_width, gpd_pack_layout* out);
+
+/* Before the exchange: for every env whose terminated or truncated flag is set in `pack`, copy
+ * columns 0..11 of its terminal_obs rows into terminal_state (other envs' entries are left
+ * as they are: the unpack never reads them).  The reference never clears the action buffer on
+ * reset (BaseRLAviary.py has no reset override), so a finished env's terminal row and its
+ * auto-reset row share the history columns: the receivers rebuild the whole row. */
+int gpd_handoff_pack(uint8_t* pack, const gpd_pack_layout* layout, void* stream);
+
+/* After the exchange: `gathered` holds n_ranks records, `stride` bytes apart (layout->record, or
+ * layout->prefix_aligned when no terminal rows travelled).  Writes the global batch in rank
+ * order: obs [n_ranks*E][D][W], reward [n_ranks*E], terminated / truncated [n_ranks*E] and, when
+ * terminal_obs != NULL (needs stride = record), the terminal rows [n_ranks*E][D][W]: for a
+ * finished env its 12 state columns followed by the gathered obs row's history columns, zero for
+ * every other env (infos[i]["terminal_observation"] of SB3's DummyVecEnv). */
+int gpd_handoff_unpack(const uint8_t* gathered, int n_ranks, long long stride, const gpd_pack_layout* layout,
+                       float* obs, float* reward, uint8_t* terminated, uint8_t* truncated, float* terminal_obs,
+                       void* stream);
 
 #ifdef __cplusplus
 }

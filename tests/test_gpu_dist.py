@@ -29,7 +29,8 @@ def _actions(E, T, D, A, seed):
     return acts
 
 
-def _worker(rank, world, port, kw, E, T, q, backend="gloo", mode="all_gather", ack=None, sync_check=False):
+def _worker(rank, world, port, kw, E, T, q, backend="gloo", mode="all_gather", ack=None, sync_check=False,
+            graph_at=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     extra = {"device_id": torch.device("cuda:0")} if backend == "nccl" else {}
@@ -49,15 +50,18 @@ def _worker(rank, world, port, kw, E, T, q, backend="gloo", mode="all_gather", a
         outs = [o0.cpu().numpy() if rank == 0 else None]
         keep = []
         for t in range(T):
+            if graph_at is not None and t == graph_at:
+                h.capture()                               # every later step replays one hipGraph
             if sync_check and t == 2:
                 torch.cuda.synchronize()
                 torch.cuda.set_sync_debug_mode("error")   # steady state: no host synchronisation at all
             r = h.step(acts_dev[t] if rank == 0 else None)
             if rank == 0:
-                keep.append(r)
+                keep.append(tuple(x.clone() for x in r))  # the hand-off's buffers: the next step overwrites them
         torch.cuda.set_sync_debug_mode("default")
         for r in keep:
             outs.append(tuple(x.cpu().numpy() for x in r))
+        h.close()
         sim.close()
         if rank == 0:
             q.put(outs)
@@ -91,12 +95,12 @@ def _collect(q, procs, limit=150, ack=None):
     return outs
 
 
-def _run(kw, E, T, world, backend, mode, sync_check=False):
+def _run(kw, E, T, world, backend, mode, sync_check=False, graph_at=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ack = ctx.Event()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, kw, E, T, q, backend, mode, ack, sync_check))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kw, E, T, q, backend, mode, ack, sync_check, graph_at))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -138,15 +142,72 @@ def test_handoff_two_ranks_bit_identical_to_one_sim(kw, mode):
     _check_against_one_sim(outs, kw, E, T)
 
 
-@pytest.mark.parametrize("mode", ["all_gather", "gather"])
-def test_handoff_rccl_one_rank(mode):
+@pytest.mark.parametrize("mode,graph_at", [("all_gather", None), ("gather", None), ("all_gather", 5), ("gather", 5)],
+                         ids=["all_gather", "gather", "all_gather_graph", "gather_graph"])
+def test_handoff_rccl_one_rank(mode, graph_at):
     """The RCCL code path of the hand-off (backend "nccl" = RCCL on ROCm) on the one-GPU box:
-    a one-rank group with the collectives forced on, so that dist.scatter, the prefix
-    gather / all_gather_into_tensor and the terminal-row all-gather of uint8 / float32 device
-    tensors really execute on RCCL.  Bit-identical to one sim stepping the same envs.  Steady-state
-    steps run under torch.cuda.set_sync_debug_mode("error"): the hand-off never waits for the
-    device (fixed-size compacted terminal blocks, device-side indices)."""
+    a one-rank group with the collectives forced on, so that the action all_to_all_single, the
+    record gather (all_to_all_single) / all_gather_into_tensor of uint8 / float32 device tensors
+    and the pack / unpack kernels really execute on RCCL.  Bit-identical to one sim stepping the
+    same envs.  Steady-state steps run under torch.cuda.set_sync_debug_mode("error"): the
+    hand-off never waits for the device.  ``graph_at``: from that step on, every step replays ONE
+    captured hipGraph (scatter + step + pack + collective + unpack)."""
     kw = dict(task="hover")
     E, T = 64, 260
-    outs = _run(kw, E, T, 1, "nccl", mode, sync_check=True)
+    outs = _run(kw, E, T, 1, "nccl", mode, sync_check=True, graph_at=graph_at)
     _check_against_one_sim(outs, kw, E, T)
+
+
+@pytest.mark.parametrize("W,D", [(72, 1), (27, 2), (36, 3)])
+def test_handoff_pack_unpack_kernels_match_host_restatement(W, D):
+    """gpd_handoff_pack / gpd_handoff_unpack (csrc/gpd_handoff.h) against their torch
+    restatement (shard._pack_host / _unpack_host) on random packs of 3 ranks: float4 rows
+    (W % 4 == 0) and scalar rows, shards of 5 envs (unaligned field ends), random done flags."""
+    import ctypes
+    from gym_pybullet_drones_routing_amd import _lib
+    from gym_pybullet_drones_routing_amd.shard import _pack_host, _unpack_host
+    from gym_pybullet_drones_routing_amd.sim import pack_layout
+    lib = _lib.load()
+    G, E = 3, 5
+    L = pack_layout(E, D, W)
+    cl = _lib.PackLayout()
+    _lib.check("gpd_pack_layout_of", lib.gpd_pack_layout_of(E, D, W, ctypes.byref(cl)))
+    for k in ("prefix", "prefix_aligned", "record", "total"):
+        assert getattr(cl, k) == L[k]
+    for k in ("obs", "reward", "terminated", "truncated", "terminal_state", "terminal_obs"):
+        assert getattr(cl, k) == L[k][0]
+    g = torch.Generator().manual_seed(W)
+    packs = []
+    for r in range(G):
+        p = torch.randint(0, 256, (L["total"],), dtype=torch.uint8, generator=g)
+        for name in ("terminated", "truncated"):
+            off, n = L[name]
+            p[off:off + n] = (torch.rand(n, generator=g) < 0.4).to(torch.uint8)
+        packs.append(p)
+    # pack on the device vs the host restatement, rank by rank
+    ref_packs = [p.clone() for p in packs]
+    for p in ref_packs:
+        _pack_host(p, L, E, D, W)
+    dev_packs = [p.cuda() for p in packs]
+    for p in dev_packs:
+        _lib.check("gpd_handoff_pack", lib.gpd_handoff_pack(p.data_ptr(), ctypes.byref(cl), None))
+    for p, q in zip(dev_packs, ref_packs):
+        assert torch.equal(p.cpu(), q)
+    rec = L["record"]
+    gathered = torch.cat([q[:rec] for q in ref_packs])
+    outs_ref = (torch.empty((G * E, D, W)), torch.empty(G * E), torch.empty(G * E, dtype=torch.uint8),
+                torch.empty(G * E, dtype=torch.uint8), torch.empty((G * E, D, W)))
+    _unpack_host(gathered, G, rec, L, E, D, W, *outs_ref)
+    outs = [torch.full(tuple(o.shape), 7, dtype=o.dtype, device="cuda") for o in outs_ref]
+    gd = gathered.cuda()
+    _lib.check("gpd_handoff_unpack", lib.gpd_handoff_unpack(gd.data_ptr(), G, rec, ctypes.byref(cl),
+                                                             *[o.data_ptr() for o in outs], None))
+    torch.cuda.synchronize()
+    for o, r in zip(outs, outs_ref):
+        # bit patterns: random bytes hold NaNs, which compare unequal as floats
+        assert torch.equal(o.cpu().view(torch.uint8), r.view(torch.uint8))
+    # a stride that is neither record nor prefix_aligned, or terminal rows without records: rejected
+    assert lib.gpd_handoff_unpack(gd.data_ptr(), G, rec + 256, ctypes.byref(cl), *[o.data_ptr() for o in outs],
+                                  None) == _lib.GPD_EINVAL
+    assert lib.gpd_handoff_unpack(gd.data_ptr(), G, L["prefix_aligned"], ctypes.byref(cl),
+                                  *[o.data_ptr() for o in outs], None) == _lib.GPD_EINVAL

@@ -1,0 +1,192 @@
+"""The fused rollout policy (libgpd_policy.so, csrc/gpd_policy.hip) against the torch forward it
+replaces: examples/learn.py's ActorCritic (SB3 MlpPolicy: separate 64-64 tanh actor and critic,
+state-independent log-std; the reference's caller examples/learn.py:52-94).
+
+Tolerances: the MLP sums in a different order than torch's GEMMs, so mu and the value agree to
+f32 rounding (1e-5 relative / 2e-6 absolute here); the buffer copy, the clip of the sampled
+action and the reward / done rows of non-bootstrapped envs are bit-exact; GAE is bit-identical
+to learn.py's torch loop (every operation rounded as torch rounds it)."""
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples"))
+
+
+def _policy(n_obs, n_act, seed):
+    import learn
+    torch.manual_seed(seed)
+    pol = learn.ActorCritic(n_obs, n_act).cuda()
+    with torch.no_grad():             # non-trivial biases and log-std (learn.py initialises them to 0)
+        for p in pol.parameters():
+            if p.dim() == 1:
+                p.copy_(0.1 * torch.randn_like(p))
+    return pol
+
+
+def _rows(E, n, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return torch.randn((E, n), generator=g, device="cuda") * 0.7
+
+
+@pytest.mark.parametrize("n_obs,n_act,E", [(27, 1, 4096), (72, 4, 4099), (54, 2, 333), (144, 8, 1000), (9, 3, 17)])
+def test_forward_matches_torch(n_obs, n_act, E):
+    from gym_pybullet_drones_routing_amd.policy import MlpPolicyKernel
+    pol = _policy(n_obs, n_act, n_obs)
+    k = MlpPolicyKernel(pol, seed=3)
+    obs = _rows(E, n_obs, 1)
+    act_env = torch.full((E, n_act), 7.0, device="cuda")
+    buf_obs = torch.zeros((E, n_obs), device="cuda")
+    buf_act, buf_logp, buf_val = torch.zeros((E, n_act), device="cuda"), torch.zeros(E, device="cuda"), \
+        torch.zeros(E, device="cuda")
+    k.step(obs, act_env, buf_obs, buf_act, buf_logp, buf_val, deterministic=True)
+    with torch.no_grad():
+        mu, v = pol.pi(obs), pol.value(obs)
+        std = pol.log_std.exp()
+    torch.cuda.synchronize()
+    assert torch.equal(buf_obs, obs)
+    torch.testing.assert_close(buf_act, mu, rtol=1e-5, atol=2e-6)
+    torch.testing.assert_close(buf_val, v, rtol=1e-5, atol=2e-6)
+    assert torch.equal(act_env, buf_act.clamp(-1, 1))
+    lp = torch.distributions.Normal(mu, std).log_prob(mu).sum(-1)
+    torch.testing.assert_close(buf_logp, lp, rtol=1e-6, atol=1e-5)
+    assert int(k.rng[1]) == 0          # deterministic calls draw nothing
+
+
+@pytest.mark.parametrize("n_obs,n_act", [(27, 1), (72, 4), (144, 8)])
+def test_sample_log_prob_and_counter(n_obs, n_act):
+    from gym_pybullet_drones_routing_amd.policy import MlpPolicyKernel
+    E = 8192
+    pol = _policy(n_obs, n_act, 5)
+    k = MlpPolicyKernel(pol, seed=11)
+    obs = _rows(E, n_obs, 2)
+    acts, envs = [], []
+    for _ in range(3):
+        a, ae, lpk = torch.zeros((E, n_act), device="cuda"), torch.zeros((E, n_act), device="cuda"), \
+            torch.zeros(E, device="cuda")
+        k.step(obs, ae, None, a, lpk, None)
+        acts.append((a, lpk))
+        envs.append(ae)
+    torch.cuda.synchronize()
+    assert int(k.rng[1]) == 3 and int(k.rng[2]) == 0      # one call counter step per sampling call
+    with torch.no_grad():
+        mu = pol.pi(obs)
+        std = pol.log_std.exp()
+        d = torch.distributions.Normal(mu, std)
+    eps = torch.cat([((a - mu) / std).reshape(-1) for a, _ in acts]).double()
+    n = eps.numel()
+    assert abs(float(eps.mean())) < 5 / math.sqrt(n)
+    assert abs(float(eps.var()) - 1.0) < 6 * math.sqrt(2.0 / n)
+    assert abs(float((eps.abs() < 1).double().mean()) - 0.682689) < 0.01
+    for (a, lpk), ae in zip(acts, envs):
+        torch.testing.assert_close(lpk, d.log_prob(a).sum(-1), rtol=1e-5, atol=2e-5)
+        assert torch.equal(ae, a.clamp(-1, 1))
+    assert not torch.equal(acts[0][0], acts[1][0])
+    # the same key and counter draw the same numbers
+    k.rng[1] = 1
+    a2 = torch.zeros((E, n_act), device="cuda")
+    k.step(obs, None, None, a2, None, None)
+    torch.cuda.synchronize()
+    assert torch.equal(a2, acts[1][0])
+
+
+def test_bootstrap_rows():
+    """Rows of the previous step: reward + gamma * V(terminal_obs) where truncated and not
+    terminated (SB3's TimeLimit.truncated bootstrap, learn.py's rollout), the reward as is
+    elsewhere; done = terminated | truncated."""
+    from gym_pybullet_drones_routing_amd.policy import MlpPolicyKernel
+    E, n_obs = 3001, 27
+    pol = _policy(n_obs, 1, 9)
+    k = MlpPolicyKernel(pol)
+    g = torch.Generator(device="cuda").manual_seed(4)
+    rew = torch.rand(E, generator=g, device="cuda") * 2
+    te = (torch.rand(E, generator=g, device="cuda") < 0.1).to(torch.uint8)
+    tr = (torch.rand(E, generator=g, device="cuda") < 0.2).to(torch.uint8)
+    tobs = _rows(E, n_obs, 5)
+    tr[:16] = 0                       # a whole row group without any bootstrap
+    te[:16] = 0
+    buf_rew, buf_done = torch.full((E,), -5.0, device="cuda"), torch.full((E,), -5.0, device="cuda")
+    k.step(None, prev=(rew, te, tr, tobs), gamma=0.99, buf_rew=buf_rew, buf_done=buf_done)
+    with torch.no_grad():
+        tv = pol.value(tobs)
+    trunc = tr.bool() & ~te.bool()
+    want = torch.where(trunc, rew + 0.99 * tv, rew)
+    torch.cuda.synchronize()
+    assert torch.equal(buf_rew[~trunc], rew[~trunc])
+    torch.testing.assert_close(buf_rew, want, rtol=1e-6, atol=2e-6)
+    assert torch.equal(buf_done, (te.bool() | tr.bool()).float())
+
+
+def test_gae_bit_identical_to_learn_loop():
+    from gym_pybullet_drones_routing_amd.policy import MlpPolicyKernel
+    T, E = 64, 4097
+    k = MlpPolicyKernel(_policy(27, 1, 1))
+    g = torch.Generator(device="cuda").manual_seed(8)
+    rew = torch.randn((T, E), generator=g, device="cuda")
+    val = torch.randn((T, E), generator=g, device="cuda")
+    done = (torch.rand((T, E), generator=g, device="cuda") < 0.05).float()
+    last_v = torch.randn(E, generator=g, device="cuda")
+    gamma, lam = 0.99, 0.95
+    adv_k, ret_k = torch.empty_like(rew), torch.empty_like(rew)
+    k.gae(rew, val, done, last_v, gamma, lam, adv_k, ret_k)
+    # examples/learn.py's loop, verbatim
+    adv = torch.zeros_like(rew)
+    gg = torch.zeros(E, device="cuda")
+    for t in reversed(range(T)):
+        nv = last_v if t == T - 1 else val[t + 1]
+        nonterm = 1.0 - done[t]
+        delta = rew[t] + gamma * nv * nonterm - val[t]
+        gg = delta + gamma * lam * nonterm * gg
+        adv[t] = gg
+    ret = adv + val
+    torch.cuda.synchronize()
+    assert torch.equal(adv_k, adv) and torch.equal(ret_k, ret)
+
+
+def test_rollout_graph_with_env_step():
+    """K x (policy kernel + gpd_step) captured in one hipGraph and replayed: the same buffers as
+    the eager sequence from the same state and counter (the counter lives on the device)."""
+    from gym_pybullet_drones_routing_amd.enums import ActionType
+    from gym_pybullet_drones_routing_amd.policy import MlpPolicyKernel
+    from gym_pybullet_drones_routing_amd.sim import BatchedAviarySim
+    E, K = 512, 8
+    sim = BatchedAviarySim(n_envs=E, task="hover", act=ActionType.ONE_D_RPM, device="cuda:0")
+    W = sim.obs_width
+    pol = _policy(W, 1, 2)
+    k = MlpPolicyKernel(pol, seed=5)
+    act = torch.zeros((E, 1, 1), device="cuda")
+    bufs = {n: torch.zeros((K, E) + s, device="cuda") for n, s in
+            (("obs", (W,)), ("act", (1,)), ("logp", ()), ("val", ()), ("rew", ()), ("done", ()))}
+    obs = sim.obs.view(E, W)
+    tobs = sim.terminal_obs.view(E, W)
+
+    def seq():
+        for t in range(K):
+            prev = (sim.reward, sim.terminated, sim.truncated, tobs) if t else None
+            k.step(obs, act, bufs["obs"][t], bufs["act"][t], bufs["logp"][t], bufs["val"][t], prev=prev,
+                   buf_rew=bufs["rew"][t - 1] if t else None, buf_done=bufs["done"][t - 1] if t else None)
+            sim.step(act)
+    blob = sim.save_state()
+    pack0 = sim.out_pack.clone()            # obs / flags / terminal rows the first call reads
+    seq()
+    eager = {n: b.clone() for n, b in bufs.items()}
+    sim.load_state(blob)
+    sim.out_pack.copy_(pack0)
+    k.rng[1] = 0
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        seq()
+    for b in bufs.values():
+        b.zero_()
+    gr.replay()
+    torch.cuda.synchronize()
+    for n in bufs:
+        assert torch.equal(bufs[n], eager[n]), n
+    assert int(k.rng[1]) == K
+    sim.close()

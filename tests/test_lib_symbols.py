@@ -39,7 +39,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 def test_host_only_entry_points(lib):
     from gym_pybullet_drones_routing_amd import _lib
-    assert lib.gpd_abi_version() == _lib.GPD_ABI_VERSION == 5
+    assert lib.gpd_abi_version() == _lib.GPD_ABI_VERSION == 6
     assert lib.gpd_nonfinite(None, None, None) == _lib.GPD_EINVAL
     q = _lib.PidParams()
     assert lib.gpd_default_pid_params(ctypes.byref(q)) == _lib.GPD_OK
@@ -56,6 +56,34 @@ def test_host_only_entry_points(lib):
     assert lib.gpd_state_bytes(None) == 0
 
 
+@pytest.mark.parametrize("E,D,W", [(4096, 1, 72), (3, 1, 72), (5, 2, 27), (1, 8, 36), (4095, 3, 27)])
+def test_pack_layout_matches_library(lib, E, D, W):
+    """sim.pack_layout (the Python restatement the CPU tests use) equals gpd_pack_layout_of; every
+    field 256-B aligned (float views at any shard size: ADVICE r5), the record ends where
+    terminal_obs begins, invalid shapes rejected (host-only calls: no GPU needed)."""
+    from gym_pybullet_drones_routing_amd import _lib
+    from gym_pybullet_drones_routing_amd.sim import pack_layout
+    L = pack_layout(E, D, W)
+    c = _lib.PackLayout()
+    assert lib.gpd_pack_layout_of(E, D, W, ctypes.byref(c)) == _lib.GPD_OK
+    assert (c.n_envs, c.drones_per_env, c.obs_width, c.state_cols) == (E, D, W, 12)
+    for k in ("obs", "reward", "terminated", "truncated", "terminal_state", "terminal_obs"):
+        assert getattr(c, k) == L[k][0] and L[k][0] % 256 == 0
+    for k in ("prefix", "prefix_aligned", "record", "total"):
+        assert getattr(c, k) == L[k]
+    assert L["prefix_aligned"] % 256 == 0 and L["record"] == L["terminal_obs"][0]
+    assert L["terminal_state"][1] == E * D * 12 * 4
+    assert lib.gpd_pack_layout_of(E, D, 11, ctypes.byref(c)) == _lib.GPD_EINVAL
+    assert lib.gpd_pack_layout_of(0, D, W, ctypes.byref(c)) == _lib.GPD_EINVAL
+    # the pack / unpack entry points validate before touching the device
+    assert lib.gpd_handoff_pack(None, ctypes.byref(c), None) == _lib.GPD_EINVAL
+    bad = _lib.PackLayout()
+    ctypes.memmove(ctypes.byref(bad), ctypes.byref(c), ctypes.sizeof(c))
+    bad.record += 256
+    assert lib.gpd_handoff_pack(None, ctypes.byref(bad), None) == _lib.GPD_EINVAL
+    assert b"layout" in lib.gpd_last_error()
+
+
 def test_struct_sizes_match_header():
     """ctypes mirrors of gpd_drone_params / gpd_config / gpd_constants have the C layout."""
     from gym_pybullet_drones_routing_amd import _lib
@@ -69,9 +97,9 @@ def test_struct_sizes_match_header():
 typedef void* hipStream_t;
 #include "gpd.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(gpd_drone_params), sizeof(gpd_config), sizeof(gpd_constants),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(gpd_drone_params), sizeof(gpd_config), sizeof(gpd_constants),
          sizeof(gpd_pid_params), offsetof(gpd_config, episode_len_sec), offsetof(gpd_config, drones_per_block),
-         offsetof(gpd_config, store_policy));
+         offsetof(gpd_config, store_policy), sizeof(gpd_pack_layout), offsetof(gpd_pack_layout, record));
   return 0;
 }
 """
@@ -83,8 +111,9 @@ int main(void) {
                                               check=True).stdout.split()]
     assert got[:4] == [ctypes.sizeof(_lib.DroneParams), ctypes.sizeof(_lib.Config), ctypes.sizeof(_lib.Constants),
                        ctypes.sizeof(_lib.PidParams)]
-    assert got[4:] == [_lib.Config.episode_len_sec.offset, _lib.Config.drones_per_block.offset,
-                       _lib.Config.store_policy.offset]
+    assert got[4:7] == [_lib.Config.episode_len_sec.offset, _lib.Config.drones_per_block.offset,
+                        _lib.Config.store_policy.offset]
+    assert got[7:] == [ctypes.sizeof(_lib.PackLayout), _lib.PackLayout.record.offset]
 
 
 def test_abi_version_consistent():
