@@ -334,7 +334,7 @@ __device__ __forceinline__ void plane_space(const R n[3], R p[3], R q[3]) {
 // pairs split into 32 tasks each (4 rims x 8 starts) over the wave's lanes (dc_narrow_pass): a
 // sparse wave (one or two near pairs, the common case) runs ONE Newton chain per lane.
 template <typename R> struct NpTol;
-template <> struct NpTol<double> { static constexpr double accept = 1e-10, same = 1e-9, tie = 1e-10; };   // RIM_ACCEPT, RIM_SAME, PAIR_TIE
+template <> struct NpTol<double> { static constexpr double accept = 1e-10, same = 1e-4, tie = 1e-7; };   // RIM_ACCEPT, RIM_SAME, PAIR_TIE
 template <> struct NpTol<float> { static constexpr float accept = 1e-5f, same = 1e-4f, tie = 1e-7f; };
 constexpr int kRimSamples = 8, kRimIters = 8;   // RIM_SAMPLES, RIM_ITERS
 template <typename R>
@@ -585,7 +585,7 @@ __device__ __forceinline__ bool face_points(const R ca[3], const R aa[3], const 
 // pairing of the cached points on A), the first of a tie; the ties (depth, area) keep rounding
 // from deciding a symmetric manifold
 template <typename R> struct MfTol;
-template <> struct MfTol<double> { static constexpr double depth = 1e-9, area = 1e-9; };   // MANIFOLD_*_TIE
+template <> struct MfTol<double> { static constexpr double depth = 1e-6, area = 1e-4; };   // MANIFOLD_*_TIE
 template <> struct MfTol<float> { static constexpr float depth = 1e-6f, area = 1e-4f; };
 template <typename R>
 __device__ __forceinline__ int manifold_replace(const R pb[3], R dist, const R n[3], const R fp[4][3], const R fd[4]) {

@@ -365,11 +365,17 @@ __global__ void __launch_bounds__(256) gae_kernel(int T, int n, const float* __r
 
 template <int NA>
 int launch(const Args& A, int grid, size_t lds, hipStream_t st) {
-  static bool attr = false;   // > 64 KB of dynamic LDS must be allowed once per kernel
-  if (!attr) {
-    HIP_TRY(hipFuncSetAttribute((const void*)rollout_kernel<NA>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024));
-    attr = true;
+  // dynamic LDS past 64 KB must be allowed per kernel, up to what this launch needs
+  static size_t allowed = 64 * 1024;
+  if (lds > allowed) {
+    const hipError_t e = hipFuncSetAttribute((const void*)rollout_kernel<NA>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();   // do not leave the error for the next caller's hipGetLastError
+      return fail(kEhip, std::string("hipFuncSetAttribute(rollout_kernel, ") + std::to_string(lds) +
+                             " B of dynamic LDS): " + hipGetErrorString(e));
+    }
+    allowed = lds;
   }
   hipLaunchKernelGGL(rollout_kernel<NA>, dim3(grid), dim3(kBlock), lds, st, A);
   HIP_TRY(hipGetLastError());

@@ -318,8 +318,10 @@ SIMDSQRT12 = 0.7071067811865475244008443621048490
 RIM_SAMPLES = 8             # start azimuths per rim circle (k * 45 deg in btPlaneSpace1 of the axis)
 RIM_ITERS = 8               # trust-region Newton steps from each start azimuth
 RIM_ACCEPT = 1e-10          # a step must lower the squared distance by this fraction (rounding-proof)
-RIM_SAME = 1e-9             # starts whose squared distances agree to this fraction reached one minimum
-PAIR_TIE = 1e-10            # candidates within this of the closest count as tied: the first wins (m)
+RIM_SAME = 1e-4             # starts whose squared distances agree to this fraction count as one minimum (sized
+                            # for the f32 kernel's rounding, so both precisions pick the same start)
+PAIR_TIE = 1e-7             # candidates within this of the closest count as tied: the first wins (m); sized
+                            # for the f32 kernel (a level side-by-side pair ties its lateral line and both rims)
 RIM_COS = (1.0, SIMDSQRT12, 0.0, -SIMDSQRT12, -1.0, -SIMDSQRT12, 0.0, SIMDSQRT12)   # k * 45 deg
 RIM_SIN = (0.0, SIMDSQRT12, 1.0, SIMDSQRT12, 0.0, -SIMDSQRT12, -1.0, -SIMDSQRT12)
 
@@ -613,8 +615,8 @@ def face_points(ca, aa, cb, ab, n, radius, half_height, mg):
 
 
 MANIFOLD_CACHE_SIZE = 4     # btPersistentManifold's point capacity
-MANIFOLD_DEPTH_TIE = 1e-9   # a cached point counts as deeper than the new one only beyond this (m)
-MANIFOLD_AREA_TIE = 1e-9    # areas within this fraction of the largest count as tied: the first wins
+MANIFOLD_DEPTH_TIE = 1e-6   # a cached point counts as deeper than the new one only beyond this (m)
+MANIFOLD_AREA_TIE = 1e-4    # areas within this fraction of the largest count as tied: the first wins
 
 
 def manifold_replace(new_a, new_d, cache):
