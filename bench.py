@@ -491,12 +491,15 @@ def _policy_mlp(n_in, n_out):
 
 
 def handoff_leg(sim, global_envs, hmode, cap, gpool, G, rank, device, force=False):
-    """One LearnerHandoff configuration, per step: eager ``step()`` calls (G steps after 3 warm
-    ones, wall clock, max over ranks); with the default capacity also the same calls replaying
-    the captured one-step hipGraph (``LearnerHandoff.capture``: scatter + shard step + pack +
-    collective + unpack) - ``ms_per_step`` - and a graph of 32 hand-off steps timed by HIP events
-    (the device-side cost per step, no host launch).  Also the bytes that land per step, how many
-    steps needed the second (overflow) exchange and the finished-env rate of the batch."""
+    """One LearnerHandoff configuration, per step.  ``ms_per_step``: a hand-off step (action
+    scatter + shard step + pack + ONE collective + unpack) inside a captured graph of 32 of them,
+    by HIP events - how examples/learn.py runs it (the fused rollout replays n_steps of them with
+    the policy kernel between, ``rollout_with_policy_us_per_step``); ``replay_ms_per_step``: one
+    ``step()`` call per step replaying the captured one-step graph (the host's launch included);
+    ``eager_ms_per_step``: the same calls without a graph (G steps after 3 warm ones, wall clock,
+    max over ranks).  Also the bytes that land per step, how many steps needed the second
+    (overflow) exchange and the finished-env rate of the batch.  A ``terminal_capacity`` below the
+    shard reads the finished count on the host every step: eager only."""
     import torch.distributed as dist
 
     from gym_pybullet_drones_routing_amd.shard import LearnerHandoff, max_over_ranks
@@ -518,23 +521,58 @@ def handoff_leg(sim, global_envs, hmode, cap, gpool, G, rank, device, force=Fals
         torch.cuda.synchronize(device)
         return max_over_ranks(time.perf_counter() - t0, device)
 
-    eager = timed()
-    out = dict(h.stats(), eager_ms_per_step=1000 * eager / G)
-    if not h.host_sync_per_step and not h._stage:
-        g32 = h.capture(n_steps=32, install=False)
-        g32.replay()
+    def graph_us(body, k=32, reps=4):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(k):
+                body()
+        g.replay()
         torch.cuda.synchronize(device)
         dist.barrier()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
-        for _ in range(4):
-            g32.replay()
+        for _ in range(reps):
+            g.replay()
         ev1.record()
         torch.cuda.synchronize(device)
-        out["graph32_us_per_step"] = max_over_ranks(1000.0 * ev0.elapsed_time(ev1) / (4 * 32), device)
-        del g32
+        del g
+        return max_over_ranks(1000.0 * ev0.elapsed_time(ev1) / (reps * k), device)
+
+    eager = timed()
+    out = dict(h.stats(), eager_ms_per_step=1000 * eager / G)
+    if not h.host_sync_per_step and not h._stage:
+        src = h.global_actions if h.is_learner else None
+        out["ms_per_step"] = graph_us(lambda: h.step_body(src)) / 1000.0
+        if hmode == "gather":
+            # the config-5 RL step: the fused policy kernel on the learner's gathered batch (the
+            # bench's 64-64 tanh actor + critic), then the hand-off step, as learn.py's rollout
+            from gym_pybullet_drones_routing_amd.policy import MlpPolicyKernel
+            Eg, D, W, A = global_envs, sim.drones_per_env, sim.obs_width, sim.act_width
+
+            class _AC(torch.nn.Module):
+                def __init__(self):
+                    super().__init__()
+                    self.pi, self.vf = _policy_mlp(D * W, D * A), _policy_mlp(D * W, 1)
+                    self.log_std = torch.nn.Parameter(torch.zeros(D * A))
+            if h.is_learner:
+                torch.manual_seed(0)
+                kern = MlpPolicyKernel(_AC().to(device), seed=3)
+                bufs = [torch.zeros((Eg, D * W), device=device), torch.zeros((Eg, D * A), device=device),
+                        torch.zeros(Eg, device=device), torch.zeros(Eg, device=device),
+                        torch.zeros(Eg, device=device), torch.zeros(Eg, device=device)]
+                obs_v, tobs_v = h.obs.view(Eg, -1), h.terminal_rows.view(Eg, -1)
+
+                def body():
+                    kern.step(obs_v, h.global_actions.view(Eg, -1), *bufs[:4],
+                              prev=(h.reward, h.terminated, h.truncated, tobs_v), buf_rew=bufs[4], buf_done=bufs[5])
+                    h.step_body(h.global_actions)
+            else:
+                def body():
+                    h.step_body(None)
+            with torch.no_grad():
+                out["rollout_with_policy_us_per_step"] = graph_us(body)
         h.capture()                       # step() replays one captured hand-off step from now on
-        out["ms_per_step"] = 1000 * timed() / G
+        out["replay_ms_per_step"] = 1000 * timed() / G
         out["graphed"] = True
     else:
         out["ms_per_step"] = out["eager_ms_per_step"]
@@ -958,12 +996,13 @@ def _run(args):
                              for hmode in ("gather", "all_gather")}
                 result["handoff"] = {
                     "mode": f"learner hand-off per step ({coll}{', one rank, collectives forced' if one_rank else ''}): "
-                            "action all_to_all_single from rank 0, shard step, pack kernel (the finished envs' 12 "
-                            "state columns into the record), ONE collective of the records (gather = "
-                            "all_to_all_single to the learner, all_gather = all_gather_into_tensor), unpack kernel; "
-                            "ms_per_step = step() replaying the captured one-step hipGraph, eager_ms_per_step = the "
-                            "same calls without the graph, graph32_us_per_step = 32 hand-off steps in one graph "
-                            "(HIP events: the device-side cost)",
+                            "actions from rank 0 (grouped RCCL send / recv), shard step, pack kernel (the finished "
+                            "envs' 12 state columns into the record), ONE collective of the records (gather = "
+                            "grouped RCCL send / recv to the learner, all_gather = ncclAllGather; rccl.RcclComm), "
+                            "unpack kernel; ms_per_step = one hand-off step inside a captured graph of 32 (HIP "
+                            "events; how examples/learn.py's fused rollout runs it, rollout_with_policy_us_per_step "
+                            "with its policy kernel), replay_ms_per_step = one step() call replaying the captured "
+                            "one-step graph, eager_ms_per_step = the same calls without a graph",
                     "step_only_ms": 1000.0 * eager_wall / args.steps, "legs": legs,
                     "synchronising_legs": sync_legs,
                     "synchronising_legs_note": f"terminal_capacity {cap} < shard: the finished envs' columns compacted "

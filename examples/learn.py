@@ -213,38 +213,62 @@ class GraphedMinibatch:
 class FusedRollout:
     """The rollout on the HIP path: per env.step ONE fused policy kernel (actor + critic forward,
     Normal sample, clip, the buffer rows, and the previous step's time-limit bootstrap;
-    ``policy.MlpPolicyKernel``) and ONE ``gpd_step``, the whole n_steps sequence captured in one
+    ``policy.MlpPolicyKernel``) and ONE env step, the whole n_steps sequence captured in one
     hipGraph and replayed every PPO iteration (the parameters are read in place, so the optimizer's
     in-place updates reach the graph); then the last value and GAE (``gpd_policy_gae``, bit-identical
     to the torch loop of ``train``).  The same quantities as the eager loop, drawn from a Philox
-    stream instead of torch's generator."""
+    stream instead of torch's generator.
 
-    def __init__(self, policy, sim, n_steps, gamma, gae_lambda, seed, bufs):
+    ``env``: an ``AviaryVecEnv`` (the step is ``gpd_step`` on its sim) or, on RCCL, a
+    ``ShardedAviaryVecEnv`` (the step is the learner hand-off: action scatter, every rank's shard
+    step, record gather and unpack, ``shard.LearnerHandoff``; the other ranks capture and replay the
+    same n_steps hand-off steps on the learner's ROLLOUT command, so the collectives pair up)."""
+
+    def __init__(self, policy, env, n_steps, gamma, gae_lambda, seed, bufs):
         from gym_pybullet_drones_routing_amd.policy import MlpPolicyKernel
         self.k = MlpPolicyKernel(policy, seed=seed)
-        self.sim, self.T, self.gamma, self.lam = sim, n_steps, gamma, gae_lambda
-        E = sim.n_envs
-        n_obs = sim.drones_per_env * sim.obs_width
-        self.obs = sim.obs.view(E, n_obs)                 # sim-owned, rewritten in place by every step
-        self.tobs = sim.terminal_obs.view(E, n_obs)
-        self.act = torch.zeros((E, sim.drones_per_env, sim.act_width), device=sim.device)
+        self.env, self.T, self.gamma, self.lam = env, n_steps, gamma, gae_lambda
+        h = getattr(env, "handoff", None)
+        self.h = h
+        if h is not None:            # the learner's global batch, rebuilt in place by every hand-off step
+            E = env.num_envs
+            n_obs = h.obs[0].numel()
+            self.obs, self.tobs = h.obs.view(E, n_obs), h.terminal_rows.view(E, n_obs)
+            self.act = h.global_actions
+            self.flags = lambda: (h.reward, h.terminated, h.truncated, self.tobs)
+            self.step_fn = lambda: h.step_body(h.global_actions)
+            dev = h.device
+        else:
+            sim = env.sim
+            E = sim.n_envs
+            n_obs = sim.drones_per_env * sim.obs_width
+            self.obs = sim.obs.view(E, n_obs)             # sim-owned, rewritten in place by every step
+            self.tobs = sim.terminal_obs.view(E, n_obs)
+            self.act = torch.zeros((E, sim.drones_per_env, sim.act_width), device=sim.device)
+            self.flags = lambda: (sim.reward, sim.terminated, sim.truncated, self.tobs)
+            self.step_fn = lambda: sim.step(self.act, terminal_obs=True)
+            dev = sim.device
+        self.E = E
         self.b = bufs
-        self.last_v = torch.zeros(E, device=sim.device)
+        self.last_v = torch.zeros(E, device=dev)
         self.graph = None
 
     def _seq(self):
-        b, k, sim = self.b, self.k, self.sim
+        b, k = self.b, self.k
         for t in range(self.T):
-            prev = (sim.reward, sim.terminated, sim.truncated, self.tobs) if t else None
-            k.step(self.obs, self.act.view(self.obs.shape[0], -1), b["obs"][t], b["act"][t], b["logp"][t],
+            prev = self.flags() if t else None
+            k.step(self.obs, self.act.view(self.E, -1), b["obs"][t], b["act"][t], b["logp"][t],
                    b["val"][t], prev=prev, gamma=self.gamma, buf_rew=b["rew"][t - 1] if t else None,
                    buf_done=b["done"][t - 1] if t else None)
-            sim.step(self.act, terminal_obs=True)
-        k.step(self.obs, buf_val=self.last_v, prev=(sim.reward, sim.terminated, sim.truncated, self.tobs),
+            self.step_fn()
+        k.step(self.obs, buf_val=self.last_v, prev=self.flags(),
                gamma=self.gamma, buf_rew=b["rew"][self.T - 1], buf_done=b["done"][self.T - 1])
         k.gae(b["rew"], b["val"], b["done"], self.last_v, self.gamma, self.lam, b["adv"], b["ret"])
 
     def run(self):
+        if self.h is not None:
+            self.env.rollout(self.T, self._seq)      # the ROLLOUT command: every rank replays its graph
+            return
         if self.graph is None:
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
@@ -297,10 +321,10 @@ def train(multiagent=False, n_envs=4096, n_steps=64, total_timesteps=int(3e7), l
     obs = env.reset().reshape(E, -1)
     fr = None
     if fused:
-        if not hasattr(env, "sim") or getattr(env, "handoff", None) is not None:
-            raise ValueError("fused=True needs a single-GPU AviaryVecEnv")
+        if getattr(env, "handoff", None) is not None and not getattr(env, "graphed", False):
+            raise ValueError("fused=True over sharded envs needs the RCCL hand-off (ShardedAviaryVecEnv(graph=True))")
         adv_buf, ret_buf = torch.zeros((n_steps, E), device=device), torch.zeros((n_steps, E), device=device)
-        fr = FusedRollout(policy, env.sim, n_steps, gamma, gae_lambda, seed,
+        fr = FusedRollout(policy, env, n_steps, gamma, gae_lambda, seed,
                           {"obs": buf_obs, "act": buf_act, "logp": buf_logp, "val": buf_val, "rew": buf_rew,
                            "done": buf_done, "adv": adv_buf, "ret": ret_buf})
     history = []
@@ -411,9 +435,9 @@ def parse_args(argv=None):
                         "arithmetic up to rounding, so a different training trajectory than the default "
                         "eager loop, which reproduces the recorded runs step for step)")
     p.add_argument("--rollout", default="fused", choices=["fused", "eager"],
-                   help="fused (one GPU): one policy kernel + one gpd_step per env.step, the rollout replayed as "
-                        "one hipGraph (FusedRollout); eager: the torch policy step by step (the loop that "
-                        "reproduces the recorded round-4/5 runs)")
+                   help="fused: one policy kernel + one env step (gpd_step, or the RCCL learner hand-off over the "
+                        "ranks) per env.step, the rollout replayed as one hipGraph (FusedRollout); eager: the "
+                        "torch policy step by step (the loop that reproduces the recorded round-4/5 runs)")
     p.add_argument("--learner", default="rank0", choices=["rank0", "per-rank"],
                    help="rank0: one learner on the gathered batch (ShardedAviaryVecEnv); per-rank: a learner "
                         "per GPU on its own env shard, gradients all-reduced")
@@ -460,7 +484,7 @@ def run(a):
             env.serve()
             dist.destroy_process_group()
             return
-    fused = a.rollout == "fused" and world == 1
+    fused = a.rollout == "fused" and (world == 1 or getattr(env, "graphed", False))
     policy, hist, best, target = train(multiagent=multi, n_envs=a.n_envs, total_timesteps=int(a.total_timesteps),
                                        max_seconds=a.max_seconds, physics=Physics(a.physics), device=device, env=env,
                                        graph=a.graph, seed=a.seed, fused=fused)

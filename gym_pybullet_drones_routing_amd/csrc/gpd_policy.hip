@@ -110,26 +110,51 @@ struct Lds {
 };
 constexpr int kRes = 16;
 
-__device__ inline void stage_w1(float4* dst, const float* __restrict__ w, int n_obs, int kq) {
-  float* d = (float*)dst;
-  for (int i = threadIdx.x; i < kq * 4 * H; i += kBlock) {
-    const int j = i / (kq * 4), k = i - j * (kq * 4);
-    d[(k >> 2) * (H * 4) + j * 4 + (k & 3)] = k < n_obs ? w[j * n_obs + k] : 0.0f;
-  }
-}
-__device__ inline void stage_w2(float4* dst, const float* __restrict__ w) {
-  float* d = (float*)dst;
-  for (int i = threadIdx.x; i < H * H; i += kBlock) {
-    const int j = i >> 6, k = i & 63;
-    d[(k >> 2) * (H * 4) + j * 4 + (k & 3)] = w[i];
+// Weight staging: row-major nn.Linear weights [64][n] -> LDS [n/4][64][4] (float4 q of neuron j
+// at q * 64 + j).  Element idx -> (q = idx / 64, j = idx % 64): consecutive lanes write consecutive
+// LDS float4s; every lane issues all its loads before its first store, so a block's ~70 KB arrive
+// in one L2 round trip instead of one per loop iteration (the first build's scalar loop of
+// dependent load -> store pairs took ~20 us of a 24 us launch).
+template <int U>
+__device__ inline void stage_rows4(float4* __restrict__ dst, const float* __restrict__ w, int n, int kq) {
+  const int total = kq * H;
+  const bool vec = (n & 3) == 0 && ((uintptr_t)w & 15) == 0;
+  for (int base = threadIdx.x; base < total; base += U * kBlock) {
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = base + u * kBlock;
+      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (idx < total) {
+        const int q = idx >> 6, j = idx & 63, k = 4 * q;
+        const float* src = w + (size_t)j * n + k;
+        if (vec) {
+          v[u] = *reinterpret_cast<const float4*>(src);
+        } else {
+          v[u].x = src[0];
+          v[u].y = k + 1 < n ? src[1] : 0.0f;
+          v[u].z = k + 2 < n ? src[2] : 0.0f;
+          v[u].w = k + 3 < n ? src[3] : 0.0f;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = base + u * kBlock;
+      if (idx < total) dst[idx] = v[u];
+    }
   }
 }
 
 // hidden layers of one network for the wave's kRows rows: x (LDS rows) -> h2 in `h` (lane = neuron)
+struct Bias {
+  float p1, v1, p2, v2;   // neuron `lane`'s first / second layer biases (actor, critic)
+};
 template <bool BOTH>
-__device__ inline void hidden(const Lds& s, const Args& A, float (&hp)[kRows], float (&hv)[kRows], int lane) {
+__device__ inline void hidden(const Lds& s, const Args& A, const Bias& B, float (&hp)[kRows], float (&hv)[kRows],
+                              int lane) {
   float ap[kRows], av[kRows];
-  const float bp = A.pi.b1[lane], bv = A.vf.b1[lane];
+  const float bp = B.p1, bv = B.v1;
 #pragma unroll
   for (int r = 0; r < kRows; ++r) { ap[r] = bp; av[r] = bv; }
   const float4* x4 = (const float4*)s.x;
@@ -154,7 +179,7 @@ __device__ inline void hidden(const Lds& s, const Args& A, float (&hp)[kRows], f
     if (BOTH) s.hp[r * H + lane] = tanhf(ap[r]);
   }
   __syncthreads();
-  const float b2p = A.pi.b2[lane], b2v = A.vf.b2[lane];
+  const float b2p = B.p2, b2v = B.v2;
 #pragma unroll
   for (int r = 0; r < kRows; ++r) { ap[r] = b2p; av[r] = b2v; }
   const float4* hv4 = (const float4*)s.hv;
@@ -217,14 +242,18 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(Args A) {
   s.hv = s.hp + kRows * H;
   s.res = s.hv + kRows * H;
 
-  stage_w1(s.w1v, A.vf.w1, A.n_obs, A.kq);
-  stage_w2(s.w2v, A.vf.w2);
+  stage_rows4<8>(s.w1v, A.vf.w1, A.n_obs, A.kq);
+  stage_rows4<4>(s.w2v, A.vf.w2, H, H / 4);
   if (A.actor) {
-    stage_w1(s.w1p, A.pi.w1, A.n_obs, A.kq);
-    stage_w2(s.w2p, A.pi.w2);
+    stage_rows4<8>(s.w1p, A.pi.w1, A.n_obs, A.kq);
+    stage_rows4<4>(s.w2p, A.pi.w2, H, H / 4);
   }
   uint64_t seed = 0, call = 0;
   if (A.sample) { seed = A.rng[0]; call = A.rng[1]; }
+  Bias B;
+  B.v1 = A.vf.b1[lane]; B.v2 = A.vf.b2[lane];
+  B.p1 = A.actor ? A.pi.b1[lane] : 0.0f;
+  B.p2 = A.actor ? A.pi.b2[lane] : 0.0f;
   // output-layer weights of neuron `lane`
   float w3p[NA], b3p[NA], scale[NA];
 #pragma unroll
@@ -249,7 +278,7 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(Args A) {
       if (__syncthreads_or(any)) {
         load_rows(s, A, A.tobs, row0, lane, nullptr);
         __syncthreads();
-        hidden<false>(s, A, hp, hv, lane);
+        hidden<false>(s, A, B, hp, hv, lane);
       } else {
 #pragma unroll
         for (int r = 0; r < kRows; ++r) hv[r] = 0.0f;
@@ -280,8 +309,8 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(Args A) {
     // ---- this step: actor + critic on obs
     load_rows(s, A, A.obs, row0, lane, A.buf_obs);
     __syncthreads();
-    if (A.actor) hidden<true>(s, A, hp, hv, lane);
-    else hidden<false>(s, A, hp, hv, lane);
+    if (A.actor) hidden<true>(s, A, B, hp, hv, lane);
+    else hidden<false>(s, A, B, hp, hv, lane);
     float val[kRows], mu[NA][kRows];
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {

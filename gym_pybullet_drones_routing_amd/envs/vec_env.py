@@ -155,9 +155,9 @@ class ShardedAviaryVecEnv:
     (RCCL only): from the second step on, every step replays the hand-off's captured hipGraph
     (``LearnerHandoff.capture``), on every rank at the same step.
     """
-    STEP, RESET, STOP = 0, 1, 2
+    STEP, RESET, STOP, ROLLOUT = 0, 1, 2, 3
 
-    def __init__(self, num_envs, graph=False, **kw):
+    def __init__(self, num_envs, graph=False, force_collectives=False, **kw):
         import torch.distributed as dist
 
         from ..shard import LearnerHandoff, env_shard
@@ -168,17 +168,20 @@ class ShardedAviaryVecEnv:
         kw["output"] = "torch"
         self.local = AviaryVecEnv(count, **kw)
         self.sim = self.local.sim
-        self.handoff = LearnerHandoff(self.sim, num_envs, mode="gather")   # one learner: rank 0
+        self.handoff = LearnerHandoff(self.sim, num_envs, mode="gather",   # one learner: rank 0
+                                      force_collectives=force_collectives)
         self.num_envs = int(num_envs)
         self.num_drones = self.local.num_drones
         self.action_space = self.local.action_space
         self.observation_space = self.local.observation_space
         self.output = "torch"
         gloo = dist.is_initialized() and dist.get_backend() == "gloo"
-        self._cmd = torch.zeros((1,), dtype=torch.int32, device="cpu" if gloo else self.sim.device)
+        self._cmd = torch.zeros((2,), dtype=torch.int32, device="cpu" if gloo else self.sim.device)
         self._actions = self.handoff.global_actions if self.rank == 0 else None
         self._graph = bool(graph) and not gloo
+        self.graphed = self._graph
         self._steps = 0
+        self._rgraph = None                 # the captured rollout (ROLLOUT command)
         self._open = True
 
     def _handoff_step(self, actions):
@@ -187,11 +190,32 @@ class ShardedAviaryVecEnv:
         self._steps += 1
         return self.handoff.step(actions)
 
-    def _send(self, cmd):
+    def _send(self, cmd, arg=0):
         if self.world > 1:
             import torch.distributed as dist
-            self._cmd.fill_(cmd)
+            self._cmd[0] = cmd
+            self._cmd[1] = arg
             dist.broadcast(self._cmd, src=0)
+
+    def rollout(self, n_steps, seq):
+        """The learner's rollout of ``n_steps`` hand-off steps as one hipGraph, replayed on every rank:
+        ``seq`` (the learner's body: its policy kernels and ``handoff.step_body`` calls) is captured on
+        the first call, the other ranks capture ``n_steps`` x ``handoff.step_body(None)`` at the same
+        time (``serve``), and later calls replay.  RCCL only (``graph=True``)."""
+        if not self._graph:
+            raise ValueError("rollout() needs graph=True (the RCCL hand-off)")
+        self._send(self.ROLLOUT, n_steps)
+        self._replay_rollout(n_steps, seq)
+
+    def _replay_rollout(self, n_steps, seq):
+        if self._rgraph is None:
+            self._rgraph = torch.cuda.CUDAGraph()
+            with torch.cuda.device(self.sim.device), torch.cuda.graph(self._rgraph):
+                seq()
+            self._rgraph_steps = n_steps
+        elif n_steps != self._rgraph_steps:
+            raise ValueError("a rollout graph replays a fixed number of steps")
+        self._rgraph.replay()
 
     def reset(self):
         self._send(self.RESET)
@@ -213,12 +237,16 @@ class ShardedAviaryVecEnv:
         import torch.distributed as dist
         while True:
             dist.broadcast(self._cmd, src=0)
-            cmd = int(self._cmd.item())
+            cmd, arg = (int(x) for x in self._cmd.tolist())
             if cmd == self.STOP:
+                self._rgraph = None
                 self.handoff.close()
                 break
             if cmd == self.RESET:
                 self.handoff.reset()
+            elif cmd == self.ROLLOUT:
+                h = self.handoff
+                self._replay_rollout(arg, lambda: [h.step_body(None) for _ in range(arg)])
             else:
                 self._handoff_step(None)
         self.local.close()
@@ -228,6 +256,7 @@ class ShardedAviaryVecEnv:
         if self._open:
             if self.rank == 0:
                 self._send(self.STOP)
+            self._rgraph = None
             self.handoff.close()
             self.local.close()
             self._open = False

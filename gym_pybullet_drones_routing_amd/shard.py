@@ -341,6 +341,12 @@ class LearnerHandoff:
     def _stage_bufs(self):
         return (self._h_send, self._h_all) if self._stage else (None, None)
 
+    def step_body(self, src):
+        """Steps 1-5 of one hand-off step on the current stream (for a caller that captures them
+        into its own graph, e.g. examples/learn.py's fused rollout); ``src``: the learner's
+        [E, D, A] float32 actions (None elsewhere)."""
+        self._step_body(src)
+
     def _step_body(self, src):
         self._scatter_actions(src)
         self.sim.step(self.local_actions, terminal_obs=self.terminal_obs)

@@ -27,6 +27,10 @@
  *   gpd_set_pid_params <- BaseControl.setPIDCoefficients()   control/BaseControl.py:138-177
  *   gpd_get/set_ctrl_state <- the per-drone DSLPIDControl attributes integral_pos_e,
  *                        integral_rpy_e, last_rpy (control/DSLPIDControl.py:65-78)
+ *   gpd_pack_layout_of / gpd_handoff_pack / gpd_handoff_unpack <- the hand-off of the
+ *                        vectorised step to the learner across GPUs (the caller SB3 runs in one
+ *                        process in examples/learn.py:52-94): obs, reward, dones and
+ *                        infos["terminal_observation"] of every rank's env shard
  *
  * Conventions
  *   - All array arguments are DEVICE pointers (hipMalloc'd memory, e.g. a torch tensor's

@@ -149,8 +149,10 @@ def test_drone_contact_resynced(prec, D):
                tuning=tuning)
     err = resynced_substep_errors(sim, env, rpms)
     sep = np.linalg.norm(env._b_pos[0] - env._b_pos[1])
+    big = np.argwhere(err > 1e-3)
     print(f"\n[parity] drone contact D={D} {prec}: max {err.max():.3e} median {np.median(err):.3e} "
-          f"(pair 0 separation after {T} substeps {sep:.4f} m)")
+          f"(pair 0 separation after {T} substeps {sep:.4f} m); {len(big)} of {err.size} drone-substeps above "
+          f"1e-3 at (substep, drone) {big[:12].tolist()}")
     if prec == "f64":
         assert err.max() <= 1e-10
     elif D < 8:

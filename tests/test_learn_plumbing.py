@@ -186,20 +186,21 @@ def test_fused_rollout_matches_torch_rollout(multi):
     import torch
     from gym_pybullet_drones_routing_amd.enums import Physics
     dev = torch.device("cuda:0")
-    E, T, gamma, lam = 256, 24, 0.99, 0.95
+    E, T, gamma, lam = 256, 80, 0.99, 0.95
     env = learn.make_env(multi, E, learn.DEFAULT_ACT, Physics.PYB, dev)
     sim = env.sim
     n_obs, n_act = sim.drones_per_env * sim.obs_width, sim.drones_per_env * sim.act_width
     torch.manual_seed(1)
     pol = learn.ActorCritic(n_obs, n_act).to(dev)
     with torch.no_grad():
-        pol.log_std.fill_(0.3)                      # wide actions: many truncations to bootstrap
+        pol.log_std.fill_(0.3)
+        pol.pi[4].bias.fill_(1.5)                   # climbing at +5 % thrust: z > 2 truncates after ~60 steps
     env.reset()
     blob, pack0 = sim.save_state(), sim.out_pack.clone()
     bufs = {n: torch.zeros((T, E) + s, device=dev) for n, s in
             (("obs", (n_obs,)), ("act", (n_act,)), ("logp", ()), ("val", ()), ("rew", ()), ("done", ()),
              ("adv", ()), ("ret", ()))}
-    fr = learn.FusedRollout(pol, sim, T, gamma, lam, 7, bufs)
+    fr = learn.FusedRollout(pol, env, T, gamma, lam, 7, bufs)
     with torch.no_grad():
         fr._seq()                                   # eager launches (the graph is tested in test_gpu_policy)
     torch.cuda.synchronize()
