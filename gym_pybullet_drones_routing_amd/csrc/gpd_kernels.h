@@ -328,10 +328,10 @@ __device__ __forceinline__ void plane_space(const R n[3], R p[3], R q[3]) {
 // ---- narrowphase (oracle/bullet_mb.py core_pair / rim_newton / rim_closest / pair_geometry / face_points)
 // The closest points of the margin-shrunk cores, converged: the near caps' centres, the lateral
 // surfaces along the axes' closest points (closed forms), and the four rim circles against the other
-// cylinder - trust-region Newton on the rim angle from each of 8 start azimuths, the smallest
+// cylinder - trust-region Newton on the rim angle from each of 4 start azimuths (0 / 90 / 180 / 270 deg), the smallest
 // squared distance per rim; the first candidate within the tie of the closest wins.  Everything in
 // B's frame (btPlaneSpace1(aB), aB); B's rims in A's frame (btPlaneSpace1 of A).  A pass's near
-// pairs split into 32 tasks each (4 rims x 8 starts) over the wave's lanes (dc_narrow_pass): a
+// pairs split into 16 tasks each (4 rims x 4 starts) over the wave's lanes (dc_narrow_pass): a
 // sparse wave (one or two near pairs, the common case) runs ONE Newton chain per lane.
 template <typename R> struct NpTol;
 template <> struct NpTol<double> { static constexpr double accept = 1e-10, same = 1e-4, tie = 1e-7; };   // RIM_ACCEPT, RIM_SAME, PAIR_TIE
@@ -1113,8 +1113,8 @@ __device__ __forceinline__ void eres_max(DcLds<R>& L, int env, R rr) {
     atomicMax(reinterpret_cast<unsigned int*>(&L.eres[env]), (unsigned int)__float_as_uint((float)rr));
 }
 // The narrowphases of a pass's nthis near pairs (L.nsij[0..nthis)): bullet_mb.pair_geometry per pair,
-// its 4 x 8 rim Newton chains as 32 tasks over the lanes (task t: slot t / 32, rim (t / 8) % 4,
-// start t % 8; the best start per rim by a butterfly over 8 lanes, ties to the lower start), the
+// its 4 x 4 rim Newton chains as 16 tasks over the lanes (task t: slot t / 16, rim (t / 4) % 4,
+// start (t % 4) * 90 deg; the best start per rim by a butterfly over 4 lanes, ties to the lower start), the
 // closed-form candidates and the selection by the pair's own lane (lane = slot), margin level by
 // margin level while some pair's cores overlap; then the fallback and the face manifold.  Lane
 // ln < nthis stages its pair's result in L.st and its face-point mask in L.nsp[ln] and returns its
@@ -1147,7 +1147,7 @@ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthis) {
   R yl[3] = {R(0), R(0), R(0)};
   L.npdone[ln] = found ? 1 : 0;
   wave_lds_sync();
-  const int ntask = nthis * 32;
+  const int ntask = nthis * 16;
 #pragma unroll 1
   for (int lv = 0; lv < 4; ++lv) {
     if (__ballot(!found) == 0ull) break;
@@ -1155,7 +1155,8 @@ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthis) {
 #pragma unroll 1
     for (int t0 = 0; t0 < ntask; t0 += kWave) {
       const int t = t0 + ln;
-      const int slot = (t >> 5) & 63, rim = (t >> 3) & 3, k = t & 7;
+      // task t: slot t / 16, rim (t / 4) % 4, start (t % 4) * 90 deg (bullet_mb.RIM_STARTS)
+      const int slot = (t >> 4) & 63, rim = (t >> 2) & 3, k = (t & 3) * 2;
       R f = R(INFINITY), x[3] = {R(0), R(0), R(0)}, y[3] = {R(0), R(0), R(0)};
       bool need = false;
       if (t < ntask && !L.npdone[slot]) {
@@ -1175,13 +1176,13 @@ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthis) {
       // the rim's result: the lowest start within RIM_SAME of the group's smallest f (bullet_mb.rim_closest)
       R fmin = f;
 #pragma unroll
-      for (int o = 1; o < 8; o <<= 1) fmin = g_min1(fmin, __shfl_xor(fmin, o));
+      for (int o = 1; o < 4; o <<= 1) fmin = g_min1(fmin, __shfl_xor(fmin, o));
       const unsigned long long near = __ballot(f <= fmin * (R(1) + NpTol<R>::same));
-      const int g0 = ln & ~7;
-      const int src = g0 + __builtin_ctz((unsigned)((near >> g0) & 0xffull) | 0x100u);
+      const int g0 = ln & ~3;
+      const int src = g0 + __builtin_ctz((unsigned)((near >> g0) & 0xfull) | 0x10u);
 #pragma unroll
       for (int e = 0; e < 3; ++e) { x[e] = __shfl(x[e], src); y[e] = __shfl(y[e], src); }
-      if (t < ntask && k == 0) {
+      if (t < ntask && (t & 3) == 0) {
 #pragma unroll
         for (int e = 0; e < 3; ++e) { L.DC_RIM(rim, e)[slot] = x[e]; L.DC_RIM(rim, 3 + e)[slot] = y[e]; }
         L.DC_RIM(rim, 6)[slot] = need ? R(0) : R(INFINITY);   // a rim the pair does not need

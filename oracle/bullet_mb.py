@@ -315,7 +315,9 @@ CORE_MARGINS = (0.001, 0.003, 0.006, 0.011)   # core shrink per level (the first
 CORE_SEP = 1e-4             # core distance below which a level has no well-conditioned normal
 SAT_SLACK = 1e-9            # the broadphase's separating-axis reject keeps this much against rounding
 SIMDSQRT12 = 0.7071067811865475244008443621048490
-RIM_SAMPLES = 8             # start azimuths per rim circle (k * 45 deg in btPlaneSpace1 of the axis)
+RIM_SAMPLES = 8             # the azimuth grid (k * 45 deg in btPlaneSpace1 of the axis): the first trust radius
+RIM_STARTS = (0, 2, 4, 6)   # the Newton starts on it (0 / 90 / 180 / 270 deg; round 5 ran all 8: the same
+                            # accuracy bound at half the chains, tests/test_oracle_drone_contact.py)
 RIM_ITERS = 8               # trust-region Newton steps from each start azimuth
 RIM_ACCEPT = 1e-10          # a step must lower the squared distance by this fraction (rounding-proof)
 RIM_SAME = 1e-4             # starts whose squared distances agree to this fraction count as one minimum (sized
@@ -452,11 +454,11 @@ def rim_closest(C, e1, e2, r, h):
     the axial cylinder (centre 0, axis z, radius r, half-height h), and that cylinder's point.
     The rim's distance is not convex in the angle (two local minima on nearly parallel stacked
     faces, a kink where the rim point crosses the other cylinder's edge), so Newton runs from each of
-    RIM_SAMPLES azimuths (rim_newton) and the lowest start whose squared distance is within the
+    the RIM_STARTS azimuths (rim_newton) and the lowest start whose squared distance is within the
     relative RIM_SAME of the smallest wins: chains that reached one minimum agree on f to rounding
     but on the point only to ~sqrt(RIM_ACCEPT) (a flat minimum), so a plain argmin would pick its
-    chain by rounding noise.  On the GPU the 8 x 4 starts of a pair run on 32 lanes at once."""
-    out = [rim_newton(C, e1, e2, r, h, RIM_COS[k], RIM_SIN[k]) for k in range(RIM_SAMPLES)]
+    chain by rounding noise.  On the GPU the 4 x 4 starts of a pair run on 16 lanes at once."""
+    out = [rim_newton(C, e1, e2, r, h, RIM_COS[k], RIM_SIN[k]) for k in RIM_STARTS]
     fmin = min(o[0] for o in out)
     k = next(i for i, o in enumerate(out) if o[0] <= fmin * (1.0 + RIM_SAME))
     return out[k][1], out[k][2]

@@ -2,7 +2,7 @@
 back-to-back launches (HIP events), for the bench's shapes, split by what the call does:
 deterministic forward, sampled forward, forward + the previous step's bootstrap, bootstrap only,
 and torch's forward of the same networks beside it.
-    python scripts/policy_probe.py [n_envs]"""
+    python scripts/policy_probe.py [n_envs | sweep]"""
 import math
 import os
 import sys
@@ -41,7 +41,7 @@ def per_launch_us(fn, n=200):
 
 def main():
     from gym_pybullet_drones_routing_amd.policy import MlpPolicyKernel
-    E = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    E = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 4096
     dev = torch.device("cuda:0")
     for n_obs, n_act in ((72, 4), (27, 1)):
         torch.manual_seed(0)
@@ -72,5 +72,25 @@ def main():
               f"; {macs / 1e6:.1f} M MACs -> {2 * macs / (res['forward_det'] * 1e-6) / 1e12:.2f} TFLOP/s", flush=True)
 
 
+def sweep():
+    """forward_det and critic_only against the batch size: a flat curve = fixed latency, a linear
+    one = throughput."""
+    from gym_pybullet_drones_routing_amd.policy import MlpPolicyKernel
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    m = ac(72, 4, dev)
+    k = MlpPolicyKernel(m, seed=1)
+    for E in (16, 256, 1024, 4096, 16384, 65536):
+        obs = torch.randn((E, 72), device=dev)
+        act = torch.zeros((E, 4), device=dev)
+        bv = torch.zeros(E, device=dev)
+        fd = per_launch_us(lambda: k.step(obs, act, None, None, None, bv, deterministic=True), 100)
+        co = per_launch_us(lambda: k.step(obs, buf_val=bv), 100)
+        print(f"[policy-sweep] E={E}: forward_det {fd:.2f} us, critic_only {co:.2f} us", flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "sweep":
+        sweep()
+    else:
+        main()
