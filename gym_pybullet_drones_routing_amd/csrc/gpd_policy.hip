@@ -5,23 +5,27 @@
 // SB3 MlpPolicy), samples Normal(mu, exp(log_std)), clips to the Box and writes the rollout
 // buffer; after env.step it bootstraps time-limit truncations with V(terminal_observation).
 // Eager, that is ~25 library launches per step (bench.py rollout leg: 62.9 us of policy beside a
-// 5.9 us env step).  Here it is ONE kernel per step:
+// 5.9 us env step).  Here it is ONE kernel per step.
 //
-//   * a block stages both networks' first two layers in LDS (float4-interleaved so that lane j
-//     reads neuron j's four weights of k..k+3 in one conflict-free ds_read_b128), then loops over
-//     groups of kWaves x kRows rows;
-//   * lane j of a wave is hidden neuron j, for kRows rows at once (register blocking: every
-//     weight read from LDS feeds kRows FMAs); the rows' inputs are broadcast LDS reads;
-//   * the output layers (n_act + 1 dot products of 64) are wave butterfly reductions;
-//   * lane r < kRows then finishes row r: the Philox4x32-10 / Box-Muller sample, the clip, the
-//     Normal log-density written as torch.distributions.Normal.log_prob computes it, the stores.
-//
-// The MLP is VALU f32 FMA work (~12-18 K MACs per row): at 4096 rows a few microseconds, the
-// weight staging (40-75 KB per block from L2) and the layer-to-layer dependency chain dominate.
-// No MFMA: f32 MFMA runs at the VALU's rate on CDNA4 and bf16 would not reproduce the torch
-// forward to f32 rounding.  Built with -ffp-contract=off: the MLP's FMAs are explicit fmaf, and
-// everything written "as torch computes it" (the sample, the log-density, the bootstrap, GAE)
-// rounds every operation as torch's elementwise kernels do.
+// A block of four waves takes groups of 16 rows (the M of v_mfma_f32_16x16x4_f32, f32 in / f32
+// accumulate: the f32 rounding the torch forward has, at the f32 VALU's rate but with one
+// 40-cycle dependent step per 4 x 16 x 16 products instead of 16 dependent FMAs).  Wave w owns
+// hidden neurons 16w .. 16w+15 of both layers and both networks:
+//   * its B operands - the slices of W1 and W2 it needs - are loaded ONCE into VGPRs at the start
+//     (no LDS staging: every load in flight at once, one L2 round trip per launch);
+//   * layer 1: the group's input rows, k-major in LDS, are the A operand; tanh(acc + b1) goes to
+//     LDS (the next layer sums over neurons of all four waves);
+//   * layer 2 likewise; its tanh stays in the accumulator registers;
+//   * the output layer (n_act + 1 dot products of 64): per lane the products of its neuron, a
+//     16-lane DPP butterfly per wave (row_mirror, row_half_mirror, two quad_perms: VALU, no LDS)
+//     and the four waves' partial sums added through LDS in wave order;
+//   * then one lane per (row, action): the Philox4x32-10 / Box-Muller sample, the clip, the Normal
+//     log-density written as torch.distributions.Normal.log_prob computes it; one lane per row:
+//     the log-probability sum, the value and the stores.
+// The previous step's time-limit bootstrap runs the critic alone on the group's terminal rows
+// first, only in groups that hold a truncated env.
+// Built with -ffp-contract=off: everything written "as torch computes it" (the sample, the
+// log-density, the bootstrap, GAE) rounds every operation as torch's elementwise kernels do.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -48,10 +52,13 @@ constexpr int kOk = 0, kEinval = -1, kEhip = -2, kEunsupported = -4;   // gpd.h 
   } while (0)
 
 constexpr int H = GPD_POLICY_HIDDEN;
-constexpr int kRows = 4;                // rows per wave pass
-constexpr int kWaves = 4;               // waves per block
+constexpr int kWaves = 4;                      // waves per block: neurons 16w .. 16w+15 each
 constexpr int kBlock = kWaves * 64;
-constexpr int kGroup = kWaves * kRows;  // rows per block pass
+constexpr int kM = 16;                         // rows per group (MFMA M)
+constexpr int kXs = kM + 1;                    // LDS row stride of the k-major tiles (odd: no bank conflicts)
+constexpr int kRes = 16;                       // LDS stride of a row's outputs (n_act + 1 <= 9)
+constexpr int kMaxKq = GPD_POLICY_MAX_OBS / 4;
+typedef float f4 __attribute__((ext_vector_type(4)));
 
 struct Net {
   const float *w1, *b1, *w2, *b2, *w3, *b3;
@@ -89,279 +96,260 @@ __device__ inline float std_normal(uint64_t seed, uint64_t call, int row, int a)
   uint32_t c[4] = {(uint32_t)row, (uint32_t)(a >> 2), (uint32_t)call, (uint32_t)(call >> 32)};
   philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
   const int p = (a & 3) >> 1;                       // Box-Muller pair (c0, c1) or (c2, c3)
-  const float u0 = u01(c[2 * p]), u1 = u01(c[2 * p + 1]);
+  const float u0 = u01(p ? c[2] : c[0]), u1 = u01(p ? c[3] : c[1]);
   const float rad = sqrtf(-2.0f * logf(u0));
   float s, co;
   sincosf(6.283185307179586f * u1, &s, &co);
   return (a & 1) ? rad * s : rad * co;
 }
 
-__device__ inline float wave_sum(float v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+template <int CTRL>
+__device__ inline float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// the sum over the 16 lanes of a DPP row (lanes 16r .. 16r+15), in every lane of the row
+__device__ inline float row16_sum(float v) {
+  v += dpp<0x140>(v);   // row_mirror: i <-> 15 - i
+  v += dpp<0x141>(v);   // row_half_mirror: i <-> 7 - i within each half
+  v += dpp<0x4E>(v);    // quad_perm [2, 3, 0, 1]
+  v += dpp<0xB1>(v);    // quad_perm [1, 0, 3, 2]
   return v;
 }
 
-// LDS layout (floats): w1 pi | w1 vf  [kq][64][4] each,  w2 pi | w2 vf  [16][64][4] each,
-// then per wave: x [kRows][kq*4], h pi [kRows][64], h vf [kRows][64], res [kRows][kRes]
 struct Lds {
-  float4 *w1p, *w1v, *w2p, *w2v;
-  float *x, *hp, *hv, *res;   // res: [kRows][kRes] per wave, the output sums handed to lane r
+  float xt[kMaxKq * 4 * kXs];      // the group's input rows, k-major: xt[k * kXs + row]
+  float h1v[H * kXs], h1p[H * kXs];   // layer-1 activations, neuron-major
+  float part[kWaves][kM][kRes];    // per wave: its 16 neurons' share of the output sums
+  float res[kM][kRes];             // per row: mu[0..n_act), value at n_act
+  float lp[kM][GPD_POLICY_MAX_ACT];
+  float b3[GPD_POLICY_MAX_ACT + 1];   // output biases: mu_0 .. mu_{n_act-1}, value
 };
-constexpr int kRes = 16;
 
-// Weight staging: row-major nn.Linear weights [64][n] -> LDS [n/4][64][4] (float4 q of neuron j
-// at q * 64 + j).  Element idx -> (q = idx / 64, j = idx % 64): consecutive lanes write consecutive
-// LDS float4s; every lane issues all its loads before its first store, so a block's ~70 KB arrive
-// in one L2 round trip instead of one per loop iteration (the first build's scalar loop of
-// dependent load -> store pairs took ~20 us of a 24 us launch).
-template <int U>
-__device__ inline void stage_rows4(float4* __restrict__ dst, const float* __restrict__ w, int n, int kq) {
-  const int total = kq * H;
-  const bool vec = (n & 3) == 0 && ((uintptr_t)w & 15) == 0;
-  for (int base = threadIdx.x; base < total; base += U * kBlock) {
-    float4 v[U];
+// This lane's slice of the weights: B operands W1[j][4s + g] (s < KQ), W2[j][4s + g], output
+// weights W3[o][j], biases of neuron j (j = 16 w + (l & 15), g = l >> 4).
+template <int NA, int KQ>
+struct Regs {
+  float w1v[KQ], w1p[KQ], w2v[16], w2p[16], w3p[NA], w3v, b1v, b1p, b2v, b2p;
+  float sc;           // exp(log_std[a]) of this lane's action a = threadIdx.x % NA (sampling lanes)
+};
+
+template <int NA, int KQ>
+__device__ inline void load_regs(const Args& A, Regs<NA, KQ>& R, int j, int g) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int idx = base + u * kBlock;
-      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (idx < total) {
-        const int q = idx >> 6, j = idx & 63, k = 4 * q;
-        const float* src = w + (size_t)j * n + k;
-        if (vec) {
-          v[u] = *reinterpret_cast<const float4*>(src);
-        } else {
-          v[u].x = src[0];
-          v[u].y = k + 1 < n ? src[1] : 0.0f;
-          v[u].z = k + 2 < n ? src[2] : 0.0f;
-          v[u].w = k + 3 < n ? src[3] : 0.0f;
-        }
-      }
-    }
+  for (int s = 0; s < KQ; ++s) {
+    const int k = 4 * s + g;
+    const bool ok = s < A.kq && k < A.n_obs;
+    R.w1v[s] = ok ? A.vf.w1[j * A.n_obs + k] : 0.0f;
+    R.w1p[s] = ok && A.actor ? A.pi.w1[j * A.n_obs + k] : 0.0f;
+  }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int idx = base + u * kBlock;
-      if (idx < total) dst[idx] = v[u];
+  for (int s = 0; s < 16; ++s) {
+    R.w2v[s] = A.vf.w2[j * H + 4 * s + g];
+    R.w2p[s] = A.actor ? A.pi.w2[j * H + 4 * s + g] : 0.0f;
+  }
+#pragma unroll
+  for (int a = 0; a < NA; ++a) R.w3p[a] = A.actor ? A.pi.w3[a * H + j] : 0.0f;
+  R.w3v = A.vf.w3[j];
+  R.b1v = A.vf.b1[j]; R.b2v = A.vf.b2[j];
+  R.b1p = A.actor ? A.pi.b1[j] : 0.0f;
+  R.b2p = A.actor ? A.pi.b2[j] : 0.0f;
+  R.sc = A.actor ? expf(A.log_std[threadIdx.x % NA]) : 1.0f;
+}
+
+// A group's rows [row0, row0 + 16) of `src` (n_obs wide) in registers (element idx = threadIdx.x +
+// u * kBlock of the row-major 16 x kq*4 tile; zero past n_rows / n_obs): issued together with
+// everything else the group needs, so a group costs one memory round trip.
+template <int KQ>
+struct RowRegs {
+  static constexpr int U = (kM * KQ * 4 + kBlock - 1) / kBlock;
+  float v[U];
+};
+template <int KQ>
+__device__ inline void load_rows(RowRegs<KQ>& X, const Args& A, const float* __restrict__ src, int row0) {
+  const int w4 = A.kq * 4;
+#pragma unroll
+  for (int u = 0; u < RowRegs<KQ>::U; ++u) {
+    const int idx = threadIdx.x + u * kBlock;
+    const int i = idx / w4, k = idx - i * w4;
+    const int row = row0 + i;
+    X.v[u] = (idx < kM * w4 && row < A.n_rows && k < A.n_obs) ? src[(size_t)row * A.n_obs + k] : 0.0f;
+  }
+}
+// ... -> L.xt (k-major, conflict-free writes: odd row stride); `copy` (nullable) receives the rows (buf_obs)
+template <int KQ>
+__device__ inline void stage_rows(Lds& L, const Args& A, const RowRegs<KQ>& X, int row0, float* copy) {
+  const int w4 = A.kq * 4;
+#pragma unroll
+  for (int u = 0; u < RowRegs<KQ>::U; ++u) {
+    const int idx = threadIdx.x + u * kBlock;
+    if (idx < kM * w4) {
+      const int i = idx / w4, k = idx - i * w4;
+      const int row = row0 + i;
+      L.xt[k * kXs + i] = X.v[u];
+      if (copy && row < A.n_rows && k < A.n_obs) copy[(size_t)row * A.n_obs + k] = X.v[u];
     }
   }
 }
 
-// hidden layers of one network for the wave's kRows rows: x (LDS rows) -> h2 in `h` (lane = neuron)
-struct Bias {
-  float p1, v1, p2, v2;   // neuron `lane`'s first / second layer biases (actor, critic)
-};
-template <bool BOTH>
-__device__ inline void hidden(const Lds& s, const Args& A, const Bias& B, float (&hp)[kRows], float (&hv)[kRows],
-                              int lane) {
-  float ap[kRows], av[kRows];
-  const float bp = B.p1, bv = B.v1;
+// The group's forward pass (rows in L.xt, staged and synchronised by the caller): L.res[row][a] =
+// mu_a (BOTH), L.res[row][NA] = the value.  Ends synchronised.
+template <int NA, int KQ, bool BOTH>
+__device__ inline void forward(Lds& L, const Args& A, const Regs<NA, KQ>& R, int w, int l) {
+  const int g = l >> 4, i = l & 15, j = 16 * w + i;
+  f4 av = {0.f, 0.f, 0.f, 0.f}, ap = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) { ap[r] = bp; av[r] = bv; }
-  const float4* x4 = (const float4*)s.x;
-  for (int q = 0; q < A.kq; ++q) {
-    const float4 wv = s.w1v[q * H + lane];
-    float4 wp = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (BOTH) wp = s.w1p[q * H + lane];
-#pragma unroll
-    for (int r = 0; r < kRows; ++r) {
-      const float4 x = x4[r * A.kq + q];
-      av[r] = fmaf(wv.x, x.x, av[r]); av[r] = fmaf(wv.y, x.y, av[r]);
-      av[r] = fmaf(wv.z, x.z, av[r]); av[r] = fmaf(wv.w, x.w, av[r]);
-      if (BOTH) {
-        ap[r] = fmaf(wp.x, x.x, ap[r]); ap[r] = fmaf(wp.y, x.y, ap[r]);
-        ap[r] = fmaf(wp.z, x.z, ap[r]); ap[r] = fmaf(wp.w, x.w, ap[r]);
-      }
+  for (int s = 0; s < KQ; ++s) {
+    if (s < A.kq) {
+      const float x = L.xt[(4 * s + g) * kXs + i];              // A[row i][k = 4s + g]
+      av = __builtin_amdgcn_mfma_f32_16x16x4f32(x, R.w1v[s], av, 0, 0, 0);
+      if (BOTH) ap = __builtin_amdgcn_mfma_f32_16x16x4f32(x, R.w1p[s], ap, 0, 0, 0);
     }
   }
+  // D[row 4g + r][col i] = neuron j of row 4g + r
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) {
-    s.hv[r * H + lane] = tanhf(av[r]);
-    if (BOTH) s.hp[r * H + lane] = tanhf(ap[r]);
+  for (int r = 0; r < 4; ++r) {
+    L.h1v[j * kXs + 4 * g + r] = tanhf(av[r] + R.b1v);
+    if (BOTH) L.h1p[j * kXs + 4 * g + r] = tanhf(ap[r] + R.b1p);
   }
   __syncthreads();
-  const float b2p = B.p2, b2v = B.v2;
+  av = f4{0.f, 0.f, 0.f, 0.f};
+  ap = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) { ap[r] = b2p; av[r] = b2v; }
-  const float4* hv4 = (const float4*)s.hv;
-  const float4* hp4 = (const float4*)s.hp;
-#pragma unroll 4
-  for (int q = 0; q < H / 4; ++q) {
-    const float4 wv = s.w2v[q * H + lane];
-    float4 wp = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (BOTH) wp = s.w2p[q * H + lane];
+  for (int s = 0; s < 16; ++s) {
+    av = __builtin_amdgcn_mfma_f32_16x16x4f32(L.h1v[(4 * s + g) * kXs + i], R.w2v[s], av, 0, 0, 0);
+    if (BOTH) ap = __builtin_amdgcn_mfma_f32_16x16x4f32(L.h1p[(4 * s + g) * kXs + i], R.w2p[s], ap, 0, 0, 0);
+  }
+  // output layer: this wave's 16 neurons' products, summed over the DPP row (the 16 lanes of one g)
 #pragma unroll
-    for (int r = 0; r < kRows; ++r) {
-      const float4 y = hv4[r * (H / 4) + q];
-      av[r] = fmaf(wv.x, y.x, av[r]); av[r] = fmaf(wv.y, y.y, av[r]);
-      av[r] = fmaf(wv.z, y.z, av[r]); av[r] = fmaf(wv.w, y.w, av[r]);
+  for (int r = 0; r < 4; ++r) {
+    const float hv = tanhf(av[r] + R.b2v);
+    const float sv = row16_sum(R.w3v * hv);
+    float sp[NA];
+    if (BOTH) {
+      const float hp = tanhf(ap[r] + R.b2p);
+#pragma unroll
+      for (int a = 0; a < NA; ++a) sp[a] = row16_sum(R.w3p[a] * hp);
+    }
+    if (i == 0) {
+      L.part[w][4 * g + r][NA] = sv;
       if (BOTH) {
-        const float4 z = hp4[r * (H / 4) + q];
-        ap[r] = fmaf(wp.x, z.x, ap[r]); ap[r] = fmaf(wp.y, z.y, ap[r]);
-        ap[r] = fmaf(wp.z, z.z, ap[r]); ap[r] = fmaf(wp.w, z.w, ap[r]);
+#pragma unroll
+        for (int a = 0; a < NA; ++a) L.part[w][4 * g + r][a] = sp[a];
       }
     }
   }
+  __syncthreads();
+  // the four waves' shares, in wave order, plus the output biases
+  const int t = threadIdx.x;
+  if (t < kM * (NA + 1)) {
+    const int row = t / (NA + 1), o = t - row * (NA + 1);
+    if (BOTH || o == NA) {
+      float acc = L.part[0][row][o];
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) {
-    hv[r] = tanhf(av[r]);
-    hp[r] = BOTH ? tanhf(ap[r]) : 0.0f;
-  }
-  __syncthreads();   // the next pass rewrites x / h of this wave
-}
-
-// rows [row0, row0 + kRows) of `src` (n_obs wide) -> the wave's x tile (zero past n_rows / n_obs);
-// `copy` (nullable) receives the same rows (buf_obs)
-__device__ inline void load_rows(const Lds& s, const Args& A, const float* __restrict__ src, int row0, int lane,
-                                 float* copy) {
-  const int w = A.kq * 4;
-  for (int i = lane; i < kRows * w; i += 64) {
-    const int r = i / w, k = i - r * w;
-    const int row = row0 + r;
-    float v = 0.0f;
-    if (row < A.n_rows && k < A.n_obs) {
-      v = src[(size_t)row * A.n_obs + k];
-      if (copy) copy[(size_t)row * A.n_obs + k] = v;
+      for (int ww = 1; ww < kWaves; ++ww) acc += L.part[ww][row][o];
+      L.res[row][o] = acc + L.b3[o];   // (an index into R, even a select chain, puts R in scratch)
     }
-    s.x[i] = v;
   }
+  __syncthreads();
 }
 
-template <int NA>
-__global__ void __launch_bounds__(kBlock) rollout_kernel(Args A) {
-  extern __shared__ float4 lds4[];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  Lds s;
-  s.w1p = lds4;
-  s.w1v = s.w1p + A.kq * H;
-  s.w2p = s.w1v + A.kq * H;
-  s.w2v = s.w2p + (H / 4) * H;
-  float* scratch = (float*)(s.w2v + (H / 4) * H);
-  const int per_wave = kRows * A.kq * 4 + 2 * kRows * H + kRows * kRes;
-  s.x = scratch + wave * per_wave;
-  s.hp = s.x + kRows * A.kq * 4;
-  s.hv = s.hp + kRows * H;
-  s.res = s.hv + kRows * H;
-
-  stage_rows4<8>(s.w1v, A.vf.w1, A.n_obs, A.kq);
-  stage_rows4<4>(s.w2v, A.vf.w2, H, H / 4);
-  if (A.actor) {
-    stage_rows4<8>(s.w1p, A.pi.w1, A.n_obs, A.kq);
-    stage_rows4<4>(s.w2p, A.pi.w2, H, H / 4);
+// a group's loads: its terminal rows, flags and rewards (bootstrap) and its observation rows
+template <int KQ>
+__device__ inline void issue_group(const Args& A, RowRegs<KQ>& X, RowRegs<KQ>& TX, float& rw, bool& te, bool& tr,
+                                   int row0, int t) {
+  if (A.reward) {
+    load_rows(TX, A, A.tobs, row0);
+    const bool mine = t < kM && row0 + t < A.n_rows;
+    rw = mine ? A.reward[row0 + t] : 0.0f;
+    te = mine && A.term[row0 + t];
+    tr = mine && A.trunc[row0 + t];
   }
+  if (A.forward) load_rows(X, A, A.obs, row0);
+}
+
+template <int NA, int KQ>
+__global__ void __launch_bounds__(kBlock) rollout_kernel(Args A) {
+  __shared__ Lds L;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, t = threadIdx.x;
   uint64_t seed = 0, call = 0;
   if (A.sample) { seed = A.rng[0]; call = A.rng[1]; }
-  Bias B;
-  B.v1 = A.vf.b1[lane]; B.v2 = A.vf.b2[lane];
-  B.p1 = A.actor ? A.pi.b1[lane] : 0.0f;
-  B.p2 = A.actor ? A.pi.b2[lane] : 0.0f;
-  // output-layer weights of neuron `lane`
-  float w3p[NA], b3p[NA], scale[NA];
-#pragma unroll
-  for (int a = 0; a < NA; ++a) {
-    w3p[a] = A.actor ? A.pi.w3[a * H + lane] : 0.0f;
-    b3p[a] = A.actor ? A.pi.b3[a] : 0.0f;
-    scale[a] = A.actor ? expf(A.log_std[a]) : 1.0f;
-  }
-  const float w3v = A.vf.w3[lane], b3v = A.vf.b3[0];
-  __syncthreads();
-
-  for (int g0 = blockIdx.x * kGroup; g0 < A.n_rows; g0 += gridDim.x * kGroup) {
-    const int row0 = g0 + wave * kRows;
-    float hp[kRows], hv[kRows];
+  // everything a group reads from memory is issued before anything waits for it; the block's
+  // weight slices go out behind the first group's rows, the next group's loads behind this one's
+  // stores (one memory round trip per group)
+  RowRegs<KQ> X, TX;
+  float rw = 0.0f;
+  bool te = false, tr = false;
+  int row0 = blockIdx.x * kM;
+  const int stride = gridDim.x * kM;
+  issue_group(A, X, TX, rw, te, tr, row0, t);
+  Regs<NA, KQ> R;
+  load_regs(A, R, 16 * w + (l & 15), l >> 4);
+  if (t <= NA) L.b3[t] = t == NA ? A.vf.b3[0] : (A.actor ? A.pi.b3[t] : 0.0f);   // read after a barrier
+  for (; row0 < A.n_rows; row0 += stride) {
     // ---- the previous step: time-limit bootstrap + reward / done rows
     if (A.reward) {
-      bool any = false;
-      if (lane < kRows) {
-        const int row = row0 + lane;
-        any = row < A.n_rows && A.trunc[row] && !A.term[row];
-      }
-      if (__syncthreads_or(any)) {
-        load_rows(s, A, A.tobs, row0, lane, nullptr);
+      const bool boot = t < kM && tr && !te;
+      if (__syncthreads_or(boot)) {
+        stage_rows(L, A, TX, row0, nullptr);
         __syncthreads();
-        hidden<false>(s, A, B, hp, hv, lane);
-      } else {
-#pragma unroll
-        for (int r = 0; r < kRows; ++r) hv[r] = 0.0f;
+        forward<NA, KQ, false>(L, A, R, w, l);
       }
-      float vb[kRows];
-#pragma unroll
-      for (int r = 0; r < kRows; ++r) vb[r] = wave_sum(w3v * hv[r]) + b3v;
-      // every lane holds the sums; lane 0 hands them to lane r through LDS (a lane-indexed pick
-      // from registers would go through scratch)
-      if (lane == 0) {
-#pragma unroll
-        for (int r = 0; r < kRows; ++r) s.res[r * kRes] = vb[r];
-      }
-      __syncthreads();
-      if (lane < kRows) {
-        const int row = row0 + lane;
-        if (row < A.n_rows) {
-          const float rw = A.reward[row];
-          const bool te = A.term[row], tr = A.trunc[row];
-          // learn.py: r + gamma * V(terminal_obs) (two roundings; this file has no contraction)
-          A.buf_rew[row] = (tr && !te) ? rw + A.gamma * s.res[lane * kRes] : rw;
-          A.buf_done[row] = (te || tr) ? 1.0f : 0.0f;
-        }
+      if (t < kM && row0 + t < A.n_rows) {
+        // learn.py: r + gamma * V(terminal_obs) (two roundings; this file has no contraction)
+        A.buf_rew[row0 + t] = (tr && !te) ? rw + A.gamma * L.res[t][NA] : rw;
+        A.buf_done[row0 + t] = (te || tr) ? 1.0f : 0.0f;
       }
       __syncthreads();
     }
-    if (!A.forward) continue;
+    if (!A.forward) {
+      if (row0 + stride < A.n_rows) issue_group(A, X, TX, rw, te, tr, row0 + stride, t);
+      continue;
+    }
     // ---- this step: actor + critic on obs
-    load_rows(s, A, A.obs, row0, lane, A.buf_obs);
+    stage_rows(L, A, X, row0, A.buf_obs);
     __syncthreads();
-    if (A.actor) hidden<true>(s, A, B, hp, hv, lane);
-    else hidden<false>(s, A, B, hp, hv, lane);
-    float val[kRows], mu[NA][kRows];
-#pragma unroll
-    for (int r = 0; r < kRows; ++r) {
-      val[r] = wave_sum(w3v * hv[r]) + b3v;
-#pragma unroll
-      for (int a = 0; a < NA; ++a) mu[a][r] = A.actor ? wave_sum(w3p[a] * hp[r]) + b3p[a] : 0.0f;
-    }
-    // lane r < kRows finishes row r; lane 0 hands it the row's sums through LDS
-    if (lane == 0) {
-#pragma unroll
-      for (int r = 0; r < kRows; ++r) {
-        s.res[r * kRes + NA] = val[r];
-#pragma unroll
-        for (int a = 0; a < NA; ++a) s.res[r * kRes + a] = mu[a][r];
+    if (A.actor) forward<NA, KQ, true>(L, A, R, w, l);
+    else forward<NA, KQ, false>(L, A, R, w, l);
+    if (A.actor && t < kM * NA) {   // one lane per (row, action)
+      const int i = t / NA, a = t - i * NA;
+      const int row = row0 + i;
+      const float m = L.res[i][a];
+      const float sc = R.sc;
+      float act = m;
+      // torch Normal.rsample: loc + eps * scale (two roundings: no contraction in this file)
+      if (!A.deterministic) act = m + std_normal(seed, call, row, a) * sc;
+      // torch.distributions.Normal.log_prob:
+      //   -((value - loc) ** 2) / (2 * var) - log(scale) - log(sqrt(2 * pi)),  var = scale ** 2
+      const float d = act - m;
+      L.lp[i][a] = -(d * d) / (2.0f * (sc * sc)) - logf(sc) - 0.91893853320467274f;
+      if (row < A.n_rows) {
+        if (A.buf_act) A.buf_act[(size_t)row * NA + a] = act;
+        if (A.act_env) A.act_env[(size_t)row * NA + a] = fminf(fmaxf(act, -1.0f), 1.0f);
       }
     }
     __syncthreads();
-    if (lane < kRows) {
-      const int row = row0 + lane;
-      const float* my = s.res + lane * kRes;
+    if (t < kM) {
+      const int row = row0 + t;
       if (row < A.n_rows) {
-        if (A.buf_val) A.buf_val[row] = my[NA];
-        if (A.actor) {
+        if (A.buf_val) A.buf_val[row] = L.res[t][NA];
+        if (A.actor && A.buf_logp) {
           float logp = 0.0f;
 #pragma unroll
-          for (int a = 0; a < NA; ++a) {
-            const float m = my[a];
-            float act = m;
-            // torch Normal.rsample: loc + eps * scale (two roundings: no contraction in this file)
-            if (!A.deterministic) act = m + std_normal(seed, call, row, a) * scale[a];
-            // torch.distributions.Normal.log_prob:
-            //   -((value - loc) ** 2) / (2 * var) - log(scale) - log(sqrt(2 * pi)),  var = scale ** 2
-            const float d = act - m;
-            const float lp = -(d * d) / (2.0f * (scale[a] * scale[a])) - logf(scale[a]) - 0.91893853320467274f;
-            logp += lp;
-            if (A.buf_act) A.buf_act[(size_t)row * NA + a] = act;
-            if (A.act_env) A.act_env[(size_t)row * NA + a] = fminf(fmaxf(act, -1.0f), 1.0f);
-          }
-          if (A.buf_logp) A.buf_logp[row] = logp;
+          for (int a = 0; a < NA; ++a) logp += L.lp[t][a];
+          A.buf_logp[row] = logp;
         }
       }
     }
-    __syncthreads();   // res is rewritten by the next pass
+    if (row0 + stride < A.n_rows) issue_group(A, X, TX, rw, te, tr, row0 + stride, t);
+    __syncthreads();   // res / lp are rewritten by the next group
   }
   // the last block to finish advances the call counter (every block has read it above)
   if (A.sample) {
     __syncthreads();
     if (threadIdx.x == 0) {
       __threadfence();
-      const unsigned long long t = atomicAdd((unsigned long long*)&A.rng[2], 1ull);
-      if (t == gridDim.x - 1) {
+      const unsigned long long tk = atomicAdd((unsigned long long*)&A.rng[2], 1ull);
+      if (tk == gridDim.x - 1) {
         A.rng[1] = call + 1;
         A.rng[2] = 0;
         __threadfence();
@@ -392,23 +380,19 @@ __global__ void __launch_bounds__(256) gae_kernel(int T, int n, const float* __r
   }
 }
 
-template <int NA>
-int launch(const Args& A, int grid, size_t lds, hipStream_t st) {
-  // dynamic LDS past 64 KB must be allowed per kernel, up to what this launch needs
-  static size_t allowed = 64 * 1024;
-  if (lds > allowed) {
-    const hipError_t e = hipFuncSetAttribute((const void*)rollout_kernel<NA>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();   // do not leave the error for the next caller's hipGetLastError
-      return fail(kEhip, std::string("hipFuncSetAttribute(rollout_kernel, ") + std::to_string(lds) +
-                             " B of dynamic LDS): " + hipGetErrorString(e));
-    }
-    allowed = lds;
-  }
-  hipLaunchKernelGGL(rollout_kernel<NA>, dim3(grid), dim3(kBlock), lds, st, A);
+template <int NA, int KQ>
+int launch(const Args& A, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((rollout_kernel<NA, KQ>), dim3(grid), dim3(kBlock), 0, st, A);
   HIP_TRY(hipGetLastError());
   return kOk;
+}
+// the weight slices live in VGPRs: the layer-1 slice sized by the obs width's bucket
+template <int NA>
+int launch_kq(const Args& A, int grid, hipStream_t st) {
+  if (A.kq <= 8) return launch<NA, 8>(A, grid, st);
+  if (A.kq <= 16) return launch<NA, 16>(A, grid, st);
+  if (A.kq <= 24) return launch<NA, 24>(A, grid, st);
+  return launch<NA, kMaxKq>(A, grid, st);
 }
 
 }  // namespace
@@ -454,21 +438,18 @@ int gpd_policy_rollout_step(const gpd_mlp_policy* p, int n_rows, const float* ob
     return fail(kEinval, "gpd_policy_rollout_step: the bootstrap needs terminated, truncated, terminal_obs, "
                          "buf_rew and buf_done");
   if (!A.forward && !reward) return fail(kEinval, "gpd_policy_rollout_step: nothing to do (obs and reward NULL)");
-  const size_t lds = sizeof(float) * ((size_t)2 * A.kq * 4 * H + (size_t)2 * H * H +
-                                      (size_t)kWaves * (kRows * A.kq * 4 + 2 * kRows * H + kRows * kRes));
-  static_assert(kRows * 4 <= 64, "rows per pass");
-  const int groups = (n_rows + kGroup - 1) / kGroup;
-  const int grid = groups < 1024 ? groups : 1024;
+  const int groups = (n_rows + kM - 1) / kM;
+  const int grid = groups < 2048 ? groups : 2048;
   hipStream_t st = (hipStream_t)stream;
   switch (p->n_act) {
-    case 1: return launch<1>(A, grid, lds, st);
-    case 2: return launch<2>(A, grid, lds, st);
-    case 3: return launch<3>(A, grid, lds, st);
-    case 4: return launch<4>(A, grid, lds, st);
-    case 5: return launch<5>(A, grid, lds, st);
-    case 6: return launch<6>(A, grid, lds, st);
-    case 7: return launch<7>(A, grid, lds, st);
-    default: return launch<8>(A, grid, lds, st);
+    case 1: return launch_kq<1>(A, grid, st);
+    case 2: return launch_kq<2>(A, grid, st);
+    case 3: return launch_kq<3>(A, grid, st);
+    case 4: return launch_kq<4>(A, grid, st);
+    case 5: return launch_kq<5>(A, grid, st);
+    case 6: return launch_kq<6>(A, grid, st);
+    case 7: return launch_kq<7>(A, grid, st);
+    default: return launch_kq<8>(A, grid, st);
   }
 }
 
