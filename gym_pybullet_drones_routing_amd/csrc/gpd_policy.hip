@@ -123,30 +123,40 @@ struct Lds {
   float res[kM][kRes];             // per row: mu[0..n_act), value at n_act
   float lp[kM][GPD_POLICY_MAX_ACT];
   float b3[GPD_POLICY_MAX_ACT + 1];   // output biases: mu_0 .. mu_{n_act-1}, value
+  unsigned long long call;            // this launch's call counter (thread 0's ticket)
 };
 
-// This lane's slice of the weights: B operands W1[j][4s + g] (s < KQ), W2[j][4s + g], output
-// weights W3[o][j], biases of neuron j (j = 16 w + (l & 15), g = l >> 4).
+// This lane's slice of the weights: B operands W1[j][g KQ + s] (s < KQ), W2[j][16 g + s], output
+// weights W3[o][j], biases of neuron j (j = 16 w + (l & 15), g = l >> 4).  The K index of MFMA
+// step s and operand slot g is g KQ + s (not 4 s + g): a lane's weights of one layer are then
+// contiguous in the row-major nn.Linear weight, so they arrive as float4 loads (a quarter of the
+// load instructions; one scalar load per element took ~2 us of address processing per launch).
 template <int NA, int KQ>
 struct Regs {
   float w1v[KQ], w1p[KQ], w2v[16], w2p[16], w3p[NA], w3v, b1v, b1p, b2v, b2p;
   float sc;           // exp(log_std[a]) of this lane's action a = threadIdx.x % NA (sampling lanes)
 };
 
+template <int N>
+__device__ inline void load_slice(float (&dst)[N], const float* __restrict__ row, int k0, int n, bool on) {
+  // dst[s] = row[k0 + s] (0 past n or when !on); float4 loads when the slice is 16-B aligned
+  if (on && (n & 3) == 0 && (k0 & 3) == 0 && ((uintptr_t)row & 15) == 0 && k0 + N <= n) {
+#pragma unroll
+    for (int q = 0; q < N / 4; ++q) {
+      const float4 v = reinterpret_cast<const float4*>(row + k0)[q];
+      dst[4 * q] = v.x; dst[4 * q + 1] = v.y; dst[4 * q + 2] = v.z; dst[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < N; ++s) dst[s] = on && k0 + s < n ? row[k0 + s] : 0.0f;
+  }
+}
 template <int NA, int KQ>
 __device__ inline void load_regs(const Args& A, Regs<NA, KQ>& R, int j, int g) {
-#pragma unroll
-  for (int s = 0; s < KQ; ++s) {
-    const int k = 4 * s + g;
-    const bool ok = s < A.kq && k < A.n_obs;
-    R.w1v[s] = ok ? A.vf.w1[j * A.n_obs + k] : 0.0f;
-    R.w1p[s] = ok && A.actor ? A.pi.w1[j * A.n_obs + k] : 0.0f;
-  }
-#pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    R.w2v[s] = A.vf.w2[j * H + 4 * s + g];
-    R.w2p[s] = A.actor ? A.pi.w2[j * H + 4 * s + g] : 0.0f;
-  }
+  load_slice<KQ>(R.w1v, A.vf.w1 + (size_t)j * A.n_obs, g * KQ, A.n_obs, true);
+  load_slice<KQ>(R.w1p, A.actor ? A.pi.w1 + (size_t)j * A.n_obs : A.vf.w1, g * KQ, A.n_obs, A.actor);
+  load_slice<16>(R.w2v, A.vf.w2 + (size_t)j * H, 16 * g, H, true);
+  load_slice<16>(R.w2p, A.actor ? A.pi.w2 + (size_t)j * H : A.vf.w2, 16 * g, H, A.actor);
 #pragma unroll
   for (int a = 0; a < NA; ++a) R.w3p[a] = A.actor ? A.pi.w3[a * H + j] : 0.0f;
   R.w3v = A.vf.w3[j];
@@ -166,7 +176,7 @@ struct RowRegs {
 };
 template <int KQ>
 __device__ inline void load_rows(RowRegs<KQ>& X, const Args& A, const float* __restrict__ src, int row0) {
-  const int w4 = A.kq * 4;
+  constexpr int w4 = KQ * 4;   // every k an MFMA step reads (zero past n_obs)
 #pragma unroll
   for (int u = 0; u < RowRegs<KQ>::U; ++u) {
     const int idx = threadIdx.x + u * kBlock;
@@ -178,7 +188,7 @@ __device__ inline void load_rows(RowRegs<KQ>& X, const Args& A, const float* __r
 // ... -> L.xt (k-major, conflict-free writes: odd row stride); `copy` (nullable) receives the rows (buf_obs)
 template <int KQ>
 __device__ inline void stage_rows(Lds& L, const Args& A, const RowRegs<KQ>& X, int row0, float* copy) {
-  const int w4 = A.kq * 4;
+  constexpr int w4 = KQ * 4;
 #pragma unroll
   for (int u = 0; u < RowRegs<KQ>::U; ++u) {
     const int idx = threadIdx.x + u * kBlock;
@@ -199,11 +209,9 @@ __device__ inline void forward(Lds& L, const Args& A, const Regs<NA, KQ>& R, int
   f4 av = {0.f, 0.f, 0.f, 0.f}, ap = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < KQ; ++s) {
-    if (s < A.kq) {
-      const float x = L.xt[(4 * s + g) * kXs + i];              // A[row i][k = 4s + g]
-      av = __builtin_amdgcn_mfma_f32_16x16x4f32(x, R.w1v[s], av, 0, 0, 0);
-      if (BOTH) ap = __builtin_amdgcn_mfma_f32_16x16x4f32(x, R.w1p[s], ap, 0, 0, 0);
-    }
+    const float x = L.xt[(g * KQ + s) * kXs + i];              // A[row i][k = g KQ + s]
+    av = __builtin_amdgcn_mfma_f32_16x16x4f32(x, R.w1v[s], av, 0, 0, 0);
+    if (BOTH) ap = __builtin_amdgcn_mfma_f32_16x16x4f32(x, R.w1p[s], ap, 0, 0, 0);
   }
   // D[row 4g + r][col i] = neuron j of row 4g + r
 #pragma unroll
@@ -216,8 +224,8 @@ __device__ inline void forward(Lds& L, const Args& A, const Regs<NA, KQ>& R, int
   ap = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
-    av = __builtin_amdgcn_mfma_f32_16x16x4f32(L.h1v[(4 * s + g) * kXs + i], R.w2v[s], av, 0, 0, 0);
-    if (BOTH) ap = __builtin_amdgcn_mfma_f32_16x16x4f32(L.h1p[(4 * s + g) * kXs + i], R.w2p[s], ap, 0, 0, 0);
+    av = __builtin_amdgcn_mfma_f32_16x16x4f32(L.h1v[(16 * g + s) * kXs + i], R.w2v[s], av, 0, 0, 0);
+    if (BOTH) ap = __builtin_amdgcn_mfma_f32_16x16x4f32(L.h1p[(16 * g + s) * kXs + i], R.w2p[s], ap, 0, 0, 0);
   }
   // output layer: this wave's 16 neurons' products, summed over the DPP row (the 16 lanes of one g)
 #pragma unroll
@@ -271,8 +279,20 @@ template <int NA, int KQ>
 __global__ void __launch_bounds__(kBlock) rollout_kernel(Args A) {
   __shared__ Lds L;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, t = threadIdx.x;
-  uint64_t seed = 0, call = 0;
-  if (A.sample) { seed = A.rng[0]; call = A.rng[1]; }
+  // rng[1] = call counter << 16 | ticket.  Every block takes a ticket with ONE atomic, which also
+  // returns the call counter; the block that takes the last ticket moves the counter on and the
+  // ticket back to 0 (a non-returning atomic).  All blocks' tickets precede it, and the next launch
+  // on the stream starts after it: no fence, no round trip at the kernel's tail.
+  uint64_t seed = 0;
+  if (A.sample) {
+    seed = A.rng[0];
+    if (threadIdx.x == 0) {
+      const unsigned long long old = atomicAdd((unsigned long long*)&A.rng[1], 1ull);
+      if ((old & 0xffffull) == gridDim.x - 1)
+        atomicAdd((unsigned long long*)&A.rng[1], (1ull << 16) - gridDim.x);
+      L.call = old >> 16;
+    }
+  }
   // everything a group reads from memory is issued before anything waits for it; the block's
   // weight slices go out behind the first group's rows, the next group's loads behind this one's
   // stores (one memory round trip per group)
@@ -317,7 +337,7 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(Args A) {
       const float sc = R.sc;
       float act = m;
       // torch Normal.rsample: loc + eps * scale (two roundings: no contraction in this file)
-      if (!A.deterministic) act = m + std_normal(seed, call, row, a) * sc;
+      if (!A.deterministic) act = m + std_normal(seed, L.call, row, a) * sc;
       // torch.distributions.Normal.log_prob:
       //   -((value - loc) ** 2) / (2 * var) - log(scale) - log(sqrt(2 * pi)),  var = scale ** 2
       const float d = act - m;
@@ -342,19 +362,6 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(Args A) {
     }
     if (row0 + stride < A.n_rows) issue_group(A, X, TX, rw, te, tr, row0 + stride, t);
     __syncthreads();   // res / lp are rewritten by the next group
-  }
-  // the last block to finish advances the call counter (every block has read it above)
-  if (A.sample) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __threadfence();
-      const unsigned long long tk = atomicAdd((unsigned long long*)&A.rng[2], 1ull);
-      if (tk == gridDim.x - 1) {
-        A.rng[1] = call + 1;
-        A.rng[2] = 0;
-        __threadfence();
-      }
-    }
   }
 }
 

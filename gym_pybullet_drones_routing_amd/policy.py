@@ -107,7 +107,16 @@ class MlpPolicyKernel:
         for n, p in zip(names, params):
             setattr(st, n, p.data_ptr())
         self._st = st
-        self.rng = torch.tensor([int(seed), 0, 0], dtype=torch.int64, device=dev)   # {key, call counter, ticket}
+        self.rng = torch.tensor([int(seed), 0, 0], dtype=torch.int64, device=dev)   # {key, counter << 16 | ticket, 0}
+
+    @property
+    def calls(self):
+        """Sampling calls made so far (the device counter; reading it synchronises)."""
+        return int(self.rng[1]) >> 16
+
+    def set_calls(self, n):
+        """Rewind / advance the Philox call counter (the same key and counter draw the same numbers)."""
+        self.rng[1] = int(n) << 16
 
     def _rows(self, t, width, name):
         if t is None:

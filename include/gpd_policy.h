@@ -47,8 +47,9 @@ typedef struct gpd_mlp_policy {
  *   buf_obs / buf_act / buf_logp / buf_val: this step's rollout-buffer rows (each nullable);
  *             buf_val alone (act_env, buf_act, buf_logp NULL) = the critic only (last value)
  *   deterministic: 1 = action = mean (EvalCallback), no sample
- *   rng       device uint64[3] = {seed, call counter, 0}: the Philox4x32-10 key and counter;
- *             every call that samples advances the counter by one (on the device)
+ *   rng       device uint64[3] = {seed, call counter << 16 | ticket, 0}: the Philox4x32-10 key and
+ *             counter; every call that samples advances the counter by one (on the device; the
+ *             ticket is 0 between calls)
  * Previous step (all nullable together; reward == NULL skips the part):
  *   reward [n_rows] f32, terminated / truncated [n_rows] u8 (gpd_step's outputs),
  *   terminal_obs [n_rows][n_obs] (the env's terminal rows), gamma:

@@ -213,7 +213,7 @@ def test_handoff_pack_unpack_kernels_match_host_restatement(W, D):
                                   *[o.data_ptr() for o in outs], None) == _lib.GPD_EINVAL
 
 
-def _fused_rollout_worker(port, q):
+def _fused_rollout_worker(port, q, ack):
     """One-rank RCCL group: examples/learn.py's FusedRollout over ShardedAviaryVecEnv (graph=True,
     collectives forced: the hand-off's RCCL send / recv and gather inside the captured rollout)
     against FusedRollout over one AviaryVecEnv with the same policy and Philox key."""
@@ -245,10 +245,11 @@ def _fused_rollout_worker(port, q):
             got = []
             for _ in range(5):                      # capture + replay, then four more replays
                 fr.run()
-                got.append({n: b.cpu().clone() for n, b in bufs.items()})
+                got.append({n: b.cpu().numpy().copy() for n, b in bufs.items()})
             outs.append(got)
             env.close()
         q.put(outs)
+        ack.wait(120)          # stay alive until the parent has read the whole message
     finally:
         dist.destroy_process_group()
 
@@ -258,13 +259,17 @@ def test_fused_rollout_over_rccl_handoff():
     hipGraph per rank) produces bit-identical rollout buffers to the single-sim fused rollout."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_fused_rollout_worker, args=(_free_port(), q))
+    ack = ctx.Event()
+    p = ctx.Process(target=_fused_rollout_worker, args=(_free_port(), q, ack))
     p.start()
-    outs = _collect(q, [p])
+    try:
+        outs = _collect(q, [p], ack=ack)
+    finally:
+        ack.set()
     single, sharded = outs
     n_done = 0
     for a, b in zip(single, sharded):
         for n in a:
-            assert torch.equal(a[n], b[n]), n
+            np.testing.assert_array_equal(a[n], b[n], err_msg=n)
         n_done += int(a["done"].sum())
     assert n_done > 0

@@ -10,7 +10,6 @@ import math
 import os
 import sys
 
-import numpy as np
 import pytest
 import torch
 
@@ -56,7 +55,7 @@ def test_forward_matches_torch(n_obs, n_act, E):
     assert torch.equal(act_env, buf_act.clamp(-1, 1))
     lp = torch.distributions.Normal(mu, std).log_prob(mu).sum(-1)
     torch.testing.assert_close(buf_logp, lp, rtol=1e-6, atol=1e-5)
-    assert int(k.rng[1]) == 0          # deterministic calls draw nothing
+    assert k.calls == 0 and int(k.rng[1]) == 0      # deterministic calls draw nothing
 
 
 @pytest.mark.parametrize("n_obs,n_act", [(27, 1), (72, 4), (144, 8)])
@@ -74,7 +73,7 @@ def test_sample_log_prob_and_counter(n_obs, n_act):
         acts.append((a, lpk))
         envs.append(ae)
     torch.cuda.synchronize()
-    assert int(k.rng[1]) == 3 and int(k.rng[2]) == 0      # one call counter step per sampling call
+    assert k.calls == 3 and int(k.rng[1]) & 0xffff == 0   # one counter step per sampling call, tickets back to 0
     with torch.no_grad():
         mu = pol.pi(obs)
         std = pol.log_std.exp()
@@ -89,7 +88,7 @@ def test_sample_log_prob_and_counter(n_obs, n_act):
         assert torch.equal(ae, a.clamp(-1, 1))
     assert not torch.equal(acts[0][0], acts[1][0])
     # the same key and counter draw the same numbers
-    k.rng[1] = 1
+    k.set_calls(1)
     a2 = torch.zeros((E, n_act), device="cuda")
     k.step(obs, None, None, a2, None, None)
     torch.cuda.synchronize()
@@ -178,7 +177,7 @@ def test_rollout_graph_with_env_step():
     eager = {n: b.clone() for n, b in bufs.items()}
     sim.load_state(blob)
     sim.out_pack.copy_(pack0)
-    k.rng[1] = 0
+    k.set_calls(0)
     gr = torch.cuda.CUDAGraph()
     with torch.cuda.graph(gr):
         seq()
@@ -188,5 +187,5 @@ def test_rollout_graph_with_env_step():
     torch.cuda.synchronize()
     for n in bufs:
         assert torch.equal(bufs[n], eager[n]), n
-    assert int(k.rng[1]) == K
+    assert k.calls == K
     sim.close()
