@@ -22,7 +22,7 @@ GPD_EUNSUPPORTED = -4
 
 GPD_MODEL_CF2X, GPD_MODEL_CF2P, GPD_MODEL_RACE = 0, 1, 2
 GPD_ACT_RPM, GPD_ACT_ONE_D_RPM, GPD_ACT_PID, GPD_ACT_VEL, GPD_ACT_ONE_D_PID = 0, 1, 2, 3, 4
-GPD_ABI_VERSION = 6
+GPD_ABI_VERSION = 7
 CTRL_COMPS = 9  # integral_pos_e(3) integral_rpy_e(3) last_rpy(3)
 GPD_TASK_NONE, GPD_TASK_HOVER, GPD_TASK_MULTIHOVER = 0, 1, 2
 GPD_F_GND, GPD_F_DRAG, GPD_F_DW, GPD_F_GEOM_WRENCH, GPD_F_BULLET, GPD_F_NO_PLANE = 1, 2, 4, 8, 16, 32
@@ -70,7 +70,8 @@ class Config(ctypes.Structure):
                 ("episode_len_sec", ctypes.c_double),
                 ("init_xyzs_host", ctypes.POINTER(ctypes.c_double)),
                 ("init_rpys_host", ctypes.POINTER(ctypes.c_double)),
-                ("drones_per_block", ctypes.c_int), ("step_waves", ctypes.c_int), ("store_policy", ctypes.c_int)]
+                ("drones_per_block", ctypes.c_int), ("step_waves", ctypes.c_int), ("store_policy", ctypes.c_int),
+                ("solver_iterations", ctypes.c_int), ("solver_residual", ctypes.c_double)]
 
 
 class PackLayout(ctypes.Structure):

@@ -199,6 +199,9 @@ Consts<R> make_consts(const gpd_sim* s) {
     c.dd_mu = (R)(0.5 * 0.5);   // drone x drone default friction
   }
   c.iters = 50;              // m_numIterations (pybullet numSolverIterations)
+  // setPhysicsEngineParameter(numSolverIterations=, solverResidualThreshold=) (gpd_config)
+  if (s->cfg.solver_iterations > 0) c.iters = s->cfg.solver_iterations;
+  if (s->cfg.solver_residual != 0.0) c.resid = (R)s->cfg.solver_residual;
 #ifdef GPD_DIAG_RESID
   c.resid = (R)GPD_DIAG_RESID;   // diagnostic builds only (e.g. -1: every solve runs c.iters iterations)
 #endif
@@ -546,6 +549,9 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
   if (C.task == GPD_TASK_HOVER && C.drones_per_env != 1)
     return fail(GPD_EINVAL, "gpd_create: HoverAviary is single-drone (drones_per_env must be 1)");
   if (C.precision != GPD_F32 && C.precision != GPD_F64) return fail(GPD_EINVAL, "gpd_create: bad precision");
+  if (C.solver_iterations < 0 || C.solver_iterations > 1000)
+    return fail(GPD_EINVAL, "gpd_create: solver_iterations must be 0 (default) or in [1, 1000]");
+  if (!std::isfinite(C.solver_residual)) return fail(GPD_EINVAL, "gpd_create: solver_residual must be finite");
   if ((C.physics_flags & GPD_F_BULLET) && C.drones_per_env > kWave && !(C.physics_flags & GPD_F_NO_DRONE_CONTACT))
     return fail(GPD_EUNSUPPORTED,
                 "gpd_create: drone <-> drone contact is implemented for envs of up to 64 drones; pass "

@@ -22,8 +22,10 @@
 //   * then one lane per (row, action): the Philox4x32-10 / Box-Muller sample, the clip, the Normal
 //     log-density written as torch.distributions.Normal.log_prob computes it; one lane per row:
 //     the log-probability sum, the value and the stores.
-// The previous step's time-limit bootstrap runs the critic alone on the group's terminal rows
-// first, only in groups that hold a truncated env.
+// The previous step's time-limit bootstrap, V(terminal row), runs in groups that hold a truncated
+// env: a third MFMA chain (critic weights, terminal rows) beside the actor's and the critic's, in
+// the same layer passes - its instruction sequence is the critic's, so the same bits as a forward
+// of its own, at no extra dependent step.
 // Built with -ffp-contract=off: everything written "as torch computes it" (the sample, the
 // log-density, the bootstrap, GAE) rounds every operation as torch's elementwise kernels do.
 #include <hip/hip_runtime.h>
@@ -118,9 +120,10 @@ __device__ inline float row16_sum(float v) {
 
 struct Lds {
   float xt[kMaxKq * 4 * kXs];      // the group's input rows, k-major: xt[k * kXs + row]
-  float h1v[H * kXs], h1p[H * kXs];   // layer-1 activations, neuron-major
+  float xb[kMaxKq * 4 * kXs];      // its terminal rows (bootstrap), the same layout
+  float h1v[H * kXs], h1p[H * kXs], h1b[H * kXs];   // layer-1 activations, neuron-major
   float part[kWaves][kM][kRes];    // per wave: its 16 neurons' share of the output sums
-  float res[kM][kRes];             // per row: mu[0..n_act), value at n_act
+  float res[kM][kRes];             // per row: mu[0..n_act), value at n_act, V(terminal row) at n_act + 1
   float lp[kM][GPD_POLICY_MAX_ACT];
   float b3[GPD_POLICY_MAX_ACT + 1];   // output biases: mu_0 .. mu_{n_act-1}, value
   unsigned long long call;            // this launch's call counter (thread 0's ticket)
@@ -187,7 +190,7 @@ __device__ inline void load_rows(RowRegs<KQ>& X, const Args& A, const float* __r
 }
 // ... -> L.xt (k-major, conflict-free writes: odd row stride); `copy` (nullable) receives the rows (buf_obs)
 template <int KQ>
-__device__ inline void stage_rows(Lds& L, const Args& A, const RowRegs<KQ>& X, int row0, float* copy) {
+__device__ inline void stage_rows(float* xt, const Args& A, const RowRegs<KQ>& X, int row0, float* copy) {
   constexpr int w4 = KQ * 4;
 #pragma unroll
   for (int u = 0; u < RowRegs<KQ>::U; ++u) {
@@ -195,67 +198,79 @@ __device__ inline void stage_rows(Lds& L, const Args& A, const RowRegs<KQ>& X, i
     if (idx < kM * w4) {
       const int i = idx / w4, k = idx - i * w4;
       const int row = row0 + i;
-      L.xt[k * kXs + i] = X.v[u];
+      xt[k * kXs + i] = X.v[u];
       if (copy && row < A.n_rows && k < A.n_obs) copy[(size_t)row * A.n_obs + k] = X.v[u];
     }
   }
 }
 
-// The group's forward pass (rows in L.xt, staged and synchronised by the caller): L.res[row][a] =
-// mu_a (BOTH), L.res[row][NA] = the value.  Ends synchronised.
-template <int NA, int KQ, bool BOTH>
+// The group's forward pass (rows staged in L.xt / L.xb and synchronised by the caller):
+//   ACT:  the actor on L.xt  -> L.res[row][a] = mu_a
+//   CRIT: the critic on L.xt -> L.res[row][NA] = V(obs)
+//   BOOT: the critic on L.xb -> L.res[row][NA + 1] = V(terminal row)
+// Ends synchronised.
+template <int NA, int KQ, bool ACT, bool CRIT, bool BOOT>
 __device__ inline void forward(Lds& L, const Args& A, const Regs<NA, KQ>& R, int w, int l) {
   const int g = l >> 4, i = l & 15, j = 16 * w + i;
-  f4 av = {0.f, 0.f, 0.f, 0.f}, ap = {0.f, 0.f, 0.f, 0.f};
+  f4 av = {0.f, 0.f, 0.f, 0.f}, ap = {0.f, 0.f, 0.f, 0.f}, ab = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < KQ; ++s) {
-    const float x = L.xt[(g * KQ + s) * kXs + i];              // A[row i][k = g KQ + s]
-    av = __builtin_amdgcn_mfma_f32_16x16x4f32(x, R.w1v[s], av, 0, 0, 0);
-    if (BOTH) ap = __builtin_amdgcn_mfma_f32_16x16x4f32(x, R.w1p[s], ap, 0, 0, 0);
+    const int o = (g * KQ + s) * kXs + i;              // A[row i][k = g KQ + s]
+    if (CRIT || ACT) {
+      const float x = L.xt[o];
+      if (CRIT) av = __builtin_amdgcn_mfma_f32_16x16x4f32(x, R.w1v[s], av, 0, 0, 0);
+      if (ACT) ap = __builtin_amdgcn_mfma_f32_16x16x4f32(x, R.w1p[s], ap, 0, 0, 0);
+    }
+    if (BOOT) ab = __builtin_amdgcn_mfma_f32_16x16x4f32(L.xb[o], R.w1v[s], ab, 0, 0, 0);
   }
   // D[row 4g + r][col i] = neuron j of row 4g + r
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    L.h1v[j * kXs + 4 * g + r] = tanhf(av[r] + R.b1v);
-    if (BOTH) L.h1p[j * kXs + 4 * g + r] = tanhf(ap[r] + R.b1p);
+    if (CRIT) L.h1v[j * kXs + 4 * g + r] = tanhf(av[r] + R.b1v);
+    if (ACT) L.h1p[j * kXs + 4 * g + r] = tanhf(ap[r] + R.b1p);
+    if (BOOT) L.h1b[j * kXs + 4 * g + r] = tanhf(ab[r] + R.b1v);
   }
   __syncthreads();
   av = f4{0.f, 0.f, 0.f, 0.f};
   ap = f4{0.f, 0.f, 0.f, 0.f};
+  ab = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
-    av = __builtin_amdgcn_mfma_f32_16x16x4f32(L.h1v[(16 * g + s) * kXs + i], R.w2v[s], av, 0, 0, 0);
-    if (BOTH) ap = __builtin_amdgcn_mfma_f32_16x16x4f32(L.h1p[(16 * g + s) * kXs + i], R.w2p[s], ap, 0, 0, 0);
+    const int o = (16 * g + s) * kXs + i;
+    if (CRIT) av = __builtin_amdgcn_mfma_f32_16x16x4f32(L.h1v[o], R.w2v[s], av, 0, 0, 0);
+    if (ACT) ap = __builtin_amdgcn_mfma_f32_16x16x4f32(L.h1p[o], R.w2p[s], ap, 0, 0, 0);
+    if (BOOT) ab = __builtin_amdgcn_mfma_f32_16x16x4f32(L.h1b[o], R.w2v[s], ab, 0, 0, 0);
   }
   // output layer: this wave's 16 neurons' products, summed over the DPP row (the 16 lanes of one g)
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const float hv = tanhf(av[r] + R.b2v);
-    const float sv = row16_sum(R.w3v * hv);
-    float sp[NA];
-    if (BOTH) {
+    float sv = 0.0f, sb = 0.0f, sp[NA];
+    if (CRIT) sv = row16_sum(R.w3v * tanhf(av[r] + R.b2v));
+    if (BOOT) sb = row16_sum(R.w3v * tanhf(ab[r] + R.b2v));
+    if (ACT) {
       const float hp = tanhf(ap[r] + R.b2p);
 #pragma unroll
       for (int a = 0; a < NA; ++a) sp[a] = row16_sum(R.w3p[a] * hp);
     }
     if (i == 0) {
-      L.part[w][4 * g + r][NA] = sv;
-      if (BOTH) {
+      if (CRIT) L.part[w][4 * g + r][NA] = sv;
+      if (BOOT) L.part[w][4 * g + r][NA + 1] = sb;
+      if (ACT) {
 #pragma unroll
         for (int a = 0; a < NA; ++a) L.part[w][4 * g + r][a] = sp[a];
       }
     }
   }
   __syncthreads();
-  // the four waves' shares, in wave order, plus the output biases
+  // the four waves' shares, in wave order, plus the output biases (the bootstrap's: the critic's)
   const int t = threadIdx.x;
-  if (t < kM * (NA + 1)) {
-    const int row = t / (NA + 1), o = t - row * (NA + 1);
-    if (BOTH || o == NA) {
+  if (t < kM * (NA + 2)) {
+    const int row = t / (NA + 2), o = t - row * (NA + 2);
+    if ((ACT && o < NA) || (CRIT && o == NA) || (BOOT && o == NA + 1)) {
       float acc = L.part[0][row][o];
 #pragma unroll
       for (int ww = 1; ww < kWaves; ++ww) acc += L.part[ww][row][o];
-      L.res[row][o] = acc + L.b3[o];   // (an index into R, even a select chain, puts R in scratch)
+      L.res[row][o] = acc + L.b3[o < NA + 1 ? o : NA];   // (an index into R, even a select chain, puts R in scratch)
     }
   }
   __syncthreads();
@@ -306,30 +321,30 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(Args A) {
   load_regs(A, R, 16 * w + (l & 15), l >> 4);
   if (t <= NA) L.b3[t] = t == NA ? A.vf.b3[0] : (A.actor ? A.pi.b3[t] : 0.0f);   // read after a barrier
   for (; row0 < A.n_rows; row0 += stride) {
-    // ---- the previous step: time-limit bootstrap + reward / done rows
-    if (A.reward) {
-      const bool boot = t < kM && tr && !te;
-      if (__syncthreads_or(boot)) {
-        stage_rows(L, A, TX, row0, nullptr);
-        __syncthreads();
-        forward<NA, KQ, false>(L, A, R, w, l);
-      }
-      if (t < kM && row0 + t < A.n_rows) {
-        // learn.py: r + gamma * V(terminal_obs) (two roundings; this file has no contraction)
-        A.buf_rew[row0 + t] = (tr && !te) ? rw + A.gamma * L.res[t][NA] : rw;
-        A.buf_done[row0 + t] = (te || tr) ? 1.0f : 0.0f;
-      }
+    // the previous step's time-limit bootstrap (groups holding a truncated env) rides in this
+    // step's forward as a third chain
+    const bool boot = A.reward && __syncthreads_or(t < kM && tr && !te);
+    if (A.forward) stage_rows(L.xt, A, X, row0, A.buf_obs);
+    if (boot) stage_rows(L.xb, A, TX, row0, nullptr);
+    if (A.forward || boot) {
       __syncthreads();
+      if (!A.forward) forward<NA, KQ, false, false, true>(L, A, R, w, l);
+      else if (A.actor && boot) forward<NA, KQ, true, true, true>(L, A, R, w, l);
+      else if (A.actor) forward<NA, KQ, true, true, false>(L, A, R, w, l);
+      else if (boot) forward<NA, KQ, false, true, true>(L, A, R, w, l);
+      else forward<NA, KQ, false, true, false>(L, A, R, w, l);
     }
-    if (!A.forward) {
+    // ---- the previous step's reward / done rows
+    if (A.reward && t < kM && row0 + t < A.n_rows) {
+      // learn.py: r + gamma * V(terminal_obs) (two roundings; this file has no contraction)
+      A.buf_rew[row0 + t] = (tr && !te) ? rw + A.gamma * L.res[t][NA + 1] : rw;
+      A.buf_done[row0 + t] = (te || tr) ? 1.0f : 0.0f;
+    }
+    if (!A.forward) {   // (the next group's first barrier orders these reads before its forward)
       if (row0 + stride < A.n_rows) issue_group(A, X, TX, rw, te, tr, row0 + stride, t);
       continue;
     }
-    // ---- this step: actor + critic on obs
-    stage_rows(L, A, X, row0, A.buf_obs);
-    __syncthreads();
-    if (A.actor) forward<NA, KQ, true>(L, A, R, w, l);
-    else forward<NA, KQ, false>(L, A, R, w, l);
+    // ---- this step: the sample and the rows
     if (A.actor && t < kM * NA) {   // one lane per (row, action)
       const int i = t / NA, a = t - i * NA;
       const int row = row0 + i;

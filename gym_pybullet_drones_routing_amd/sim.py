@@ -159,9 +159,13 @@ class BatchedAviarySim:
         cfg.precision = _lib.GPD_F32 if precision == "f32" else _lib.GPD_F64
         cfg.autoreset = 1 if autoreset else 0
         cfg.episode_len_sec = float(episode_len_sec)
-        # launch tuning (gpd_config: drones_per_block, step_waves, store_policy; 0 = automatic)
+        # launch tuning (gpd_config: drones_per_block, step_waves, store_policy; 0 = automatic) and
+        # the PYB* contact solver's numSolverIterations / solverResidualThreshold (0 = pybullet's)
         for name, val in (tuning or {}).items():
-            if name not in ("drones_per_block", "step_waves", "store_policy"):
+            if name == "solver_residual":
+                cfg.solver_residual = float(val)
+                continue
+            if name not in ("drones_per_block", "step_waves", "store_policy", "solver_iterations"):
                 raise ValueError(f"unknown tuning field {name!r}")
             setattr(cfg, name, int(val))
         keep = []

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GPD_ABI_VERSION 6
+#define GPD_ABI_VERSION 7
 
 /* return codes */
 #define GPD_OK 0
@@ -132,6 +132,12 @@ typedef struct gpd_config {
   int step_waves;            /* plain-DYN single-drone RPM path: 1 single-wave kernel,
                               * 2 pose+rate waves, 3 pose+rate+io waves */
   int store_policy;          /* 1 + write-through mask: bit 0 obs/terminal rows, bit 1 state */
+  /* Contact solver of the PYB* modes, as pybullet's setPhysicsEngineParameter sets it
+   * (numSolverIterations, solverResidualThreshold; BaseAviary.py never calls it, so the
+   * defaults are the reference's): 0 = default (50 iterations, residual 1e-7); a residual < 0
+   * makes every solve run all its iterations. */
+  int solver_iterations;     /* 0 or [1, 1000] */
+  double solver_residual;
 } gpd_config;
 
 /* Derived constants, BaseAviary.py:117-128 (read-only view for tests/facades). */

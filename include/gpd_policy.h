@@ -12,7 +12,7 @@
  *     rollout_buffer.add(obs, actions, rewards, episode_starts, values, log_probs)
  * gpd_policy_rollout_step fuses everything except env.step (gpd_step) into ONE kernel: the
  * bootstrap and buffer write of the PREVIOUS step's reward, then the actor + critic forward, the
- * Normal sample, the clip and the buffer writes of THIS step, with the weights staged in LDS.
+ * Normal sample, the clip and the buffer writes of THIS step, with the weight slices in VGPRs.
  *
  * Conventions as in gpd.h: device pointers, caller-owned buffers, asynchronous on `stream`,
  * GPD_OK (0) or a negative GPD_E* code with gpd_policy_last_error().

@@ -163,6 +163,9 @@ CONTACT_ERP = 0.08          # btContactSolverInfo::m_erp2 as pybullet sets it (c
 LINEAR_SLOP = 1e-5          # m_linearSlop as pybullet sets it
 SOLVER_ITERS = 50           # m_numIterations as pybullet sets it (numSolverIterations)
 RESIDUAL_THRESHOLD = 1e-7   # m_leastSquaresResidualThreshold as pybullet sets it
+# test instrumentation: when a list, every drone <-> drone solve appends its iteration count
+# (SOLVER_ITERS + 1 = stopped by the cap without reaching RESIDUAL_THRESHOLD)
+SOLVE_LOG = None
 FRICTION = 0.5 * 1.0        # combined friction = drone (btCollisionObject default 0.5, the URDFs
                             # carry no <contact>) x plane.urdf lateral_friction 1; restitution 0
 URDF_MARGIN = 0.001         # gUrdfDefaultCollisionMargin (collision-shape margin of URDF shapes)
@@ -807,7 +810,8 @@ def drone_contact(pos, rot_bw, vel_w, omega_w, m, inertia, dt, radius, half_heig
             return s1 * f, s2 * f
         return s1, s2
 
-    for _ in range(SOLVER_ITERS):
+    used = SOLVER_ITERS + 1
+    for it in range(SOLVER_ITERS):
         res = 0.0
         for i, pr in prows.items():                           # plane normal rows
             for c in pr:
@@ -858,7 +862,10 @@ def drone_contact(pos, rot_bw, vel_w, omega_w, m, inertia, dt, radius, half_heig
             apply(c, 2, d2)
             res = max(res, (d1 + d2) ** 2)
         if res <= RESIDUAL_THRESHOLD:
+            used = it + 1
             break
+    if SOLVE_LOG is not None:
+        SOLVE_LOG.append(used)
     for i in touched:
         vel[i] = vel[i] + dl[i]
         omg[i] = omg[i] + da[i]

@@ -98,10 +98,17 @@ def resynced_substep_errors(sim, env, rpms):
     """Local parity of chaotic runs (drones crashing into the plane): before every substep the
     GPU sim is set to the oracle's state, both take ONE substep on the same RPMs, and the
     per-drone relative state error of that substep is recorded.  Rounding differences cannot
-    compound, so an identical algorithm agrees to rounding at every substep.  Returns [T, N]."""
+    compound, so an identical algorithm agrees to rounding at every substep.  An f32 sim holds
+    the state rounded to f32, so the oracle is then set to those same values: both step from the
+    same input (a contact decided at a tie - a symmetric squeezed stack - can jump under a 1e-8
+    change of the input; the f64 oracle itself moves 0.1 when its input is rounded to f32).
+    Returns [T, N]."""
     errs = []
+    same_input = getattr(sim, "precision", "f64") == "f32"
     for t in range(rpms.shape[0]):
         sim.set_raw_state(oracle_raw(env))
+        if same_input:
+            env.set_raw_state(sim.raw_state().cpu().numpy())
         g = sim.integrate(rpms[t:t + 1], record=True).cpu().numpy()
         r = env.integrate(rpms[t:t + 1])
         errs.append(state_rel_err(g, r)[0])

@@ -136,10 +136,16 @@ def _cases(D):
     return np.concatenate([_cube(rng) for _ in range(8)]), {"drones_per_block": 64}
 
 
-@pytest.mark.parametrize("prec", ["f64", "f32"])
-@pytest.mark.parametrize("D", [2, 3, 4, 8])
-def test_drone_contact_resynced(prec, D):
+def _contact_errors(D, prec, fixed_iters, monkeypatch):
+    """Resynced substep errors of the _cases(D) batch.  fixed_iters: both solvers run all 50
+    Gauss-Seidel iterations (solverResidualThreshold < 0 in the kernel and the oracle), so the
+    comparison isolates rounding from WHERE the stopping rule ends a solve."""
+    import oracle.bullet_mb as bm
     raw0, tuning = _cases(D)
+    tuning = dict(tuning or {})
+    if fixed_iters:
+        tuning["solver_residual"] = -1.0
+        monkeypatch.setattr(bm, "RESIDUAL_THRESHOLD", -1.0)
     n = raw0.shape[0]
     T = 40
     rpms = np.full((T, n, 4), HOVER)
@@ -147,22 +153,50 @@ def test_drone_contact_resynced(prec, D):
     env.set_raw_state(raw0)
     sim = _sim(n_envs=n // D, drones_per_env=D, task="none", precision=prec, physics=_pyb(), aero=("no_plane",),
                tuning=tuning)
-    err = resynced_substep_errors(sim, env, rpms)
+    bm.SOLVE_LOG = []
+    try:
+        err = resynced_substep_errors(sim, env, rpms)
+        iters = list(bm.SOLVE_LOG)
+    finally:
+        bm.SOLVE_LOG = None
+        sim.close()
     sep = np.linalg.norm(env._b_pos[0] - env._b_pos[1])
     big = np.argwhere(err > 1e-3)
-    print(f"\n[parity] drone contact D={D} {prec}: max {err.max():.3e} median {np.median(err):.3e} "
-          f"(pair 0 separation after {T} substeps {sep:.4f} m); {len(big)} of {err.size} drone-substeps above "
-          f"1e-3 at (substep, drone) {big[:12].tolist()}")
+    print(f"\n[parity] drone contact D={D} {prec}{' fixed 50 iterations' if fixed_iters else ''}: max {err.max():.3e} "
+          f"median {np.median(err):.3e} (pair 0 separation after {T} substeps {sep:.4f} m; oracle solves: "
+          f"{len(iters)}, most iterations {max(iters) if iters else 0}); {len(big)} of {err.size} drone-substeps "
+          f"above 1e-3 at (substep, drone) {big[:12].tolist()}")
+    return err, iters
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+@pytest.mark.parametrize("D", [2, 3, 4, 8])
+def test_drone_contact_resynced(prec, D, monkeypatch):
+    err, _ = _contact_errors(D, prec, False, monkeypatch)
     if prec == "f64":
         assert err.max() <= 1e-10
     elif D < 8:
+        # f32: the oracle steps from the sim's f32-rounded state (oracle_runs.resynced_substep_errors)
         assert np.median(err) <= 1e-6 and err.max() <= 1e-3
     else:
-        # the squeezed 2 x 2 x 2 stacks: every pair a face contact of five points (redundant rows),
-        # so the f32 Gauss-Seidel stops at another iteration than the f64 oracle's on the first
-        # substeps (worst 0.1 relative at substep 0); rounding afterwards
-        assert np.median(err) <= 1e-6 and np.percentile(err, 95) <= 1e-3 and err.max() <= 0.2
-    sim.close()
+        # the squeezed 2 x 2 x 2 stacks: 12+ contacts of four rows each in one island (a face
+        # manifold's normal rows span three directions), so f32 rounding inside the solve is
+        # amplified by its conditioning: measured 1.03e-3 on 1 of 2 560 drone-substeps (round 6;
+        # with the oracle stepping from its own f64 state, round 5 gated this at 0.2 - that 0.1 was
+        # the input rounding, which the f64 oracle alone reproduces)
+        assert np.median(err) <= 1e-6 and (err > 1e-3).mean() <= 1e-3 and err.max() <= 2e-3
+
+
+@pytest.mark.parametrize("D", [2, 3, 4])
+def test_drone_contact_resynced_f32_fixed_iterations(D, monkeypatch):
+    """The solver parameters (pybullet's setPhysicsEngineParameter solverResidualThreshold < 0:
+    every solve runs all 50 Gauss-Seidel iterations; gpd_config::solver_residual, bullet_mb alike)
+    reach the contact kernels: f32 against the f64 oracle, every substep <= 1e-3, every oracle
+    solve at the cap.  (The squeezed 8-drone stacks iterated 15 past their convergence drift to
+    5.5e-3 in f32: an ill-conditioned island, not gated here.)"""
+    err, iters = _contact_errors(D, "f32", True, monkeypatch)
+    assert iters and min(iters) == 51             # SOLVER_ITERS + 1: no solve stopped early
+    assert np.median(err) <= 1e-6 and err.max() <= 1e-3
 
 
 @pytest.mark.parametrize("D", [16, 64])
