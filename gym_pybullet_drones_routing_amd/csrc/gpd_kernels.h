@@ -259,21 +259,6 @@ __device__ __forceinline__ void mark_last_in_ring(const SimView<R>& v, long long
 // vector-memory operation in flight, including an LDS-DMA that nobody reads until much later.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Point-to-point hand-off between two waves of a block through an LDS counter, without a
-// workgroup barrier (so a third wave of the block need not take part).  The producer's data
-// writes have completed before the counter moves (the wait); the consumer polls the counter
-// (wave-uniform) and reads the data after it.
-__device__ __forceinline__ void lds_publish(volatile int* ctr, int v) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  *ctr = v;
-  asm volatile("" ::: "memory");
-}
-__device__ __forceinline__ void lds_wait_for(volatile int* ctr, int v) {
-  while (__builtin_amdgcn_readfirstlane(*ctr) < v) {
-  }
-  asm volatile("" ::: "memory");
-}
-
 // LDS exchange among the lanes of ONE wave (the step / integrate kernels' blocks are one wave):
 // a wave's LDS instructions execute in order, so a later ds_read sees an earlier ds_write of
 // any lane without a wait or a hardware barrier; the fence only keeps the compiler from
@@ -2224,9 +2209,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(GPD_STEP_
 // the current action) WHILE the pose / rate waves integrate, and appends the action to the
 // ring.  The pose wave then stores only the 12 state columns of its rows straight from
 // registers, so the LDS observation tile and its copy-out leave the critical path.
-#ifndef GPD_DUO_FLAGS
-#define GPD_DUO_FLAGS 0
-#endif
 template <typename R, int ACT, bool IO>
 __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R* __restrict__ state_p,
                                                              const float* __restrict__ actions_p,
@@ -2239,15 +2221,7 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
   constexpr int A = act_width(ACT);
   extern __shared__ float4 tile4[];
   float* tilef = reinterpret_cast<float*>(tile4);
-#if GPD_DUO_FLAGS
-  // hand-offs through LDS counters (lds_publish / lds_wait_for): hpub = hand-offs published by
-  // the rate wave, hack = hand-offs the pose wave has read; kNB slots in flight
-  constexpr int kNB = 4;
-  __shared__ R shand[kNB][5][kWave];
-  __shared__ int hpub, hack;
-#else
   __shared__ R shand[2][5][kWave];        // rate_half -> pose_half, by substep parity
-#endif
   __shared__ R sw[3][kWave];              // rpy_rates after the last substep
   __shared__ unsigned long long sdone;    // done-row mask of the block (tile rows)
   GPD_RSTAMP(11);
@@ -2268,10 +2242,6 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
   }
 #endif
 
-#if GPD_DUO_FLAGS
-  if (threadIdx.x == 0) { hpub = 0; hack = 0; }
-  lds_barrier();     // the counters are set before any wave reads them (all waves, once)
-#endif
   if (IO && wave == 2) {
     // ------------------------------------------------------------ wave 2: history columns
     // The history columns of a row are ring slots head+1 .. head+L-1 (oldest first,
@@ -2304,13 +2274,11 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
     // This wave publishes nothing to the others, so its barriers skip lds_barrier's
     // lgkmcnt(0) wait: an LDS-DMA in flight holds that counter until it lands.
     GPD_IOSTAMP(0);
-#if GPD_DUO_FLAGS
-    (void)nsub;        // the pose / rate hand-offs go through LDS counters: no barrier to follow
-#else
+    // (an LDS-counter hand-off between the pose and rate waves, which would free this wave of
+    // their barriers, measured 5.3 / 6.4 us against 4.9: profiles/r6/duo_flags/)
     asm volatile("s_barrier" ::: "memory");       // hand-off 0
     GPD_IOSTAMP(1);
     for (int k = 1; k < nsub; ++k) asm volatile("s_barrier" ::: "memory");   // hand-offs 1 .. nsub-1
-#endif
     // history ring -> tile (LDS-DMA) behind the last hand-off: an LDS-DMA in flight while the
     // pose / rate waves still exchange hand-offs slowed their substeps by ~850 cycles per launch
     // (phase stamps, 4096 envs), issued here it lands beside the pose wave's last substep and
@@ -2416,23 +2384,13 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
     for (int k = 0; k < nsub; ++k) {
       R h[5];
       rate_half(wx, wy, wz, W, dk, h);
-#if GPD_DUO_FLAGS
-      if (k >= kNB) lds_wait_for(&hack, k - kNB + 1);   // slot k % kNB read by the pose wave
-#pragma unroll
-      for (int j = 0; j < 5; ++j) shand[k % kNB][j][tid] = h[j];
-      if (k == nsub - 1) { sw[0][tid] = wx; sw[1][tid] = wy; sw[2][tid] = wz; }
-      lds_publish(&hpub, k + 1);   // hand-off k published
-#else
 #pragma unroll
       for (int j = 0; j < 5; ++j) shand[k & 1][j][tid] = h[j];
       if (k == nsub - 1) { sw[0][tid] = wx; sw[1][tid] = wy; sw[2][tid] = wz; }
       lds_barrier();   // hand-off k published
-#endif
     }
     if (IO) {          // the io wave owns the history columns and the ring append
-#if !GPD_DUO_FLAGS
-      lds_barrier();   // final (with flags this wave has no part in it: an ended wave is not waited for)
-#endif
+      lds_barrier();   // final
       return;
     }
     // history ring -> obs tile (LDS-DMA): issued once the last hand-off is out, it lands while
@@ -2507,49 +2465,24 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
   }
   const R wnone[3] = {R(0), R(0), R(0)};
-#if GPD_DUO_FLAGS == 2
-  // the counter and the slot read in one batch (a wave's LDS reads execute in order, and the rate
-  // wave's slot writes completed before its counter write): valid when the counter says so
-  auto hand_off = [&](int k, R h[5]) {
-    const volatile R* sh = &shand[k % kNB][0][tid];
-    int f;
-    do {
-      f = *(const volatile int*)&hpub;
-#pragma unroll
-      for (int j = 0; j < 5; ++j) h[j] = sh[j * kWave];
-    } while (__builtin_amdgcn_readfirstlane(f) < k + 1);
-    if (nsub > kNB) lds_publish(&hack, k + 1);   // slot free again (the wait covers the reads)
-  };
-#define GPD_HANDOFF_SYNC() do {} while (0)
-#elif GPD_DUO_FLAGS
-  auto hand_off = [&](int k, R h[5]) {
-    lds_wait_for(&hpub, k + 1);
-#pragma unroll
-    for (int j = 0; j < 5; ++j) h[j] = shand[k % kNB][j][tid];
-    if (nsub > kNB) lds_publish(&hack, k + 1);   // slot free again (the wait covers the reads)
-  };
-#define GPD_HANDOFF_SYNC() do {} while (0)
-#else
   auto hand_off = [&](int k, R h[5]) {
 #pragma unroll
     for (int j = 0; j < 5; ++j) h[j] = shand[k & 1][j][tid];
   };
-#define GPD_HANDOFF_SYNC() lds_barrier()
-#endif
   if (nsub > 1) {
-    GPD_HANDOFF_SYNC();   // hand-off 0
+    lds_barrier();   // hand-off 0
     R h[5];
     hand_off(0, h);
     pose_half<R, false, true>(s, fz, h, wnone, dk);
     GPD_STAMP(1);
     for (int k = 1; k < nsub - 1; ++k) {
-      GPD_HANDOFF_SYNC();   // hand-off k
+      lds_barrier();   // hand-off k
       hand_off(k, h);
       pose_half<R, false, false>(s, fz, h, wnone, dk);
     }
   }
   {
-    GPD_HANDOFF_SYNC();   // last hand-off + final rates
+    lds_barrier();   // last hand-off + final rates
     R h[5];
     hand_off(nsub - 1, h);
     s.wx = sw[0][tid]; s.wy = sw[1][tid]; s.wz = sw[2][tid];
@@ -2658,7 +2591,6 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
   }
   GPD_STAMP(7);
   GPD_RSTAMP(12);
-#undef GPD_HANDOFF_SYNC
   if (!active) return;
   store_drone_step(v, n, s, last);
   mark_last_in_ring(v, n);

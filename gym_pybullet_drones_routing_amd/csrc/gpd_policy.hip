@@ -142,12 +142,18 @@ struct Regs {
 
 template <int N>
 __device__ inline void load_slice(float (&dst)[N], const float* __restrict__ row, int k0, int n, bool on) {
-  // dst[s] = row[k0 + s] (0 past n or when !on); float4 loads when the slice is 16-B aligned
-  if (on && (n & 3) == 0 && (k0 & 3) == 0 && ((uintptr_t)row & 15) == 0 && k0 + N <= n) {
+  // dst[s] = row[k0 + s] (0 past n or when !on); float4 / float2 loads when the slice is 16- / 8-B aligned
+  if (N % 4 == 0 && on && (n & 3) == 0 && (k0 & 3) == 0 && ((uintptr_t)row & 15) == 0 && k0 + N <= n) {
 #pragma unroll
     for (int q = 0; q < N / 4; ++q) {
       const float4 v = reinterpret_cast<const float4*>(row + k0)[q];
       dst[4 * q] = v.x; dst[4 * q + 1] = v.y; dst[4 * q + 2] = v.z; dst[4 * q + 3] = v.w;
+    }
+  } else if (N % 2 == 0 && on && (n & 1) == 0 && (k0 & 1) == 0 && ((uintptr_t)row & 7) == 0 && k0 + N <= n) {
+#pragma unroll
+    for (int q = 0; q < N / 2; ++q) {   // float2 (KQ = 18: the slices start 72 B apart)
+      const float2 v = reinterpret_cast<const float2*>(row + k0)[q];
+      dst[2 * q] = v.x; dst[2 * q + 1] = v.y;
     }
   } else {
 #pragma unroll
@@ -408,12 +414,15 @@ int launch(const Args& A, int grid, hipStream_t st) {
   HIP_TRY(hipGetLastError());
   return kOk;
 }
-// the weight slices live in VGPRs: the layer-1 slice sized by the obs width's bucket
+// the weight slices live in VGPRs: the layer-1 slice sized by the obs width's bucket (18 / 36:
+// the KIN observation of one / two RPM drones, 72 / 144 wide, without padding MFMA steps)
 template <int NA>
 int launch_kq(const Args& A, int grid, hipStream_t st) {
   if (A.kq <= 8) return launch<NA, 8>(A, grid, st);
   if (A.kq <= 16) return launch<NA, 16>(A, grid, st);
+  if (A.kq <= 18) return launch<NA, 18>(A, grid, st);
   if (A.kq <= 24) return launch<NA, 24>(A, grid, st);
+  if (A.kq <= 36) return launch<NA, 36>(A, grid, st);
   return launch<NA, kMaxKq>(A, grid, st);
 }
 
