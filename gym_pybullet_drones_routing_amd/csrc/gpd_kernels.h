@@ -328,15 +328,16 @@ __device__ __forceinline__ void plane_space(const R n[3], R p[3], R q[3]) {
 // ---- narrowphase (oracle/bullet_mb.py core_pair / rim_newton / rim_closest / pair_geometry / face_points)
 // The closest points of the margin-shrunk cores, converged: the near caps' centres, the lateral
 // surfaces along the axes' closest points (closed forms), and the four rim circles against the other
-// cylinder - trust-region Newton on the rim angle from each of 4 start azimuths (0 / 90 / 180 / 270 deg), the smallest
-// squared distance per rim; the first candidate within the tie of the closest wins.  Everything in
-// B's frame (btPlaneSpace1(aB), aB); B's rims in A's frame (btPlaneSpace1 of A).  A pass's near
-// pairs split into 16 tasks each (4 rims x 4 starts) over the wave's lanes (dc_narrow_pass): a
-// sparse wave (one or two near pairs, the common case) runs ONE Newton chain per lane.
+// cylinder - 5 trust-region Newton steps on the rim angle from each of 16 start azimuths (k x 22.5
+// deg), the smallest squared distance per rim; the first candidate within the tie of the closest
+// wins.  Everything in B's frame (btPlaneSpace1(aB), aB); B's rims in A's frame (btPlaneSpace1 of A).
+// A pass's near pairs split into 64 tasks each (4 rims x 16 starts) over the wave's lanes
+// (dc_narrow_pass): a sparse wave (one near pair, the common case) runs ONE Newton chain of 6
+// evaluations per lane (round 5: 4 starts x 8 steps, 9 evaluations).
 template <typename R> struct NpTol;
 template <> struct NpTol<double> { static constexpr double accept = 1e-10, same = 1e-4, tie = 1e-7; };   // RIM_ACCEPT, RIM_SAME, PAIR_TIE
 template <> struct NpTol<float> { static constexpr float accept = 1e-5f, same = 1e-4f, tie = 1e-7f; };
-constexpr int kRimSamples = 8, kRimIters = 8;   // RIM_SAMPLES, RIM_ITERS
+constexpr int kRimSamples = 16, kRimIters = 5;   // RIM_SAMPLES, RIM_ITERS
 template <typename R>
 __device__ __forceinline__ void axial_project(R x, R y, R z, R r, R h, R& qx, R& qy, R& qz) {
   const R rho2 = x * x + y * y;
@@ -378,7 +379,7 @@ template <typename R>
 __device__ __forceinline__ void rim_newton(const R C[3], const R e1[3], const R e2[3], R r, R h, R c, R s, RimEval<R>& cur) {
   constexpr R kAcc = NpTol<R>::accept;
   rim_eval(C, e1, e2, c, s, r, h, cur);
-  R rad = R(0.39269908169872414);   // pi / RIM_SAMPLES
+  R rad = R(0.19634954084936207);   // pi / RIM_SAMPLES
 #pragma unroll 1
   for (int it = 0; it < kRimIters; ++it) {
     // -g / hh and 1 / sqrt as Newton-refined reciprocals (~1 ulp; the oracle divides)
@@ -443,12 +444,17 @@ __device__ __forceinline__ void np_to_b(const NpPair<R>& q, const R v[3], R o[3]
   o[2] = ((q.ap[2] * v[0] + q.aq[2] * v[1]) + q.A[2] * v[2]) + q.L[2];
 }
 // one rim task: rim 0/2 = A's near / far rim against B, 1/3 = B's near / far rim against A, from
-// start azimuth k; (x on A, y on B) in B's frame and the squared distance
+// start azimuth k (k x 22.5 deg); (x on A, y on B) in B's frame and the squared distance
 template <typename R>
 __device__ __forceinline__ void np_rim_task(const NpPair<R>& q, int rim, int k, R r, R h, R& f, R x[3], R y[3]) {
-  const R S = R(0.7071067811865475244008443621048490);   // bullet_mb.RIM_COS / RIM_SIN
-  const R c0 = k == 0 ? R(1) : (k == 1 || k == 7 ? S : (k == 3 || k == 5 ? -S : (k == 4 ? R(-1) : R(0))));
-  const R s0 = k == 2 ? R(1) : (k == 1 || k == 3 ? S : (k == 5 || k == 7 ? -S : (k == 6 ? R(-1) : R(0))));
+  // bullet_mb.RIM_COS / RIM_SIN: the first quadrant's (cos, sin) turned by k / 4 quarter turns,
+  // negations as 0 - x (+0.0 where the oracle's table has it)
+  const R H = R(0.7071067811865475244008443621048490), C1 = R(0.92387953251128674), S1 = R(0.38268343236508978);
+  const int qd = k & 3, qt = k >> 2;
+  const R qc = qd == 0 ? R(1) : (qd == 1 ? C1 : (qd == 2 ? H : S1));
+  const R qs = qd == 0 ? R(0) : (qd == 1 ? S1 : (qd == 2 ? H : C1));
+  const R c0 = qt == 0 ? qc : (qt == 1 ? R(0) - qs : (qt == 2 ? R(0) - qc : qs));
+  const R s0 = qt == 0 ? qs : (qt == 1 ? qc : (qt == 2 ? R(0) - qs : R(0) - qc));
   const bool on_a = (rim & 1) == 0;
   const R sg = on_a ? (rim < 2 ? q.sa : -q.sa) : (rim < 2 ? q.sb : -q.sb);
   const R* base = on_a ? q.L : q.Lb;
@@ -1113,8 +1119,8 @@ __device__ __forceinline__ void eres_max(DcLds<R>& L, int env, R rr) {
     atomicMax(reinterpret_cast<unsigned int*>(&L.eres[env]), (unsigned int)__float_as_uint((float)rr));
 }
 // The narrowphases of a pass's nthis near pairs (L.nsij[0..nthis)): bullet_mb.pair_geometry per pair,
-// its 4 x 4 rim Newton chains as 16 tasks over the lanes (task t: slot t / 16, rim (t / 4) % 4,
-// start (t % 4) * 90 deg; the best start per rim by a butterfly over 4 lanes, ties to the lower start), the
+// its 4 x 16 rim Newton chains as 64 tasks over the lanes (task t: slot t / 64, rim (t / 16) % 4,
+// start t % 16; the best start per rim by a butterfly over 16 lanes, ties to the lower start), the
 // closed-form candidates and the selection by the pair's own lane (lane = slot), margin level by
 // margin level while some pair's cores overlap; then the fallback and the face manifold.  Lane
 // ln < nthis stages its pair's result in L.st and its face-point mask in L.nsp[ln] and returns its
@@ -1147,7 +1153,7 @@ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthis) {
   R yl[3] = {R(0), R(0), R(0)};
   L.npdone[ln] = found ? 1 : 0;
   wave_lds_sync();
-  const int ntask = nthis * 16;
+  const int ntask = nthis * 64;
 #pragma unroll 1
   for (int lv = 0; lv < 4; ++lv) {
     if (__ballot(!found) == 0ull) break;
@@ -1155,8 +1161,8 @@ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthis) {
 #pragma unroll 1
     for (int t0 = 0; t0 < ntask; t0 += kWave) {
       const int t = t0 + ln;
-      // task t: slot t / 16, rim (t / 4) % 4, start (t % 4) * 90 deg (bullet_mb.RIM_STARTS)
-      const int slot = (t >> 4) & 63, rim = (t >> 2) & 3, k = (t & 3) * 2;
+      // task t: slot t / 64, rim (t / 16) % 4, start t % 16 (bullet_mb.RIM_STARTS)
+      const int slot = (t >> 6) & 63, rim = (t >> 4) & 3, k = t & 15;
       R f = R(INFINITY), x[3] = {R(0), R(0), R(0)}, y[3] = {R(0), R(0), R(0)};
       bool need = false;
       if (t < ntask && !L.npdone[slot]) {
@@ -1176,13 +1182,13 @@ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthis) {
       // the rim's result: the lowest start within RIM_SAME of the group's smallest f (bullet_mb.rim_closest)
       R fmin = f;
 #pragma unroll
-      for (int o = 1; o < 4; o <<= 1) fmin = g_min1(fmin, __shfl_xor(fmin, o));
+      for (int o = 1; o < 16; o <<= 1) fmin = g_min1(fmin, __shfl_xor(fmin, o));
       const unsigned long long near = __ballot(f <= fmin * (R(1) + NpTol<R>::same));
-      const int g0 = ln & ~3;
-      const int src = g0 + __builtin_ctz((unsigned)((near >> g0) & 0xfull) | 0x10u);
+      const int g0 = ln & ~15;
+      const int src = g0 + __builtin_ctz((unsigned)((near >> g0) & 0xffffull) | 0x10000u);
 #pragma unroll
       for (int e = 0; e < 3; ++e) { x[e] = __shfl(x[e], src); y[e] = __shfl(y[e], src); }
-      if (t < ntask && (t & 3) == 0) {
+      if (t < ntask && (t & 15) == 0) {
 #pragma unroll
         for (int e = 0; e < 3; ++e) { L.DC_RIM(rim, e)[slot] = x[e]; L.DC_RIM(rim, 3 + e)[slot] = y[e]; }
         L.DC_RIM(rim, 6)[slot] = need ? R(0) : R(INFINITY);   // a rim the pair does not need

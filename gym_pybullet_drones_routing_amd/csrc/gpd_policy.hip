@@ -126,7 +126,6 @@ struct Lds {
   float res[kM][kRes];             // per row: mu[0..n_act), value at n_act, V(terminal row) at n_act + 1
   float lp[kM][GPD_POLICY_MAX_ACT];
   float b3[GPD_POLICY_MAX_ACT + 1];   // output biases: mu_0 .. mu_{n_act-1}, value
-  unsigned long long call;            // this launch's call counter (thread 0's ticket)
 };
 
 // This lane's slice of the weights: B operands W1[j][g KQ + s] (s < KQ), W2[j][16 g + s], output
@@ -285,7 +284,8 @@ __device__ inline void forward(Lds& L, const Args& A, const Regs<NA, KQ>& R, int
 // a group's loads: its terminal rows, flags and rewards (bootstrap) and its observation rows
 template <int KQ>
 __device__ inline void issue_group(const Args& A, RowRegs<KQ>& X, RowRegs<KQ>& TX, float& rw, bool& te, bool& tr,
-                                   int row0, int t) {
+                                   uint64_t& call, int row0, int t) {
+  if (A.sample) call = A.rng[2 + row0 / kM];
   if (A.reward) {
     load_rows(TX, A, A.tobs, row0);
     const bool mine = t < kM && row0 + t < A.n_rows;
@@ -300,29 +300,21 @@ template <int NA, int KQ>
 __global__ void __launch_bounds__(kBlock) rollout_kernel(Args A) {
   __shared__ Lds L;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, t = threadIdx.x;
-  // rng[1] = call counter << 16 | ticket.  Every block takes a ticket with ONE atomic, which also
-  // returns the call counter; the block that takes the last ticket moves the counter on and the
-  // ticket back to 0 (a non-returning atomic).  All blocks' tickets precede it, and the next launch
-  // on the stream starts after it: no fence, no round trip at the kernel's tail.
-  uint64_t seed = 0;
-  if (A.sample) {
-    seed = A.rng[0];
-    if (threadIdx.x == 0) {
-      const unsigned long long old = atomicAdd((unsigned long long*)&A.rng[1], 1ull);
-      if ((old & 0xffffull) == gridDim.x - 1)
-        atomicAdd((unsigned long long*)&A.rng[1], (1ull << 16) - gridDim.x);
-      L.call = old >> 16;
-    }
-  }
+  // the Philox call counter of a row group is rng[2 + group]: read with the group's loads, moved on
+  // by the block that samples the group (one reader-writer per counter and call: a plain load and
+  // store; a single counter took one atomic per block, ~3.8 us of a sampled launch as 256 blocks
+  // queued on one address: scripts/policy_probe.py graph, profiles/r6/policy/)
+  const uint64_t seed = A.sample ? A.rng[0] : 0;
   // everything a group reads from memory is issued before anything waits for it; the block's
   // weight slices go out behind the first group's rows, the next group's loads behind this one's
   // stores (one memory round trip per group)
   RowRegs<KQ> X, TX;
   float rw = 0.0f;
   bool te = false, tr = false;
+  uint64_t call = 0;
   int row0 = blockIdx.x * kM;
   const int stride = gridDim.x * kM;
-  issue_group(A, X, TX, rw, te, tr, row0, t);
+  issue_group(A, X, TX, rw, te, tr, call, row0, t);
   Regs<NA, KQ> R;
   load_regs(A, R, 16 * w + (l & 15), l >> 4);
   if (t <= NA) L.b3[t] = t == NA ? A.vf.b3[0] : (A.actor ? A.pi.b3[t] : 0.0f);   // read after a barrier
@@ -347,7 +339,7 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(Args A) {
       A.buf_done[row0 + t] = (te || tr) ? 1.0f : 0.0f;
     }
     if (!A.forward) {   // (the next group's first barrier orders these reads before its forward)
-      if (row0 + stride < A.n_rows) issue_group(A, X, TX, rw, te, tr, row0 + stride, t);
+      if (row0 + stride < A.n_rows) issue_group(A, X, TX, rw, te, tr, call, row0 + stride, t);
       continue;
     }
     // ---- this step: the sample and the rows
@@ -358,7 +350,7 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(Args A) {
       const float sc = R.sc;
       float act = m;
       // torch Normal.rsample: loc + eps * scale (two roundings: no contraction in this file)
-      if (!A.deterministic) act = m + std_normal(seed, L.call, row, a) * sc;
+      if (!A.deterministic) act = m + std_normal(seed, call, row, a) * sc;
       // torch.distributions.Normal.log_prob:
       //   -((value - loc) ** 2) / (2 * var) - log(scale) - log(sqrt(2 * pi)),  var = scale ** 2
       const float d = act - m;
@@ -368,6 +360,7 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(Args A) {
         if (A.act_env) A.act_env[(size_t)row * NA + a] = fminf(fmaxf(act, -1.0f), 1.0f);
       }
     }
+    if (A.sample && t == 0) A.rng[2 + row0 / kM] = call + 1;   // this group's counter moves on
     __syncthreads();
     if (t < kM) {
       const int row = row0 + t;
@@ -381,7 +374,7 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(Args A) {
         }
       }
     }
-    if (row0 + stride < A.n_rows) issue_group(A, X, TX, rw, te, tr, row0 + stride, t);
+    if (row0 + stride < A.n_rows) issue_group(A, X, TX, rw, te, tr, call, row0 + stride, t);
     __syncthreads();   // res / lp are rewritten by the next group
   }
 }
@@ -435,7 +428,7 @@ const char* gpd_policy_last_error(void) { return g_err.c_str(); }
 
 int gpd_policy_rollout_step(const gpd_mlp_policy* p, int n_rows, const float* obs, float* act_env, float* buf_obs,
                             float* buf_act, float* buf_logp, float* buf_val, int deterministic, uint64_t* rng,
-                            const float* reward, const uint8_t* terminated, const uint8_t* truncated,
+                            int rng_groups, const float* reward, const uint8_t* terminated, const uint8_t* truncated,
                             const float* terminal_obs, float gamma, float* buf_rew, float* buf_done, void* stream) {
   if (!p) return fail(kEinval, "gpd_policy_rollout_step: NULL policy");
   if (n_rows < 1) return fail(kEinval, "gpd_policy_rollout_step: n_rows < 1");
@@ -465,6 +458,10 @@ int gpd_policy_rollout_step(const gpd_mlp_policy* p, int n_rows, const float* ob
   if (A.actor && (!p->pi_w1 || !p->pi_b1 || !p->pi_w2 || !p->pi_b2 || !p->pi_w3 || !p->pi_b3 || !p->log_std))
     return fail(kEinval, "gpd_policy_rollout_step: NULL actor weight");
   if (A.sample && !rng) return fail(kEinval, "gpd_policy_rollout_step: sampling needs the rng state");
+  if (A.sample && (long long)rng_groups * kM < n_rows)
+    return fail(kEinval, "gpd_policy_rollout_step: rng holds " + std::to_string(rng_groups) +
+                             " row-group counters, sampling " + std::to_string(n_rows) + " rows needs " +
+                             std::to_string((n_rows + kM - 1) / kM));
   if (reward && (!terminated || !truncated || !terminal_obs || !buf_rew || !buf_done))
     return fail(kEinval, "gpd_policy_rollout_step: the bootstrap needs terminated, truncated, terminal_obs, "
                          "buf_rew and buf_done");

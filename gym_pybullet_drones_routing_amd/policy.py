@@ -18,7 +18,8 @@ from ._lib import GpdError, GpdLibraryError
 
 LIB_PATH = pathlib.Path(os.environ.get("GPD_POLICY_LIB") or (pathlib.Path(__file__).resolve().parent /
                                                                "libgpd_policy.so"))
-GPD_POLICY_ABI_VERSION = 1
+GPD_POLICY_ABI_VERSION = 2
+GROUP_ROWS = 16                 # rows per Philox call counter (the kernel's row group)
 HIDDEN = 64
 MAX_OBS = 192
 MAX_ACT = 8
@@ -51,7 +52,7 @@ def load():
     lib.gpd_policy_last_error.restype = ctypes.c_char_p
     lib.gpd_policy_last_error.argtypes = []
     lib.gpd_policy_rollout_step.restype = ci
-    lib.gpd_policy_rollout_step.argtypes = [ctypes.POINTER(MlpPolicyStruct), ci, vp, vp, vp, vp, vp, vp, ci, vp,
+    lib.gpd_policy_rollout_step.argtypes = [ctypes.POINTER(MlpPolicyStruct), ci, vp, vp, vp, vp, vp, vp, ci, vp, ci,
                                             vp, vp, vp, vp, ctypes.c_float, vp, vp, vp]
     lib.gpd_policy_gae.restype = ci
     lib.gpd_policy_gae.argtypes = [ci, ci, vp, vp, vp, vp, ctypes.c_double, ctypes.c_double, vp, vp, vp]
@@ -81,9 +82,11 @@ class MlpPolicyKernel:
     """The actor-critic ``module`` (``.pi``, ``.vf`` as Linear-Tanh-Linear-Tanh-Linear, ``.log_std``;
     examples/learn.py's ``ActorCritic``) as one rollout kernel per step.  The parameters are read
     in place: an optimizer step that updates them in place is seen by the next call (and by a
-    captured graph).  ``seed``: the Philox key; the call counter lives on the device (``rng``)."""
+    captured graph).  ``seed``: the Philox key; the call counters (one per group of 16 rows) live
+    on the device (``rng``), sized for ``max_rows`` rows (grown by a call with more rows, which a
+    captured graph must not do)."""
 
-    def __init__(self, module, seed=0):
+    def __init__(self, module, seed=0, max_rows=1 << 16):
         self._lib = load()
         pi, vf = _linears(module.pi), _linears(module.vf)
         if vf[2].out_features != 1:
@@ -107,16 +110,34 @@ class MlpPolicyKernel:
         for n, p in zip(names, params):
             setattr(st, n, p.data_ptr())
         self._st = st
-        self.rng = torch.tensor([int(seed), 0, 0], dtype=torch.int64, device=dev)   # {key, counter << 16 | ticket, 0}
+        # {key, 0, call counter of row group 0, 1, ...} (include/gpd_policy.h)
+        self.rng = torch.zeros(2 + -(-int(max_rows) // GROUP_ROWS), dtype=torch.int64, device=dev)
+        self.rng[0] = int(seed)
+
+    @property
+    def rng_groups(self):
+        return self.rng.numel() - 2
+
+    def _fit(self, n_rows):
+        need = -(-n_rows // GROUP_ROWS)
+        if need > self.rng_groups:
+            if torch.cuda.is_current_stream_capturing():
+                raise ValueError(f"{n_rows} rows need {need} row-group counters, the rng holds {self.rng_groups}: "
+                                 "pass max_rows >= the largest batch before capturing a graph")
+            grown = torch.zeros(2 + need, dtype=torch.int64, device=self.device)
+            grown[:self.rng.numel()] = self.rng
+            grown[self.rng.numel():] = self.rng[2]      # new groups join at the batch's call count
+            self.rng = grown
 
     @property
     def calls(self):
-        """Sampling calls made so far (the device counter; reading it synchronises)."""
-        return int(self.rng[1]) >> 16
+        """Sampling calls made so far (row group 0's device counter; reading it synchronises)."""
+        return int(self.rng[2])
 
     def set_calls(self, n):
-        """Rewind / advance the Philox call counter (the same key and counter draw the same numbers)."""
-        self.rng[1] = int(n) << 16
+        """Rewind / advance the Philox call counters of every row group (the same key and counter draw
+        the same numbers)."""
+        self.rng[2:] = int(n)
 
     def _rows(self, t, width, name):
         if t is None:
@@ -135,6 +156,7 @@ class MlpPolicyKernel:
         if src is None:
             raise ValueError("nothing to do: neither obs nor prev")
         self._n = int(n_rows) if n_rows is not None else src.numel() // self.n_obs
+        self._fit(self._n)
         args = [self._rows(obs, self.n_obs, "obs"), self._rows(act_env, self.n_act, "act_env"),
                 self._rows(buf_obs, self.n_obs, "buf_obs"), self._rows(buf_act, self.n_act, "buf_act"),
                 self._rows(buf_logp, 1, "buf_logp"), self._rows(buf_val, 1, "buf_val")]
@@ -151,7 +173,7 @@ class MlpPolicyKernel:
         stream = torch.cuda.current_stream(self.device).cuda_stream
         _check("gpd_policy_rollout_step", self._lib.gpd_policy_rollout_step(
             ctypes.byref(self._st), self._n, *args, 1 if deterministic else 0, ctypes.c_void_p(self.rng.data_ptr()),
-            *pv, float(gamma), *outs, ctypes.c_void_p(stream)))
+            self.rng_groups, *pv, float(gamma), *outs, ctypes.c_void_p(stream)))
 
     def gae(self, rew, val, done, last_val, gamma, lam, adv, ret):
         """GAE over a rollout, bit-identical to examples/learn.py's torch loop: [T, E] tensors."""

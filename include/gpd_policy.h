@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GPD_POLICY_ABI_VERSION 1
+#define GPD_POLICY_ABI_VERSION 2
 #define GPD_POLICY_HIDDEN 64      /* SB3 MlpPolicy net_arch [64, 64], tanh */
 #define GPD_POLICY_MAX_OBS 192    /* obs row width: both networks' layers staged in 160 KB of LDS */
 #define GPD_POLICY_MAX_ACT 8
@@ -47,9 +47,12 @@ typedef struct gpd_mlp_policy {
  *   buf_obs / buf_act / buf_logp / buf_val: this step's rollout-buffer rows (each nullable);
  *             buf_val alone (act_env, buf_act, buf_logp NULL) = the critic only (last value)
  *   deterministic: 1 = action = mean (EvalCallback), no sample
- *   rng       device uint64[3] = {seed, call counter << 16 | ticket, 0}: the Philox4x32-10 key and
- *             counter; every call that samples advances the counter by one (on the device; the
- *             ticket is 0 between calls)
+ *   rng       device uint64[2 + rng_groups] = {seed, 0, counter of row group 0, of group 1, ...}: the
+ *             Philox4x32-10 key and a call counter per group of 16 rows (rows 16 g .. 16 g + 15); every
+ *             call that samples advances the counters of the groups it covers by one, each in the
+ *             block that samples the group (no atomic: one reader-writer per counter and call).
+ *             Calls over the same n_rows keep the counters equal: the call count of the whole batch
+ *   rng_groups  counters in rng (>= ceil(n_rows / 16) when sampling)
  * Previous step (all nullable together; reward == NULL skips the part):
  *   reward [n_rows] f32, terminated / truncated [n_rows] u8 (gpd_step's outputs),
  *   terminal_obs [n_rows][n_obs] (the env's terminal rows), gamma:
@@ -58,8 +61,9 @@ typedef struct gpd_mlp_policy {
  *   buf_done[i] = terminated[i] || truncated[i]  (1.0f / 0.0f) */
 int gpd_policy_rollout_step(const gpd_mlp_policy* policy, int n_rows, const float* obs, float* act_env,
                             float* buf_obs, float* buf_act, float* buf_logp, float* buf_val, int deterministic,
-                            uint64_t* rng, const float* reward, const uint8_t* terminated, const uint8_t* truncated,
-                            const float* terminal_obs, float gamma, float* buf_rew, float* buf_done, void* stream);
+                            uint64_t* rng, int rng_groups, const float* reward, const uint8_t* terminated,
+                            const uint8_t* truncated, const float* terminal_obs, float gamma, float* buf_rew,
+                            float* buf_done, void* stream);
 
 /* GAE(gamma, lambda) over a finished rollout (SB3 RolloutBuffer.compute_returns_and_advantage):
  * rew / val / done [n_steps][n_rows] f32, last_val [n_rows] -> adv, ret [n_steps][n_rows];

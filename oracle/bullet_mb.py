@@ -318,17 +318,24 @@ CORE_MARGINS = (0.001, 0.003, 0.006, 0.011)   # core shrink per level (the first
 CORE_SEP = 1e-4             # core distance below which a level has no well-conditioned normal
 SAT_SLACK = 1e-9            # the broadphase's separating-axis reject keeps this much against rounding
 SIMDSQRT12 = 0.7071067811865475244008443621048490
-RIM_SAMPLES = 8             # the azimuth grid (k * 45 deg in btPlaneSpace1 of the axis): the first trust radius
-RIM_STARTS = (0, 2, 4, 6)   # the Newton starts on it (0 / 90 / 180 / 270 deg; round 5 ran all 8: the same
-                            # accuracy bound at half the chains, tests/test_oracle_drone_contact.py)
-RIM_ITERS = 8               # trust-region Newton steps from each start azimuth
+RIM_SAMPLES = 16            # the azimuth grid (k * 22.5 deg in btPlaneSpace1 of the axis): the first trust radius
+RIM_STARTS = tuple(range(16))   # the Newton starts on it: every grid azimuth
+RIM_ITERS = 5               # trust-region Newton steps from each start azimuth.  Round 6: 16 starts x 5
+                            # steps (6 evaluations a chain) instead of 4 x 8 (9): on the GPU a pair's chains
+                            # run side by side, one per lane, so a chain's length is the latency.  Against the
+                            # certified exact distance: max 3.4e-6 m over 1 095 random near pairs (4 x 8:
+                            # 2.0e-6; 8 x 5: 5.3e-5, 8 x 6: 1.4e-5), tests/test_oracle_drone_contact.py
 RIM_ACCEPT = 1e-10          # a step must lower the squared distance by this fraction (rounding-proof)
 RIM_SAME = 1e-4             # starts whose squared distances agree to this fraction count as one minimum (sized
                             # for the f32 kernel's rounding, so both precisions pick the same start)
 PAIR_TIE = 1e-7             # candidates within this of the closest count as tied: the first wins (m); sized
                             # for the f32 kernel (a level side-by-side pair ties its lateral line and both rims)
-RIM_COS = (1.0, SIMDSQRT12, 0.0, -SIMDSQRT12, -1.0, -SIMDSQRT12, 0.0, SIMDSQRT12)   # k * 45 deg
-RIM_SIN = (0.0, SIMDSQRT12, 1.0, SIMDSQRT12, 0.0, -SIMDSQRT12, -1.0, -SIMDSQRT12)
+# k * 22.5 deg: the first quadrant's (cos, sin) rotated by quarter turns, negations as 0 - x (no -0.0),
+# exactly as gpd_kernels.h np_rim_task forms them
+_C1, _S1 = 0.92387953251128674, 0.38268343236508978      # cos / sin 22.5 deg
+_QC, _QS = (1.0, _C1, SIMDSQRT12, _S1), (0.0, _S1, SIMDSQRT12, _C1)
+RIM_COS = tuple((_QC[q], 0.0 - _QS[q], 0.0 - _QC[q], _QS[q])[k] for k in range(4) for q in range(4))
+RIM_SIN = tuple((_QS[q], _QC[q], 0.0 - _QS[q], 0.0 - _QC[q])[k] for k in range(4) for q in range(4))
 
 
 def plane_space(n):
@@ -460,7 +467,7 @@ def rim_closest(C, e1, e2, r, h):
     the RIM_STARTS azimuths (rim_newton) and the lowest start whose squared distance is within the
     relative RIM_SAME of the smallest wins: chains that reached one minimum agree on f to rounding
     but on the point only to ~sqrt(RIM_ACCEPT) (a flat minimum), so a plain argmin would pick its
-    chain by rounding noise.  On the GPU the 4 x 4 starts of a pair run on 16 lanes at once."""
+    chain by rounding noise.  On the GPU the 4 x 16 starts of a pair run on 64 lanes at once."""
     out = [rim_newton(C, e1, e2, r, h, RIM_COS[k], RIM_SIN[k]) for k in RIM_STARTS]
     fmin = min(o[0] for o in out)
     k = next(i for i, o in enumerate(out) if o[0] <= fmin * (1.0 + RIM_SAME))
