@@ -146,9 +146,9 @@ def test_handoff_two_ranks_bit_identical_to_one_sim(kw, mode):
                          ids=["all_gather", "gather", "all_gather_graph", "gather_graph"])
 def test_handoff_rccl_one_rank(mode, graph_at):
     """The RCCL code path of the hand-off (backend "nccl" = RCCL on ROCm) on the one-GPU box:
-    a one-rank group with the collectives forced on, so that the action all_to_all_single, the
-    record gather (all_to_all_single) / all_gather_into_tensor of uint8 / float32 device tensors
-    and the pack / unpack kernels really execute on RCCL.  Bit-identical to one sim stepping the
+    a one-rank group with the collectives forced on, so that the action send / recv, the record
+    gather (grouped ncclSend / ncclRecv) / ncclAllGather through rccl.RcclComm and the pack /
+    unpack kernels really execute on RCCL.  Bit-identical to one sim stepping the
     same envs.  Steady-state steps run under torch.cuda.set_sync_debug_mode("error"): the
     hand-off never waits for the device.  ``graph_at``: from that step on, every step replays ONE
     captured hipGraph (scatter + step + pack + collective + unpack)."""
