@@ -900,6 +900,10 @@ __device__ __forceinline__ void plane_contact(Drone<R>& s, const R Rm[9], const 
 //   * a normal row's clamp at 0 applies new - old (== -old when clamped, the oracle's form);
 //   * residual: the largest |row residual| is squared once per iteration (squaring is monotonic,
 //     so this equals the largest squared residual exactly).
+// (Round 6: a look-ahead form - unit k's row product as J_k v_{k-2} plus a per-solve coupling
+// times d_{k-1}, one dependent FMA after its predecessor - measured 61.5 -> 72.1 us on the 4096-env
+// PYB crash batch, branch-free and without the row skips: the loop is issue-bound, not chain-bound;
+// profiles/r6/contact/probe_plane_lookahead_ab.log.)
 // A solve holds its wave for (setup + iterations x ~300 instructions); a crashing
 // batch's worst solve and the multi-drone batches' solves run into the iteration cap (50), so the
 // per-iteration instruction count is what the PYB step time follows.  PK's park() / unpark()
@@ -935,9 +939,6 @@ __device__ __forceinline__ float max_abs(float r, float x) {
   asm("v_max_f32 %0, %1, |%2|" : "=v"(o) : "v"(r), "v"(x));
   return o;
 }
-#ifndef GPD_PC_LOOKAHEAD
-#define GPD_PC_LOOKAHEAD 0   // 1: the look-ahead form of the sweep (plane_contact_regs)
-#endif
 template <typename R, class PK = NoPark>
 __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], const Consts<R>& c, const DynK<R>& k,
                                                    const PK& pk = PK(), bool skip = false) {
@@ -1004,124 +1005,6 @@ __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], c
   bool done = !any;
   const R mu = c.mu, resid = c.resid, im = k.inv_m;
   const int iters = c.iters;
-#if GPD_PC_LOOKAHEAD
-  // Look-ahead form of the same sweep (round 6).  Unit k's row product at v_{k-1} (the velocity
-  // change after unit k-1) is J_k v_{k-2} + (J_k M^-1 J_{k-1}^T) d_{k-1}: the first term is formed
-  // while unit k-1 is still being solved, and with c = jdi_k (J_k M^-1 J_{k-1}^T) formed once per
-  // solve, unit k's projected impulse is  t_k - c d_{k-1}  with  t_k = lam_k + (rhs_k - jdi_k
-  // J_k v_{k-2}): ONE dependent FMA after its predecessor instead of the whole row product, and
-  // unit k-1's update of v runs beside it.  The units, in the sweep's order: the 4 normal rows
-  // (all of them: a row no lane touches has rhs = jdi = 0 and solves to d = 0 exactly, as the
-  // skipped row did), then the 4 friction pairs (d = 0 on lanes with no normal impulse at the
-  // point); N0's predecessor is the previous iteration's F3.  The same projections, clamps, cone
-  // and stopping rule; every value equals the velocity form's up to rounding.
-  // coupling of a row (direction e, world arm a = r x e) with another (e', g' = I_w^-1 (r' x e')):
-  // J M^-1 J'^T = im (e . e') + a . g'
-  R cN[4][2];        // N_p on its predecessor: N_{p-1} (p > 0: [0]) or F3 (p = 0: [0] row 1, [1] row 2)
-  R cF0[2];          // F0's rows on N3
-  R cF[4][2][2];     // F_p's row r on F_{p-1}'s row s (p > 0)
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const R ax = rwy[p], ay = -rwx[p];                              // normal: e = z, a = (ry, -rx, 0)
-    const R f1x = rwz[p], f1z = -rwx[p], f2y = rwz[p], f2z = -rwy[p];   // (0,-1,0): (rz, 0, -rx); (1,0,0): (0, rz, -ry)
-    if (p == 0) {
-      cN[0][0] = jdi[0][0] * (ax * g[3][1][0] + ay * g[3][1][1]);
-      cN[0][1] = jdi[0][0] * (ax * g[3][2][0] + ay * g[3][2][1]);
-    } else {
-      cN[p][0] = jdi[p][0] * (im + (ax * g[p - 1][0][0] + ay * g[p - 1][0][1]));
-      cN[p][1] = R(0);
-      cF[p][0][0] = jdi[p][1] * (im + (f1x * g[p - 1][1][0] + f1z * g[p - 1][1][2]));
-      cF[p][0][1] = jdi[p][1] * (f1x * g[p - 1][2][0] + f1z * g[p - 1][2][2]);
-      cF[p][1][0] = jdi[p][2] * (f2y * g[p - 1][1][1] + f2z * g[p - 1][1][2]);
-      cF[p][1][1] = jdi[p][2] * (im + (f2y * g[p - 1][2][1] + f2z * g[p - 1][2][2]));
-    }
-    if (p == 0) {
-      cF0[0] = jdi[0][1] * (f1x * g[3][0][0] + f1z * g[3][0][2]);
-      cF0[1] = jdi[0][2] * (f2y * g[3][0][1] + f2z * g[3][0][2]);
-    }
-  }
-  R pf1 = R(0), pf2 = R(0);   // F3's impulse changes of the previous iteration (not yet in v)
-  pk.park();   // from here on only the solve's own values are live in this thread
-#ifdef GPD_CONTACT_STATS
-  int it_used = 0;
-  const unsigned long long nact = __ballot(any);
-  const unsigned long long t_loop = __builtin_readcyclecounter();
-#endif
-  for (int it = 0; it < iters; ++it) {
-    if (__ballot(!done) == 0ull) break;
-#ifdef GPD_CONTACT_STATS
-    it_used = it + 1;
-#endif
-    if (!done) {
-      R res = R(0);
-      R dn[4];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {                  // normal rows
-        const R t = lam[p][0] + (rhs[p][0] - jdi[p][0] * (DLz + (rwy[p] * DAx - rwx[p] * DAy)));
-        // the predecessor's update of v (it is in t's correction below, and in the next unit's t)
-        if (p == 0) {
-          DLy = DLy - im * pf1;
-          DLx = DLx + im * pf2;
-          DAx = DAx + g[3][1][0] * pf1; DAy = DAy + g[3][1][1] * pf1; DAz = DAz + g[3][1][2] * pf1;
-          DAx = DAx + g[3][2][0] * pf2; DAy = DAy + g[3][2][1] * pf2; DAz = DAz + g[3][2][2] * pf2;
-        } else {
-          const R d = dn[p - 1];
-          DLz = DLz + im * d;
-          DAx = DAx + g[p - 1][0][0] * d; DAy = DAy + g[p - 1][0][1] * d; DAz = DAz + g[p - 1][0][2] * d;
-        }
-        const R sum = p == 0 ? t - (cN[0][0] * pf1 + cN[0][1] * pf2) : t - cN[p][0] * dn[p - 1];
-        const R ln = sum < R(0) ? R(0) : sum;
-        dn[p] = ln - lam[p][0];
-        lam[p][0] = ln;
-        res = max_abs(res, dn[p] * jdn[p]);
-      }
-      R df1[4], df2[4];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {                  // friction pairs on the cone
-        const R lnrm = lam[p][0];
-        const bool on = lnrm > R(0);
-        const R lim = mu * lnrm;
-        const R l1 = lam[p][1], l2 = lam[p][2];
-        const R t1 = l1 + (rhs[p][1] - jdi[p][1] * ((rwz[p] * DAx - rwx[p] * DAz) - DLy));
-        const R t2 = l2 + (rhs[p][2] - jdi[p][2] * ((rwz[p] * DAy - rwy[p] * DAz) + DLx));
-        R s1, s2;
-        if (p == 0) {
-          const R d = dn[3];
-          DLz = DLz + im * d;
-          DAx = DAx + g[3][0][0] * d; DAy = DAy + g[3][0][1] * d; DAz = DAz + g[3][0][2] * d;
-          s1 = t1 - cF0[0] * d;
-          s2 = t2 - cF0[1] * d;
-        } else {
-          const R e1 = df1[p - 1], e2 = df2[p - 1];
-          DLy = DLy - im * e1;
-          DLx = DLx + im * e2;
-          DAx = DAx + g[p - 1][1][0] * e1; DAy = DAy + g[p - 1][1][1] * e1; DAz = DAz + g[p - 1][1][2] * e1;
-          DAx = DAx + g[p - 1][2][0] * e2; DAy = DAy + g[p - 1][2][1] * e2; DAz = DAz + g[p - 1][2][2] * e2;
-          s1 = t1 - (cF[p][0][0] * e1 + cF[p][0][1] * e2);
-          s2 = t2 - (cF[p][1][0] * e1 + cF[p][1][1] * e2);
-        }
-        const R m2 = s1 * s1 + s2 * s2;
-        const bool clip = m2 > lim * lim;            // onto the cone: (s1, s2) * lim / |s|
-        const R f = lim * g_rsqrt(clip ? m2 : R(1));
-        s1 = clip ? s1 * f : s1;
-        s2 = clip ? s2 * f : s2;
-        df1[p] = on ? s1 - l1 : R(0);
-        df2[p] = on ? s2 - l2 : R(0);
-        lam[p][1] = on ? s1 : l1;
-        lam[p][2] = on ? s2 : l2;
-        res = on ? max_abs(res, df1[p] + df2[p]) : res;
-      }
-      pf1 = df1[3];
-      pf2 = df2[3];
-      done = res * res <= resid;
-    }
-  }
-  // F3's last impulse changes (lanes that stopped carry theirs from their last iteration)
-  DLy = DLy - im * pf1;
-  DLx = DLx + im * pf2;
-  DAx = DAx + g[3][1][0] * pf1; DAy = DAy + g[3][1][1] * pf1; DAz = DAz + g[3][1][2] * pf1;
-  DAx = DAx + g[3][2][0] * pf2; DAy = DAy + g[3][2][1] * pf2; DAz = DAz + g[3][2][2] * pf2;
-#else
   // normal rows some lane of the wave touches (a row that only finished lanes need runs with
   // them masked off and changes nothing)
   bool wrow[4];
@@ -1181,7 +1064,6 @@ __device__ __forceinline__ void plane_contact_regs(Drone<R>& s, const R Rm[9], c
       done = res * res <= resid;
     }
   }
-#endif
   pk.unpark();
 #ifdef GPD_CONTACT_STATS
   const unsigned long long t_end = __builtin_readcyclecounter();
