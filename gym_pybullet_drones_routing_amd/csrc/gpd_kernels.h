@@ -1124,17 +1124,10 @@ __device__ __forceinline__ void eres_max(DcLds<R>& L, int env, R rr) {
 // closed-form candidates and the selection by the pair's own lane (lane = slot), margin level by
 // margin level while some pair's cores overlap; then the fallback and the face manifold.  Lane
 // ln < nthis stages its pair's result in L.st and its face-point mask in L.nsp[ln] and returns its
-// contact count.  A call: its registers stay out of dc_solve's Gauss-Seidel loops.
+// contact count.  dc_narrow_pass: a call, so its registers stay out of dc_solve's Gauss-Seidel
+// loops; dc_solve_body<.., INL = true> inlines it (see DcHookT).
 template <typename R>
-#ifndef GPD_NP_INLINE
-#define GPD_NP_INLINE 0   // A/B builds: 1 = the narrowphase pass inlined into dc_solve
-#endif
-#if GPD_NP_INLINE
-__device__ __forceinline__
-#else
-__device__ __noinline__
-#endif
-int dc_narrow_pass(const Consts<R>* cp, int ln, int nthis) {
+__device__ __forceinline__ int dc_narrow_pass_body(const Consts<R>* cp, int ln, int nthis) {
   DcLds<R>& L = dc_lds<R>();
   const Consts<R>& c = *cp;
 #ifdef GPD_CONTACT_STATS
@@ -1302,10 +1295,14 @@ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthis) {
                                           // mask, and 1 + the slot the closest point replaces (0: none)
   return con ? (rep >= 0 ? 4 : 1 + __popc(fmask)) : 0;
 }
+template <typename R>
+__device__ __noinline__ int dc_narrow_pass(const Consts<R>* cp, int ln, int nthis) {
+  return dc_narrow_pass_body<R>(cp, ln, nthis);
+}
 // plane: the ground plane is on (the island solve takes the plane rows of drones in a pair contact
 // that touch it, bullet_mb.drone_contact(plane=True)); nact: the block's drones
-template <typename R, bool STAGE>
-__device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln, DcPairs dp, bool plane) {
+template <typename R, bool STAGE, bool INL>
+__device__ __forceinline__ void dc_solve_body(const Consts<R>* cp, R inv_m, R dt, int ln, DcPairs dp, bool plane) {
 #ifdef GPD_CONTACT_STATS
   const unsigned long long t0 = __builtin_readcyclecounter();
   unsigned long long t1 = t0, t2 = t0, t_np = t0;
@@ -1358,7 +1355,7 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
 #ifdef GPD_CONTACT_STATS
     n_near += ln < nthis ? 1 : 0;
 #endif
-    const int cnt = dc_narrow_pass<R>(cp, ln, nthis);
+    const int cnt = INL ? dc_narrow_pass_body<R>(cp, ln, nthis) : dc_narrow_pass<R>(cp, ln, nthis);
     int total;
     const int off = wave_excl_scan(cnt, ln, total);
     if (cnt > 0) {
@@ -1662,10 +1659,22 @@ __device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln,
 #endif
   wave_lds_sync();   // the caller reads the velocity deltas
 }
+// the solve as a call (its registers out of the caller's allocation; the run-time-flag kernels and
+// the downwash flag sets)
+template <typename R, bool STAGE>
+__device__ GPD_DC_ATTR void dc_solve(const Consts<R>* cp, R inv_m, R dt, int ln, DcPairs dp, bool plane) {
+  dc_solve_body<R, STAGE, false>(cp, inv_m, dt, ln, dp, plane);
+}
 // the hook bullet_substep calls (multi-drone envs of one-wave blocks): pk parks the caller's
 // values in LDS around the solve (bullet_substep), so nothing of the substep loop is live across
-// the call and the loop's own register allocation does not see the solve
-struct DcHook {
+// the call and the loop's own register allocation does not see the solve.  INL: the solve and its
+// narrowphase inlined (no call, no callee-saved register spills): the compiled-in PYB flag sets
+// without downwash - the 2-drone MultiHover PYB batch 127.1 -> 119.5 us, while the 8-drone
+// PYB_GND_DRAG_DW batch, whose island sweeps then share the kernel's register allocation, went
+// 3 103 -> 3 535 us (profiles/r6/contact/probe_inline_ab.log); inlined only here: 2-drone
+// 126.7 -> 119.9 us, 8-drone PYB 16.3 -> 14.2 us, 8-drone PYB_GND_DRAG_DW unchanged (probe_selective_inline_ab.log)
+template <bool INL>
+struct DcHookT {
   int tid;
   DcPairs dp;
   // returns whether this lane's drone joined the island (its plane rows were solved here)
@@ -1729,7 +1738,8 @@ struct DcHook {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const unsigned long long tr2 = __builtin_readcyclecounter();
 #endif
-      dc_solve<R, PK::kStage>(&c, inv_m, dt, ln, dpc, plane);
+      if (INL) dc_solve_body<R, PK::kStage, true>(&c, inv_m, dt, ln, dpc, plane);
+      else dc_solve<R, PK::kStage>(&c, inv_m, dt, ln, dpc, plane);
 #ifdef GPD_CONTACT_STATS
       const unsigned long long tr3 = __builtin_readcyclecounter();
 #endif
@@ -1783,7 +1793,9 @@ __device__ __forceinline__ void substep_block(Drone<R>& s, R rpm[4], R W[4], R l
     }
     wave_lds_sync();
   }
-  if (MULTI) dyn_substep<R, PF, ANGV, 1, DcHook>(s, rpm, W, last, dw, c, k, DcHook{tid, dcp});
+  // the drone contact inlined in the compiled-in flag sets without downwash (DcHookT)
+  constexpr bool kDcInl = PF != kPfRuntime && (PF & F_DW) == 0;
+  if (MULTI) dyn_substep<R, PF, ANGV, 1, DcHookT<kDcInl>>(s, rpm, W, last, dw, c, k, DcHookT<kDcInl>{tid, dcp});
   else dyn_substep<R, PF, ANGV>(s, rpm, W, last, dw, c, k);
 }
 
