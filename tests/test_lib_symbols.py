@@ -54,6 +54,36 @@ def test_host_only_entry_points(lib):
     assert p.kf == 3.16e-10 and p.m == 0.027
     assert lib.gpd_destroy(None) == _lib.GPD_EINVAL
     assert lib.gpd_state_bytes(None) == 0
+    # the contact solver's parameters (setPhysicsEngineParameter) are validated before any device call
+    cfg = _lib.Config(n_envs=4, drones_per_env=1, pyb_freq=240, ctrl_freq=30, act_type=_lib.GPD_ACT_RPM,
+                      task=1, physics_flags=0, precision=_lib.GPD_F64, autoreset=1, episode_len_sec=8.0)
+    out = ctypes.c_void_p()
+    for it, res, msg in ((1001, 0.0, b"solver_iterations"), (-1, 0.0, b"solver_iterations"),
+                         (0, float("nan"), b"solver_residual")):
+        cfg.solver_iterations, cfg.solver_residual = it, res
+        assert lib.gpd_create(ctypes.byref(p), ctypes.byref(cfg), ctypes.byref(out)) == _lib.GPD_EINVAL
+        assert msg in lib.gpd_last_error()
+
+
+def test_policy_library_host_checks():
+    """libgpd_policy.so: ABI 2 and the argument checks that run before any device call - in
+    particular the per-row-group Philox counters must cover every sampled row."""
+    from gym_pybullet_drones_routing_amd import _build, policy
+    _build.build_policy()
+    pl = policy.load()
+    assert pl.gpd_policy_abi_version() == policy.GPD_POLICY_ABI_VERSION == 2
+    st = policy.MlpPolicyStruct()
+    st.n_obs, st.n_act = 72, 4
+    fake = 256          # never dereferenced: every call below fails its host-side checks
+    for n in ("pi_w1", "pi_b1", "pi_w2", "pi_b2", "pi_w3", "pi_b3", "vf_w1", "vf_b1", "vf_w2", "vf_b2", "vf_w3",
+              "vf_b3", "log_std"):
+        setattr(st, n, fake)
+    vp = ctypes.c_void_p
+    rc = pl.gpd_policy_rollout_step(ctypes.byref(st), 100, vp(fake), vp(fake), None, vp(fake), None, None, 0,
+                                    vp(fake), 6, None, None, None, None, 0.99, None, None, None)
+    assert rc == -1 and b"row-group counters" in pl.gpd_policy_last_error()
+    assert pl.gpd_policy_rollout_step(None, 100, None, None, None, None, None, None, 0, None, 0, None, None, None,
+                                      None, 0.99, None, None, None) == -1
 
 
 @pytest.mark.parametrize("E,D,W", [(4096, 1, 72), (3, 1, 72), (5, 2, 27), (1, 8, 36), (4095, 3, 27)])
