@@ -833,12 +833,42 @@ def main():
         raise SystemExit(f"bench.py: rank exit codes {codes}")
 
 
+_JSON_FD = None     # the process's real stdout while fd 1 points at stderr (run())
+
+
+class _HandoffWatchdog:
+    """N > 1: the hand-off legs run last, and theirs are the only collectives of the run that span
+    GPUs (one-rank RCCL is all this pipeline can execute before the driver's multi-GPU runs).
+    Should they hang, the weak-scaling line must still come out: after ``limit`` s rank 0 writes
+    the line measured so far with ``handoff = {"error": ...}`` to the real stdout and every rank
+    ends its process (os._exit: no collective teardown to wait for)."""
+
+    def __init__(self, result, rank, limit):
+        import threading
+        self.result, self.rank, self.limit = result, rank, limit
+        self.timer = threading.Timer(limit, self._fire)
+        self.timer.daemon = True
+        self.timer.start()
+
+    def _fire(self):
+        if self.rank == 0 and self.result is not None and _JSON_FD is not None:
+            line = dict(self.result, handoff={"error": f"hand-off legs unfinished after {self.limit:.0f} s "
+                                                       "(watchdog; the step line above them is complete)"})
+            os.write(_JSON_FD, (json.dumps(line) + "\n").encode())
+        os._exit(0)
+
+    def cancel(self):
+        self.timer.cancel()
+
+
 def run(args):
     # the JSON line is the only thing this process writes to stdout: native libraries write to fd 1
     # directly (RCCL prints its version banner when it creates a communicator), so fd 1 points at
     # stderr until the line is printed; restored whatever happens (ADVICE r5)
+    global _JSON_FD
     sys.stdout.flush()
     json_fd = os.dup(1)
+    _JSON_FD = json_fd
     os.dup2(2, 1)
     try:
         result = _run(args)
@@ -846,6 +876,7 @@ def run(args):
         sys.stdout.flush()
         os.dup2(json_fd, 1)
         os.close(json_fd)
+        _JSON_FD = None
     if result is not None:
         print(json.dumps(result), flush=True)
 
@@ -978,6 +1009,7 @@ def _run(args):
         # optional leg: a failure is recorded, never the end of the run
         one_rank = world == 1
         created = False
+        dog = _HandoffWatchdog(result if rank == 0 else None, rank, 240.0) if world > 1 else None
         try:
             if one_rank and args.dist_backend == "nccl" and not torch.distributed.is_initialized():
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -1012,6 +1044,8 @@ def _run(args):
         except Exception as exc:
             result["handoff"] = {"error": f"{type(exc).__name__}: {exc}"}
         finally:
+            if dog is not None:
+                dog.cancel()
             if created:
                 torch.distributed.destroy_process_group()
 
