@@ -117,12 +117,18 @@ class RcclComm:
         st = self._stream()
         lib = self.lib
         _check(lib, "ncclGroupStart", lib.ncclGroupStart())
-        if self.rank == root:
-            base = recv.data_ptr()
-            for r in range(self.world):
-                _check(lib, "ncclRecv", lib.ncclRecv(ctypes.c_void_p(base + r * n * es), n, dt, r, self.comm, st))
-        _check(lib, "ncclSend", lib.ncclSend(ctypes.c_void_p(send.data_ptr()), n, dt, root, self.comm, st))
-        _check(lib, "ncclGroupEnd", lib.ncclGroupEnd())
+        ok = False
+        try:
+            if self.rank == root:
+                base = recv.data_ptr()
+                for r in range(self.world):
+                    _check(lib, "ncclRecv", lib.ncclRecv(ctypes.c_void_p(base + r * n * es), n, dt, r, self.comm, st))
+            _check(lib, "ncclSend", lib.ncclSend(ctypes.c_void_p(send.data_ptr()), n, dt, root, self.comm, st))
+            ok = True
+        finally:
+            rc = lib.ncclGroupEnd()     # the group is closed whatever failed inside it
+            if ok:
+                _check(lib, "ncclGroupEnd", rc)
 
     def scatter(self, send, recv, root):
         """recv [n] on every rank <- block r of ``root``'s send [world * n] (ignored elsewhere)."""
@@ -133,12 +139,18 @@ class RcclComm:
         st = self._stream()
         lib = self.lib
         _check(lib, "ncclGroupStart", lib.ncclGroupStart())
-        if self.rank == root:
-            base = send.data_ptr()
-            for r in range(self.world):
-                _check(lib, "ncclSend", lib.ncclSend(ctypes.c_void_p(base + r * n * es), n, dt, r, self.comm, st))
-        _check(lib, "ncclRecv", lib.ncclRecv(ctypes.c_void_p(recv.data_ptr()), n, dt, root, self.comm, st))
-        _check(lib, "ncclGroupEnd", lib.ncclGroupEnd())
+        ok = False
+        try:
+            if self.rank == root:
+                base = send.data_ptr()
+                for r in range(self.world):
+                    _check(lib, "ncclSend", lib.ncclSend(ctypes.c_void_p(base + r * n * es), n, dt, r, self.comm, st))
+            _check(lib, "ncclRecv", lib.ncclRecv(ctypes.c_void_p(recv.data_ptr()), n, dt, root, self.comm, st))
+            ok = True
+        finally:
+            rc = lib.ncclGroupEnd()
+            if ok:
+                _check(lib, "ncclGroupEnd", rc)
 
     def destroy(self):
         if self.comm:
