@@ -119,7 +119,8 @@ struct gpd_sim {
   int wt = 0;                     // SimView::wt (write-through store policy)
   int nc_magic = 0;               // SimView::nc_magic
   bool duo = false;               // step launches step_kernel_duo (two or three waves per block)
-  bool wide = false;              // D > 64: step_kernel_wide / integrate_kernel_wide, one env per workgroup
+  bool wide = false;              // step_kernel_wide / integrate_kernel_wide, one env per workgroup: D > 64,
+                                  // or an observation row too long for the one-wave kernels' LDS tile
   int step_waves = 1;             // waves per step block (1, 2, or 3 with the io wave)
   bool stream = false;            // streaming cache policies (step_kernel STREAM): batches past the MALL
   bool generic_pf = false;        // the run-time-flag step kernel even where a flag set is compiled in
@@ -312,6 +313,26 @@ const void* step_kernel_fn(const gpd_sim* s) {
   }
 }
 
+// static LDS of the run-time-flag step kernel of an action type (the one-wave kernel every sim
+// that is not wide can fall back to: upload_tables)
+template <typename R>
+size_t runtime_step_lds(int act, bool multi) {
+  const void* f;
+  switch (act) {
+    case GPD_ACT_RPM: f = step_fn_act<R, ACT_RPM>(multi, kPfRuntime, false); break;
+    case GPD_ACT_ONE_D_RPM: f = step_fn_act<R, ACT_ONE_D_RPM>(multi, kPfRuntime, false); break;
+    case GPD_ACT_PID: f = step_fn_pid<R, ACT_PID>(multi, kPfRuntime); break;
+    case GPD_ACT_VEL: f = step_fn_pid<R, ACT_VEL>(multi, kPfRuntime); break;
+    default: f = step_fn_pid<R, ACT_ONE_D_PID>(multi, kPfRuntime); break;
+  }
+  hipFuncAttributes fa;
+  if (hipFuncGetAttributes(&fa, f) != hipSuccess) {
+    (void)hipGetLastError();
+    return kLdsBytes;
+  }
+  return fa.sharedSizeBytes;
+}
+
 template <typename R>
 int upload_tables(gpd_sim* s) {
   std::vector<R> ini(s->init_tmpl.begin(), s->init_tmpl.end());
@@ -320,6 +341,7 @@ int upload_tables(gpd_sim* s) {
   HIP_TRY(hipMemcpy(s->d_init, ini.data(), ini.size() * sizeof(R), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(s->d_target, tgt.data(), tgt.size() * sizeof(R), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(s->d_consts, &c, sizeof(c), hipMemcpyHostToDevice));
+  if (s->wide) return GPD_OK;   // step_kernel_wide: no observation tile
   // the step kernel's static LDS (the PYB flag-set kernels park 44 KB of per-lane values around
   // the contact solve, gpd_device.h bullet_substep) beside the observation tile must fit the
   // workgroup's LDS; a long action history (high ctrl_freq) that leaves no room for it gets the
@@ -333,7 +355,8 @@ int upload_tables(gpd_sim* s) {
     HIP_TRY(hipFuncGetAttributes(&fa, f));
   }
   if (fa.sharedSizeBytes + (size_t)s->tile_bytes > kLdsBytes)
-    return fail(GPD_EUNSUPPORTED, "gpd_create: ctrl_freq too high (observation tile + the step kernel's LDS exceed 160 KiB)");
+    return fail(GPD_EUNSUPPORTED, "gpd_create: ctrl_freq too high for drone <-> drone contact (observation tile + "
+                                  "the step kernel's LDS exceed 160 KiB; GPD_F_NO_DRONE_CONTACT lifts the limit)");
   // the observation tile can exceed the 64 KiB default dynamic-LDS limit for long histories
   if (s->tile_bytes > 65536)
     HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, s->tile_bytes));
@@ -596,8 +619,17 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     want = std::max(s->D, (want / s->D) * s->D);
     if (C.drones_per_block > 0) want = std::max(s->D, std::min(full, (C.drones_per_block / s->D) * s->D));
     s->tpb = want;
-    // envs of more than 64 drones: one env per multi-wave workgroup (step_kernel_wide)
-    s->wide = s->D > kWave;
+    // envs of more than 64 drones: one env per multi-wave workgroup (step_kernel_wide).  Also an
+    // observation row too long for the one-wave kernels (their LDS tile of 64 rows beside the
+    // run-time-flag kernel's static LDS: a long action history, e.g. RPM actions at ctrl_freq 480)
+    // when the env has no drone <-> drone contact, which only the one-wave kernels solve: the wide
+    // kernel stores the rows from registers, one env per workgroup
+    const bool dc_env = (C.physics_flags & GPD_F_BULLET) && s->D > 1 && !(C.physics_flags & GPD_F_NO_DRONE_CONTACT);
+    const size_t tile = (size_t)step_tile_bytes(s->A, s->ring_len);
+    const size_t lds_rt = s->D > kWave ? 0
+                          : (C.precision == GPD_F64 ? runtime_step_lds<double>(C.act_type, s->D > 1)
+                                                    : runtime_step_lds<float>(C.act_type, s->D > 1));
+    s->wide = s->D > kWave || (!dc_env && tile + lds_rt > (size_t)kLdsBytes);
     if (s->wide) s->tpb = s->D;
   }
   s->npad = ((long long)s->N + 63) / 64 * 64;
@@ -628,7 +660,7 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     // division-free row/column split of the copy-out (t / NC for t <= 64)
     const int NC = s->A == 4 ? 3 + s->ring_len : 12 + s->ring_len * s->A;
     s->nc_magic = (65536 + NC - 1) / NC;
-    for (int t = 0; t <= kWave; ++t)
+    for (int t = 0; t <= kWave && !s->wide; ++t)   // (the wide kernel has no tile copy-out)
       if ((t * s->nc_magic) >> 16 != t / NC) {
         delete s;
         return fail(GPD_EUNSUPPORTED, "gpd_create: observation width not supported by the tile copy-out");
@@ -643,7 +675,7 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     // 5.33, but 8192 envs 5.72 -> 5.90 and 16384 envs 6.23 -> 7.20: with fuller blocks the
     // two-wave copy-out overlaps other blocks' work anyway.
     // gpd_config::step_waves overrides (1, 2 or 3).
-    const bool duo_ok = s->D == 1 && C.physics_flags == 0 &&
+    const bool duo_ok = !s->wide && s->D == 1 && C.physics_flags == 0 &&
                         (C.act_type == GPD_ACT_RPM || C.act_type == GPD_ACT_ONE_D_RPM);
     int waves = !duo_ok || s->N > 65536 ? 1 : (s->N <= 4096 ? 3 : 2);
     if (C.step_waves > 0) waves = duo_ok ? std::min(3, C.step_waves) : 1;
@@ -655,7 +687,7 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     // (~820 B per drone: state, ring, rows) is well past the 256 MB Infinity Cache (>= 512K drones;
     // 262144 envs = 215 MB stay with the default policies, 1M envs 194 -> 145 us with STREAM,
     // 4096 envs 4.93 -> 6.31 us had it been used there)
-    s->stream = !s->duo && s->D == 1 && C.physics_flags == 0 &&
+    s->stream = !s->duo && !s->wide && s->D == 1 && C.physics_flags == 0 &&
                 (C.act_type == GPD_ACT_RPM || C.act_type == GPD_ACT_ONE_D_RPM) && s->N >= (1 << 19);
     // the multi-wave kernels store their state plainly (measured 4096 envs 5.47 -> 5.37 us/step);
     // the single-wave kernel keeps write-through state stores (262144 envs 36.7 -> 35.9 us)
@@ -671,9 +703,10 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     const size_t state_bytes = (size_t)kStateComps * s->npad * (C.precision == GPD_F64 ? 8 : 4);
     if (state_bytes >= 0x7fffffffULL) s->wt &= ~2;
   }
-  if (s->tile_bytes > kLdsBytes) {
+  if (s->tile_bytes > kLdsBytes && !s->wide) {
     delete s;
-    return fail(GPD_EUNSUPPORTED, "gpd_create: ctrl_freq too high (observation tile exceeds 160 KiB of LDS)");
+    return fail(GPD_EUNSUPPORTED, "gpd_create: ctrl_freq too high for drone <-> drone contact (observation tile "
+                                  "exceeds 160 KiB of LDS; GPD_F_NO_DRONE_CONTACT lifts the limit)");
   }
 
   // derived constants (BaseAviary.py:117-128)

@@ -394,3 +394,42 @@ def test_contact_step_resynced_pyb_flag_kernels(D, aero, freq, prec, monkeypatch
         # in round 4: 1.75e-3 over 960 x 8 drone-substeps); the median is rounding
         assert np.median(err) <= 1e-5 and err.max() <= 5e-3
     sim.close()
+
+
+@pytest.mark.parametrize("D,aero", [(1, ()), (2, ("no_drone_contact",))], ids=["single_pyb", "multi2_pyb_no_drone_contact"])
+def test_contact_step_resynced_long_history_wide_kernel(D, aero):
+    """Physics.PYB at ctrl_freq = pyb_freq = 480: the 240-step RPM action history makes a
+    972-float observation row whose 64-row LDS tile (249 KB) no one-wave step kernel holds, and
+    gpd_create runs such envs (without drone <-> drone contact) on step_kernel_wide, one env per
+    workgroup, with its plane contact solve.  Checked resynced per step as the flag-set kernels
+    above (one step = one substep), f64 to 1e-12."""
+    from gym_pybullet_drones_routing_amd.enums import ActionType, Physics
+    rng = np.random.default_rng(46)
+    E, freq = 8, 480
+    T = freq // 2
+    raw0 = _crash_case(rng, E * D)
+    acts = rng.uniform(-1, 0.2, (T, E, D, 4)).astype(np.float32)
+    task = "multihover" if D > 1 else "hover"
+    envs = [RefAviary(num_drones=D, task=task, aero=aero, integrator="bullet", pyb_freq=freq, ctrl_freq=freq)
+            for _ in range(E)]
+    for e in range(E):
+        envs[e].set_raw_state(raw0[e * D:(e + 1) * D])
+    sim = _sim(n_envs=E, drones_per_env=D, task=task, precision="f64", act=ActionType.RPM, physics=Physics.PYB,
+               aero=aero, autoreset=False, pyb_freq=freq, ctrl_freq=freq)
+    assert sim.obs_width == 12 + 240 * 4
+    assert sim.constants.drones_per_block == D          # one env per workgroup: the wide kernel
+    errs, low = [], 0
+    for t in range(T):
+        sim.set_raw_state(np.concatenate([oracle_raw(ev) for ev in envs]))
+        o, _, _, _ = sim.step(torch.from_numpy(acts[t]).cuda())
+        g = sim.raw_state().cpu().numpy()
+        for e, ev in enumerate(envs):
+            ev.step(acts[t, e])
+        r = np.concatenate([oracle_raw(ev) for ev in envs])
+        low += int((r[:, 2] < 0.02).sum())
+        errs.append(state_rel_err(g[:, :16], r[:, :16]))
+    err = np.array(errs)
+    print(f"\n[parity] long-history wide kernel D={D} {aero}: max {err.max():.3e} median {np.median(err):.3e}")
+    assert low > E * D * T // 6
+    assert err.max() <= 1e-12
+    sim.close()

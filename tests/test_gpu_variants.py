@@ -63,6 +63,25 @@ def test_frequencies_step_parity(pyb, ctrl, act):
                  ref_kw=dict(pyb_freq=pyb, ctrl_freq=ctrl))
 
 
+@pytest.mark.parametrize("D,act,task", [(1, "rpm", "hover"), (2, "rpm", "multihover"), (1, "pid", "hover"),
+                                        (3, "vel", "multihover")])
+def test_long_history_wide_kernel_step_parity(D, act, task):
+    """ctrl_freq 480 (pyb_freq 960): the 240-step action history makes observation rows of
+    12 + 240 A floats (972 for RPM, 732 for PID / VEL), whose 64-row LDS tile no one-wave step
+    kernel holds; gpd_create runs these envs on step_kernel_wide, one env per workgroup
+    (drones_per_block == D), rows stored from registers."""
+    rng = np.random.default_rng(34)
+    E, T = 6, 40
+    A = 4 if act in ("rpm", "vel") else 3
+    acts = np.clip(rng.normal(0, 0.2, (T, E, D, A)), -1, 1).astype(np.float32)
+    from gym_pybullet_drones_routing_amd.enums import ActionType
+    probe = _sim(n_envs=E, drones_per_env=D, task=task, act=ActionType(act), pyb_freq=960, ctrl_freq=480)
+    assert probe.constants.drones_per_block == D and probe.obs_width == 12 + 240 * A
+    probe.close()
+    _compare_run(acts, E, D=D, act=act, task=task, sim_kw=dict(pyb_freq=960, ctrl_freq=480),
+                 ref_kw=dict(pyb_freq=960, ctrl_freq=480))
+
+
 def test_initial_pose_step_parity():
     """Custom INIT_XYZS / INIT_RPYS: the reset template goes through the Bullet orientation
     round trip (quat from Euler -> btTransform -> readback)."""
