@@ -2641,6 +2641,54 @@ __device__ __forceinline__ R wide_downwash(const Drone<R>& s, R* sx, R* sy, R* s
   return dw;
 }
 
+// The history columns of an env's D observation rows (and terminal rows with TROW): ring slots
+// head+1 .. head+L-1 of each drone, copied by every thread of the workgroup (ACT's A floats per
+// slot, float4 items for A = 4), kWideU loads in flight per thread before their stores.
+constexpr int kWideU = 4;
+template <typename R, int A>
+__device__ __forceinline__ void wide_history(const SimView<R>& v, const StepIO<R>& io, long long n0, int D, int head,
+                                             bool trow) {
+  const int L = v.ring_len, Wd = v.W, H = L - 1, nth = blockDim.x;
+  constexpr int G = A == 4 ? 4 : 1;              // floats per item
+  const int per = H * (A / G);                   // items per drone
+  const int total = D * per;
+  for (int i0 = 0; i0 < total; i0 += nth * kWideU) {
+    float x[kWideU][G];
+    long long dst[kWideU];
+#pragma unroll
+    for (int u = 0; u < kWideU; ++u) {
+      const int i = i0 + u * nth + (int)threadIdx.x;
+      dst[u] = -1;
+      if (i < total) {
+        const int dq = i / per, r = i - dq * per;
+        const int k = G == 4 ? r : r / A, j = G == 4 ? 0 : r - k * A;
+        int slot = head + 1 + k;
+        slot -= slot >= L ? L : 0;
+        const float* src = v.ring + ridx(n0 + dq, slot, L, A) + j;
+        if (G == 4) {
+          const float4 q = *reinterpret_cast<const float4*>(src);
+          x[u][0] = q.x; x[u][G > 1 ? 1 : 0] = q.y; x[u][G > 2 ? 2 : 0] = q.z; x[u][G > 3 ? 3 : 0] = q.w;
+        } else {
+          x[u][0] = *src;
+        }
+        dst[u] = (n0 + dq) * Wd + 12 + k * A + j;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kWideU; ++u) {
+      if (dst[u] < 0) continue;
+      if (G == 4) {
+        const float4 q = make_float4(x[u][0], x[u][G > 1 ? 1 : 0], x[u][G > 2 ? 2 : 0], x[u][G > 3 ? 3 : 0]);
+        *reinterpret_cast<float4*>(io.obs + dst[u]) = q;
+        if (trow) *reinterpret_cast<float4*>(io.terminal_obs + dst[u]) = q;
+      } else {
+        io.obs[dst[u]] = x[u][0];
+        if (trow) io.terminal_obs[dst[u]] = x[u][0];
+      }
+    }
+  }
+}
+
 // MAXT: the workgroup size bound the instantiation is compiled for (256 / 512 / 1024 threads:
 // the register budget per lane halves with each doubling, 1024 spills to scratch).
 template <typename R, int ACT, int MAXT>
@@ -2730,25 +2778,19 @@ __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R>
   const bool do_reset = done && v.autoreset;
   float row12[12] = {(float)s.px, (float)s.py, (float)s.pz, roll, pitch, yaw,
                      (float)s.vx, (float)s.vy, (float)s.vz, (float)s.ax, (float)s.ay, (float)s.az};
+  const int L = v.ring_len, Wd = v.W;
+  // history columns: ring slots head+1 .. head+L-1 (oldest first), then the current action
+  // (BaseRLAviary.py:307-319); the same for the terminal row and the (reset) observation.  The
+  // env's history columns are copied by the whole workgroup, kWideU independent loads per thread
+  // before their stores: a lane copying its own row element by element waited out one memory
+  // round trip per element (680 us per step for 4096 single-drone envs with a 240-step history)
+  wide_history<R, A>(v, io, e * D, D, head, do_reset && io.terminal_obs);
   // every wave has read ctr[e] (kernel entry) before lane d == 0 overwrites it below; without a
   // task, downwash or contact no other workgroup barrier orders the two
   __syncthreads();
   if (!active) return;
-  const int L = v.ring_len, Wd = v.W;
-  // history columns: ring slots head+1 .. head+L-1 (oldest first), then the current action
-  // (BaseRLAviary.py:307-319); the same for the terminal row and the (reset) observation
   float* orow = io.obs + n * Wd;
   float* trow = (do_reset && io.terminal_obs) ? io.terminal_obs + n * Wd : nullptr;
-  for (int k = 0; k < L - 1; ++k) {
-    int slot = head + 1 + k;
-    slot -= slot >= L ? L : 0;
-    const float* src = v.ring + ridx(n, slot, L, A);
-    for (int j = 0; j < A; ++j) {
-      const float x = src[j];
-      orow[12 + k * A + j] = x;
-      if (trow) trow[12 + k * A + j] = x;
-    }
-  }
   for (int j = 0; j < A; ++j) {
     orow[12 + (L - 1) * A + j] = a[j];
     if (trow) trow[12 + (L - 1) * A + j] = a[j];
