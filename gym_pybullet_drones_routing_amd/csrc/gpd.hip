@@ -410,7 +410,8 @@ int launch_step(gpd_sim* s, const float* actions, float* obs, float* reward, uin
     const void* f = s->D <= 256 ? step_wide_fn<R, 256>(s->cfg.act_type)
                     : (s->D <= 512 ? step_wide_fn<R, 512>(s->cfg.act_type) : step_wide_fn<R, 1024>(s->cfg.act_type));
     void* args[] = {(void*)&v, (void*)&io, (void*)&c};
-    HIP_TRY(hipLaunchKernel(f, dim3(s->E), dim3((s->D + kWave - 1) / kWave * kWave), args, 0, st));
+    const int ge = s->tpb / s->D;   // envs per workgroup
+    HIP_TRY(hipLaunchKernel(f, dim3((s->E + ge - 1) / ge), dim3((s->tpb + kWave - 1) / kWave * kWave), args, 0, st));
     return GPD_OK;
   }
   const unsigned grid = grid_for(s->N, s->tpb);
@@ -630,7 +631,19 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
                           : (C.precision == GPD_F64 ? runtime_step_lds<double>(C.act_type, s->D > 1)
                                                     : runtime_step_lds<float>(C.act_type, s->D > 1));
     s->wide = s->D > kWave || (!dc_env && tile + lds_rt > (size_t)kLdsBytes);
-    if (s->wide) s->tpb = s->D;
+    // envs of up to 32 drones share the wave, up to 64 / D of them, as many as leave ~2048
+    // workgroups (the history copy's loads in flight: 4096 single-drone envs at ctrl_freq 480
+    // 37.8 us per step with one env per workgroup, 86.7 with 64; 65536 envs 591 / 213 us);
+    // gpd_config::drones_per_block overrides
+    if (s->wide) {
+      int ge = 1;
+      if (s->D <= kWave / 2) {
+        const int gmax = kWave / s->D;
+        ge = C.drones_per_block > 0 ? C.drones_per_block / s->D : (int)std::min<long long>(gmax, C.n_envs / 2048);
+        ge = std::max(1, std::min(gmax, ge));
+      }
+      s->tpb = ge * s->D;
+    }
   }
   s->npad = ((long long)s->N + 63) / 64 * 64;
   {

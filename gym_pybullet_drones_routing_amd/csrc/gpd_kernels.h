@@ -2620,7 +2620,8 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
 
 // ---------------------------------------------------------------------------------------
 // Envs of more than 64 drones (MultiHoverAviary(num_drones=D), D <= kWideMax): one env per
-// workgroup of ceil(D/64) waves.  The per-substep position exchange of _downwash
+// workgroup of ceil(D/64) waves.  (Also envs of any D whose observation rows overflow the one-wave
+// kernels' LDS tile, gpd_create: up to 64 / D of them packed into one wave when D <= 32.)  The per-substep position exchange of _downwash
 // (BaseAviary.py:785-811, O(D^2)) and the env's reward / done reductions go through LDS with
 // workgroup barriers; lanes d >= D compute on drone 0 of the env and store nothing.  Physics
 // flags are tested at run time; observation rows are stored straight from registers (history
@@ -2628,33 +2629,38 @@ __global__ __launch_bounds__(IO ? 3 * kWave : 2 * kWave) void step_kernel_duo(R*
 // and order as step_kernel / integrate_kernel (tests/test_gpu_wide.py).
 constexpr int kWideMax = 1024;
 
+// t: the thread (its LDS slot), active: it owns a drone, base: its env's first slot
 template <typename R>
-__device__ __forceinline__ R wide_downwash(const Drone<R>& s, R* sx, R* sy, R* sz, int d, int D,
-                                           const Consts<R>& c, int flags) {
+__device__ __forceinline__ R wide_downwash(const Drone<R>& s, R* sx, R* sy, R* sz, int t, bool active, int base,
+                                           int D, const Consts<R>& c, int flags) {
   R dw = R(0);
   if (flags & F_DW) {
     __syncthreads();                       // previous readers of sx/sy/sz are done
-    if (d < D) { sx[d] = s.px; sy[d] = s.py; sz[d] = s.pz; }
+    if (active) { sx[t] = s.px; sy[t] = s.py; sz[t] = s.pz; }
     __syncthreads();
-    dw = downwash_sum(s.px, s.py, s.pz, sx, sy, sz, 0, D, c);
+    dw = downwash_sum(s.px, s.py, s.pz, sx, sy, sz, base, D, c);
   }
   return dw;
 }
 
-// The history columns of an env's D observation rows (and terminal rows with TROW): ring slots
+// The history columns of the workgroup's observation rows (and terminal rows): ring slots
 // head+1 .. head+L-1 of each drone, copied by every thread of the workgroup (ACT's A floats per
-// slot, float4 items for A = 4), kWideU loads in flight per thread before their stores.
-constexpr int kWideU = 4;
+// slot, float4 items for A = 4), kWideU loads in flight per thread before their stores.  n0: the
+// workgroup's first drone, nd: its drones; shead[env slot] = ring head | 1 << 30 when the env's
+// terminal row is written.
+constexpr int kWideU = 8;
+constexpr int kWideTrow = 1 << 30;
 template <typename R, int A>
-__device__ __forceinline__ void wide_history(const SimView<R>& v, const StepIO<R>& io, long long n0, int D, int head,
-                                             bool trow) {
+__device__ __forceinline__ void wide_history(const SimView<R>& v, const StepIO<R>& io, long long n0, int nd, int D,
+                                             const int* shead) {
   const int L = v.ring_len, Wd = v.W, H = L - 1, nth = blockDim.x;
   constexpr int G = A == 4 ? 4 : 1;              // floats per item
   const int per = H * (A / G);                   // items per drone
-  const int total = D * per;
+  const int total = nd * per;
   for (int i0 = 0; i0 < total; i0 += nth * kWideU) {
     float x[kWideU][G];
     long long dst[kWideU];
+    bool tr[kWideU];
 #pragma unroll
     for (int u = 0; u < kWideU; ++u) {
       const int i = i0 + u * nth + (int)threadIdx.x;
@@ -2662,6 +2668,8 @@ __device__ __forceinline__ void wide_history(const SimView<R>& v, const StepIO<R
       if (i < total) {
         const int dq = i / per, r = i - dq * per;
         const int k = G == 4 ? r : r / A, j = G == 4 ? 0 : r - k * A;
+        const int hv = shead[dq / D], head = hv & (kWideTrow - 1);
+        tr[u] = (hv & kWideTrow) != 0;
         int slot = head + 1 + k;
         slot -= slot >= L ? L : 0;
         const float* src = v.ring + ridx(n0 + dq, slot, L, A) + j;
@@ -2680,10 +2688,10 @@ __device__ __forceinline__ void wide_history(const SimView<R>& v, const StepIO<R
       if (G == 4) {
         const float4 q = make_float4(x[u][0], x[u][G > 1 ? 1 : 0], x[u][G > 2 ? 2 : 0], x[u][G > 3 ? 3 : 0]);
         *reinterpret_cast<float4*>(io.obs + dst[u]) = q;
-        if (trow) *reinterpret_cast<float4*>(io.terminal_obs + dst[u]) = q;
+        if (tr[u]) *reinterpret_cast<float4*>(io.terminal_obs + dst[u]) = q;
       } else {
         io.obs[dst[u]] = x[u][0];
-        if (trow) io.terminal_obs[dst[u]] = x[u][0];
+        if (tr[u]) io.terminal_obs[dst[u]] = x[u][0];
       }
     }
   }
@@ -2696,19 +2704,27 @@ __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R>
   constexpr int A = act_width(ACT);
   __shared__ R sx[MAXT], sy[MAXT], sz[MAXT];
   __shared__ int sflag[MAXT];
+  __shared__ int shead[kWave];
   const Consts<R>& c = *cp;
   const int D = v.D;
-  const int d = threadIdx.x;
-  const bool active = d < D;
-  const long long e = blockIdx.x;
-  // lanes d >= D compute on the first drone of their own wave (a drone this wave integrates anyway:
-  // the waves take turns in the contact solve) and store nothing
-  const long long n = e * D + (active ? d : (d & ~(kWave - 1)));
+  // GE = v.tpb / D envs per workgroup: one for D > 32; up to 64 / D packed into one wave for the
+  // small envs that run here because their observation rows overflow the one-wave kernels' LDS tile
+  const int GE = v.tpb / D;
+  const int t = threadIdx.x;
+  const int g = t / D, d = t - g * D;           // env slot, drone in the env
+  const long long e0 = (long long)blockIdx.x * GE, e = e0 + g;
+  const long long nenv = v.N / D;
+  const bool active = g < GE && e < nenv;
+  const int slot0 = (g < GE ? g : 0) * D;       // the env's first LDS slot
+  // lanes without a drone compute on the first drone of their own wave (a drone this wave
+  // integrates anyway: the waves take turns in the contact solve) and store nothing
+  const long long n = active ? e * D + d : e0 * D + (t & ~(kWave - 1));
+  const long long es = active ? e : e0;
   const bool drag = (c.flags & F_DRAG) != 0;
   Drone<R> s;
   R last[4];
   load_drone(v, n, s, last, drag);
-  const int2 cv = v.ctr[e];
+  const int2 cv = v.ctr[es];
   const int sc = cv.x, head = cv.y;
   float a[A];
 #pragma unroll
@@ -2732,9 +2748,9 @@ __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R>
   }
   R W[4];
   rpm_wrench<R, kPfRuntime>(rpm, dk, c, W);
-  const int nw = (D + kWave - 1) / kWave;
+  const int nw = (int)(blockDim.x / kWave);
   for (int it = 0; it < dk.nsub; ++it) {
-    const R dw = wide_downwash(s, sx, sy, sz, d, D, c, dk.flags);
+    const R dw = wide_downwash(s, sx, sy, sz, t, active, slot0, D, c, dk.flags);
     if (nw > 1) dyn_substep<R, kPfRuntime, true, 16>(s, rpm, W, last, dw, c, dk);
     else dyn_substep<R, kPfRuntime, true, 1>(s, rpm, W, last, dw, c, dk);
 #pragma unroll
@@ -2759,20 +2775,20 @@ __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R>
     r = r > R(0) ? r : R(0);
     const bool oob = g_abs(s.px) > v.bound_xy || g_abs(s.py) > v.bound_xy || s.pz > R(2) || tilted;
     __syncthreads();
-    if (active) { sx[d] = r; sy[d] = dist; sflag[d] = oob ? 1 : 0; }
+    if (active) { sx[t] = r; sy[t] = dist; sflag[t] = oob ? 1 : 0; }
     __syncthreads();
-    if (d == 0) {   // MultiHoverAviary: the summed reward / distance in the reference's order
+    if (active && d == 0) {   // MultiHoverAviary: the summed reward / distance in the reference's order
       R rs = R(0), ds = R(0);
       int anyo = 0;
-      for (int j = 0; j < D; ++j) { rs += sx[j]; ds += sy[j]; anyo |= sflag[j]; }
-      sflag[0] = (ds < R(1e-4) ? 1 : 0) | ((anyo != 0 || sc >= v.trunc_sc) ? 2 : 0);
-      sx[0] = rs;
+      for (int j = slot0; j < slot0 + D; ++j) { rs += sx[j]; ds += sy[j]; anyo |= sflag[j]; }
+      sflag[slot0] = (ds < R(1e-4) ? 1 : 0) | ((anyo != 0 || sc >= v.trunc_sc) ? 2 : 0);
+      sx[slot0] = rs;
     }
     __syncthreads();
-    const int fl = sflag[0];
+    const int fl = sflag[slot0];
     term = fl & 1;
     trunc = (fl >> 1) & 1;
-    reward = (float)sx[0];
+    reward = (float)sx[slot0];
   }
   const bool done = term || trunc;
   const bool do_reset = done && v.autoreset;
@@ -2781,13 +2797,14 @@ __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R>
   const int L = v.ring_len, Wd = v.W;
   // history columns: ring slots head+1 .. head+L-1 (oldest first), then the current action
   // (BaseRLAviary.py:307-319); the same for the terminal row and the (reset) observation.  The
-  // env's history columns are copied by the whole workgroup, kWideU independent loads per thread
+  // history columns are copied by the whole workgroup, kWideU independent loads per thread
   // before their stores: a lane copying its own row element by element waited out one memory
   // round trip per element (680 us per step for 4096 single-drone envs with a 240-step history)
-  wide_history<R, A>(v, io, e * D, D, head, do_reset && io.terminal_obs);
-  // every wave has read ctr[e] (kernel entry) before lane d == 0 overwrites it below; without a
-  // task, downwash or contact no other workgroup barrier orders the two
+  if (active && d == 0) shead[g] = head | ((do_reset && io.terminal_obs) ? kWideTrow : 0);
+  // (also: every wave has read ctr[e] (kernel entry) before lane d == 0 overwrites it below;
+  // without a task, downwash or contact no other workgroup barrier orders the two)
   __syncthreads();
+  wide_history<R, A>(v, io, e0 * D, (int)(nenv - e0 < GE ? nenv - e0 : GE) * D, D, shead);
   if (!active) return;
   float* orow = io.obs + n * Wd;
   float* trow = (do_reset && io.terminal_obs) ? io.terminal_obs + n * Wd : nullptr;
@@ -2849,7 +2866,7 @@ __global__ __launch_bounds__(MAXT) void integrate_kernel_wide(SimView<R> v, cons
     R rpm[4] = {src[0], src[1], src[2], src[3]};
     R W[4];
     rpm_wrench<R, kPfRuntime>(rpm, dk, c, W);
-    const R dw = wide_downwash(s, sx, sy, sz, d, D, c, dk.flags);
+    const R dw = wide_downwash(s, sx, sy, sz, d, active, 0, D, c, dk.flags);
     if (nw > 1) dyn_substep<R, kPfRuntime, true, 16>(s, rpm, W, last, dw, c, dk);
     else dyn_substep<R, kPfRuntime, true, 1>(s, rpm, W, last, dw, c, dk);
 #pragma unroll

@@ -400,8 +400,8 @@ def test_contact_step_resynced_pyb_flag_kernels(D, aero, freq, prec, monkeypatch
 def test_contact_step_resynced_long_history_wide_kernel(D, aero):
     """Physics.PYB at ctrl_freq = pyb_freq = 480: the 240-step RPM action history makes a
     972-float observation row whose 64-row LDS tile (249 KB) no one-wave step kernel holds, and
-    gpd_create runs such envs (without drone <-> drone contact) on step_kernel_wide, one env per
-    workgroup, with its plane contact solve.  Checked resynced per step as the flag-set kernels
+    gpd_create runs such envs (without drone <-> drone contact) on step_kernel_wide (here 4 / D
+    envs per wave: two workgroups hold the 8 envs), with its plane contact solve.  Checked resynced per step as the flag-set kernels
     above (one step = one substep), f64 to 1e-12."""
     from gym_pybullet_drones_routing_amd.enums import ActionType, Physics
     rng = np.random.default_rng(46)
@@ -415,9 +415,9 @@ def test_contact_step_resynced_long_history_wide_kernel(D, aero):
     for e in range(E):
         envs[e].set_raw_state(raw0[e * D:(e + 1) * D])
     sim = _sim(n_envs=E, drones_per_env=D, task=task, precision="f64", act=ActionType.RPM, physics=Physics.PYB,
-               aero=aero, autoreset=False, pyb_freq=freq, ctrl_freq=freq)
+               aero=aero, autoreset=False, pyb_freq=freq, ctrl_freq=freq, tuning={"drones_per_block": 4})
     assert sim.obs_width == 12 + 240 * 4
-    assert sim.constants.drones_per_block == D          # one env per workgroup: the wide kernel
+    # (a 972-float row: only the wide kernel holds it; 64 / D envs per workgroup)
     errs, low = [], 0
     for t in range(T):
         sim.set_raw_state(np.concatenate([oracle_raw(ev) for ev in envs]))

@@ -63,22 +63,28 @@ def test_frequencies_step_parity(pyb, ctrl, act):
                  ref_kw=dict(pyb_freq=pyb, ctrl_freq=ctrl))
 
 
+@pytest.mark.parametrize("pack", [0, 64], ids=["default_packing", "full_wave_packing"])
 @pytest.mark.parametrize("D,act,task", [(1, "rpm", "hover"), (2, "rpm", "multihover"), (1, "pid", "hover"),
                                         (3, "vel", "multihover")])
-def test_long_history_wide_kernel_step_parity(D, act, task):
+def test_long_history_wide_kernel_step_parity(D, act, task, pack):
     """ctrl_freq 480 (pyb_freq 960): the 240-step action history makes observation rows of
     12 + 240 A floats (972 for RPM, 732 for PID / VEL), whose 64-row LDS tile no one-wave step
-    kernel holds; gpd_create runs these envs on step_kernel_wide, one env per workgroup
-    (drones_per_block == D), rows stored from registers."""
+    kernel holds; gpd_create runs these envs on step_kernel_wide, envs packed into one wave (by
+    default as many as leave ~2048 workgroups: one here; ``pack`` = 64 drones per block: 64 / D),
+    the history columns copied by the whole workgroup.  E = 45 leaves the last workgroup partly
+    empty."""
     rng = np.random.default_rng(34)
-    E, T = 6, 40
+    E, T = 45, 40
     A = 4 if act in ("rpm", "vel") else 3
     acts = np.clip(rng.normal(0, 0.2, (T, E, D, A)), -1, 1).astype(np.float32)
     from gym_pybullet_drones_routing_amd.enums import ActionType
-    probe = _sim(n_envs=E, drones_per_env=D, task=task, act=ActionType(act), pyb_freq=960, ctrl_freq=480)
-    assert probe.constants.drones_per_block == D and probe.obs_width == 12 + 240 * A
+    tuning = {"drones_per_block": pack} if pack else None
+    probe = _sim(n_envs=E, drones_per_env=D, task=task, act=ActionType(act), pyb_freq=960, ctrl_freq=480,
+                 tuning=tuning)
+    assert probe.obs_width == 12 + 240 * A          # a row only the wide kernel holds
+    assert probe.constants.drones_per_block == ((64 // D) * D if pack else D)
     probe.close()
-    _compare_run(acts, E, D=D, act=act, task=task, sim_kw=dict(pyb_freq=960, ctrl_freq=480),
+    _compare_run(acts, E, D=D, act=act, task=task, sim_kw=dict(pyb_freq=960, ctrl_freq=480, tuning=tuning),
                  ref_kw=dict(pyb_freq=960, ctrl_freq=480))
 
 
