@@ -367,14 +367,14 @@ inline unsigned grid_for(long long n, int tpb) { return (unsigned)((n + tpb - 1)
 inline size_t real_size(const gpd_sim* s) { return s->prec == GPD_F64 ? sizeof(double) : sizeof(float); }
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-template <typename R, int MAXT>
+template <typename R, int MAXT, bool DC = false>
 const void* step_wide_fn(int act) {
   switch (act) {
-    case GPD_ACT_RPM: return (const void*)step_kernel_wide<R, ACT_RPM, MAXT>;
-    case GPD_ACT_ONE_D_RPM: return (const void*)step_kernel_wide<R, ACT_ONE_D_RPM, MAXT>;
-    case GPD_ACT_PID: return (const void*)step_kernel_wide<R, ACT_PID, MAXT>;
-    case GPD_ACT_VEL: return (const void*)step_kernel_wide<R, ACT_VEL, MAXT>;
-    default: return (const void*)step_kernel_wide<R, ACT_ONE_D_PID, MAXT>;
+    case GPD_ACT_RPM: return (const void*)step_kernel_wide<R, ACT_RPM, MAXT, DC>;
+    case GPD_ACT_ONE_D_RPM: return (const void*)step_kernel_wide<R, ACT_ONE_D_RPM, MAXT, DC>;
+    case GPD_ACT_PID: return (const void*)step_kernel_wide<R, ACT_PID, MAXT, DC>;
+    case GPD_ACT_VEL: return (const void*)step_kernel_wide<R, ACT_VEL, MAXT, DC>;
+    default: return (const void*)step_kernel_wide<R, ACT_ONE_D_PID, MAXT, DC>;
   }
 }
 template <typename R, int MAXT>
@@ -407,7 +407,10 @@ int launch_step(gpd_sim* s, const float* actions, float* obs, float* reward, uin
   const SimView<R> v = make_view<R>(s);
   const Consts<R>* c = (const Consts<R>*)s->d_consts;
   if (s->wide) {
-    const void* f = s->D <= 256 ? step_wide_fn<R, 256>(s->cfg.act_type)
+    // drone <-> drone contact: the one-wave instantiation with the contact solve (D <= 64)
+    const bool dc = s->dcP > 0;
+    const void* f = dc ? step_wide_fn<R, kWave, true>(s->cfg.act_type)
+                    : s->D <= 256 ? step_wide_fn<R, 256>(s->cfg.act_type)
                     : (s->D <= 512 ? step_wide_fn<R, 512>(s->cfg.act_type) : step_wide_fn<R, 1024>(s->cfg.act_type));
     void* args[] = {(void*)&v, (void*)&io, (void*)&c};
     const int ge = s->tpb / s->D;   // envs per workgroup
@@ -435,7 +438,7 @@ int launch_integrate(gpd_sim* s, const void* rpm, int n_sub, void* traj, hipStre
   const bool plain = s->cfg.physics_flags == 0;
   const R* r = (const R*)rpm;
   R* tr = (R*)traj;
-  if (s->wide) {
+  if (s->wide && s->D > kWave) {   // (long-history envs of <= 64 drones: the one-wave kernels, no tile)
     const void* fw = s->D <= 256 ? integrate_wide_fn<R, 256>(tr != nullptr)
                      : (s->D <= 512 ? integrate_wide_fn<R, 512>(tr != nullptr) : integrate_wide_fn<R, 1024>(tr != nullptr));
     void* args[] = {(void*)&v, (void*)&c, (void*)&r, (void*)&n_sub, (void*)&tr};
@@ -622,15 +625,14 @@ int gpd_create(const gpd_drone_params* params, const gpd_config* cfg, gpd_sim** 
     s->tpb = want;
     // envs of more than 64 drones: one env per multi-wave workgroup (step_kernel_wide).  Also an
     // observation row too long for the one-wave kernels (their LDS tile of 64 rows beside the
-    // run-time-flag kernel's static LDS: a long action history, e.g. RPM actions at ctrl_freq 480)
-    // when the env has no drone <-> drone contact, which only the one-wave kernels solve: the wide
-    // kernel stores the rows from registers, one env per workgroup
-    const bool dc_env = (C.physics_flags & GPD_F_BULLET) && s->D > 1 && !(C.physics_flags & GPD_F_NO_DRONE_CONTACT);
+    // run-time-flag kernel's static LDS: a long action history, e.g. RPM actions at ctrl_freq 480):
+    // the wide kernel copies the history columns without a tile (with the drone <-> drone contact
+    // in its one-wave instantiation, D <= 64)
     const size_t tile = (size_t)step_tile_bytes(s->A, s->ring_len);
     const size_t lds_rt = s->D > kWave ? 0
                           : (C.precision == GPD_F64 ? runtime_step_lds<double>(C.act_type, s->D > 1)
                                                     : runtime_step_lds<float>(C.act_type, s->D > 1));
-    s->wide = s->D > kWave || (!dc_env && tile + lds_rt > (size_t)kLdsBytes);
+    s->wide = s->D > kWave || tile + lds_rt > (size_t)kLdsBytes;
     // envs of up to 32 drones share the wave, up to 64 / D of them, as many as leave ~2048
     // workgroups (the history copy's loads in flight: 4096 single-drone envs at ctrl_freq 480
     // 37.8 us per step with one env per workgroup, 86.7 with 64; 65536 envs 591 / 213 us);

@@ -2699,7 +2699,10 @@ __device__ __forceinline__ void wide_history(const SimView<R>& v, const StepIO<R
 
 // MAXT: the workgroup size bound the instantiation is compiled for (256 / 512 / 1024 threads:
 // the register budget per lane halves with each doubling, 1024 spills to scratch).
-template <typename R, int ACT, int MAXT>
+// DC: the drone <-> drone contact (DcHookT, the one-wave kernels' solve): one-wave workgroups
+// (D <= 64, MAXT = 64) of a long-history PYB* env; its DcLds is static LDS, so only these
+// instantiations carry it.
+template <typename R, int ACT, int MAXT, bool DC = false>
 __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R> io, const Consts<R>* __restrict__ cp) {
   constexpr int A = act_width(ACT);
   __shared__ R sx[MAXT], sy[MAXT], sz[MAXT];
@@ -2720,6 +2723,8 @@ __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R>
   // integrates anyway: the waves take turns in the contact solve) and store nothing
   const long long n = active ? e * D + d : e0 * D + (t & ~(kWave - 1));
   const long long es = active ? e : e0;
+  const int nact = (int)(nenv - e0 < GE ? nenv - e0 : GE) * D;   // drones owned by this workgroup
+  const DcPairs dcp = DC ? dc_pairs_for(v, t, nact) : dc_pairs_none();
   const bool drag = (c.flags & F_DRAG) != 0;
   Drone<R> s;
   R last[4];
@@ -2751,7 +2756,8 @@ __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R>
   const int nw = (int)(blockDim.x / kWave);
   for (int it = 0; it < dk.nsub; ++it) {
     const R dw = wide_downwash(s, sx, sy, sz, t, active, slot0, D, c, dk.flags);
-    if (nw > 1) dyn_substep<R, kPfRuntime, true, 16>(s, rpm, W, last, dw, c, dk);
+    if (DC) dyn_substep<R, kPfRuntime, true, 1, DcHookT<false>>(s, rpm, W, last, dw, c, dk, DcHookT<false>{t, dcp});
+    else if (nw > 1) dyn_substep<R, kPfRuntime, true, 16>(s, rpm, W, last, dw, c, dk);
     else dyn_substep<R, kPfRuntime, true, 1>(s, rpm, W, last, dw, c, dk);
 #pragma unroll
     for (int k = 0; k < 4; ++k) last[k] = rpm[k];   // self.last_clipped_action = clipped_action  :372
@@ -2804,7 +2810,7 @@ __global__ __launch_bounds__(MAXT) void step_kernel_wide(SimView<R> v, StepIO<R>
   // (also: every wave has read ctr[e] (kernel entry) before lane d == 0 overwrites it below;
   // without a task, downwash or contact no other workgroup barrier orders the two)
   __syncthreads();
-  wide_history<R, A>(v, io, e0 * D, (int)(nenv - e0 < GE ? nenv - e0 : GE) * D, D, shead);
+  wide_history<R, A>(v, io, e0 * D, nact, D, shead);
   if (!active) return;
   float* orow = io.obs + n * Wd;
   float* trow = (do_reset && io.terminal_obs) ? io.terminal_obs + n * Wd : nullptr;

@@ -237,7 +237,7 @@ def test_drone_contact_counts_beyond_d():
         assert len(cons) > D
 
 
-@pytest.mark.parametrize("case", ["2", "3", "4", "4-ground", "8"])
+@pytest.mark.parametrize("case", ["2", "3", "4", "4-ground", "8", "2-480hz", "4-480hz", "4-ground-480hz", "8-480hz"])
 def test_drone_contact_step_kernel_resynced(case):
     """The Physics.PYB flag-set step kernel (MultiHoverAviary's default physics; the parked call, one
     copy of the substep, the history DMA after the substeps) for D = 2, 3, 4, for a stack on the plane
@@ -246,26 +246,33 @@ def test_drone_contact_step_kernel_resynced(case):
     _downwash (BaseAviary.py:785-811) scales as (r_prop / 4 dz)^2 for ANY drone above another within
     10 m, so drones in contact (|dz| < 2.5 cm) or at rounding-level height differences push each
     other with tens to 1e30 N, and a control step amplifies rounding differences beyond any gate
-    (tests/tools/dbg_dc8.py: the same stacks without the pair contact fail the same way)."""
+    (tests/tools/dbg_dc8.py: the same stacks without the pair contact fail the same way).
+    The -480hz cases run ctrl_freq 480 / pyb_freq 960: the 240-step action history's rows overflow
+    the one-wave kernels' LDS tile, and the envs step on step_kernel_wide's one-wave instantiation
+    with the same contact solve (48 steps of 2 substeps at 960 Hz: 0.1 s, the collisions included)."""
     from gym_pybullet_drones_routing_amd.enums import ActionType
     D = int(case.split("-")[0])
+    hz = case.endswith("480hz")
+    freq = dict(pyb_freq=960, ctrl_freq=480) if hz else {}
     physics, aero, lo, hi, tuning = _pyb(), (), -0.2, 0.2, None
-    if case == "4-ground":
+    if case.startswith("4-ground"):
         raw0, lo, hi = _ground_stack(), -1.0, -0.9      # ~0.95 hover RPM: the stacks stay down
-    elif case == "8":     # eight stacks in one 64-drone block: 224 pairs, several 64-pair passes
+    elif D == 8:          # eight stacks in one 64-drone block: 224 pairs, several 64-pair passes
         raw0 = np.concatenate([_cube(np.random.default_rng(3 + k)) for k in range(8)])
         tuning = {"drones_per_block": 64}
     else:
         raw0 = {2: _scenarios, 3: _triples, 4: _pile6}[D]()
     n = raw0.shape[0]
-    env = RefAviary(num_drones=n, task="none", integrator="bullet", act="rpm", drones_per_env=D, aero=aero)
+    env = RefAviary(num_drones=n, task="none", integrator="bullet", act="rpm", drones_per_env=D, aero=aero, **freq)
     env.set_raw_state(raw0)
     sim = _sim(n_envs=n // D, drones_per_env=D, task="none", precision="f64", physics=physics, act=ActionType.RPM,
-               tuning=tuning)
+               tuning=tuning, **freq)
+    if hz:
+        assert sim.obs_width == 12 + 240 * 4     # a row only the wide kernel holds
     sim.reset()
     rng = np.random.default_rng(5)
     errs = []
-    for t in range(12):
+    for t in range(48 if hz else 12):
         a = rng.uniform(lo, hi, (n, 4)).astype(np.float32)
         sim.set_raw_state(oracle_raw(env))
         sim.step(torch.from_numpy(a.reshape(n // D, D, 4)).cuda())
